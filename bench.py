@@ -1,0 +1,165 @@
+"""Benchmark of the hot path: per-layer pairwise distance + Vietoris-Rips
+persistence H0-H2 (BASELINE.json metric "layers/sec ... at 1/2/4/8 MI355X").
+
+A step = one pass of the hot path over one batch: the reference's 32-layer
+sweep (debug_tda_pipeline.py:92-150) of 48-point clouds (configs[1] per layer:
+48 points, D=3, H0/H1/H2), inputs already resident in HBM, diagrams returned
+to the host.  Multi-GPU: one process per GPU (torchrun), every rank runs its
+own 32-layer batch (weak scaling) and the per-layer summary records are
+all-gathered over RCCL each step.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def algo_bytes_per_layer(n: int, d: int, maxdim: int) -> int:
+    """B = 4ND + 4C(N,2) + sum_{k=1..maxdim} 12 C(N,k+1)."""
+    return 4 * n * d + 4 * math.comb(n, 2) + sum(12 * math.comb(n, k + 1) for k in range(1, maxdim + 1))
+
+
+def workload(name: str, layers: int):
+    pkg = importlib.import_module("tda-multimodal_amd")
+    syn = pkg.synthetic
+    if name == "sweep48":
+        return syn.sweep48(layers), 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2"
+    if name == "grid144":
+        return syn.sweep144(layers), 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2"
+    if name == "torus1024":
+        return syn.torus(1024)[None].repeat(layers, 0), 1, "S1xS1 torus N=1024 (configs[3]), D=3, H0-H1"
+    raise ValueError(name)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--workload", default="sweep48", choices=["sweep48", "grid144", "torus1024"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import numpy as np
+    import torch
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    pkg = importlib.import_module("tda-multimodal_amd")
+    if pkg.lib().tda_device_ok(local) != 1:
+        raise RuntimeError("no gfx950 device")
+
+    L = args.layers if args.workload != "torus1024" else max(1, min(args.layers, 1))
+    X_host, maxdim, wl_desc = workload(args.workload, L)
+    n, d = X_host.shape[1], X_host.shape[2]
+    X = torch.from_numpy(X_host).to(dev)  # resident in HBM before the timed region
+    torch.cuda.synchronize()
+
+    stage_acc: dict = {}
+
+    def step(record: bool):
+        res, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, stage_times=True)
+        if record:
+            for name, ms in info["stages"]:
+                stage_acc.setdefault(name, []).append(ms)
+        if world > 1:
+            lo = rank * L
+            recs = [pkg.layer_record(lo + i, r.dgms) for i, r in enumerate(res)]
+            pkg.distributed.gather_records(recs, L * world, device=dev)
+        return res
+
+    for _ in range(args.warmup):
+        step(False)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    value = L * world * args.steps / el
+    stage_avg = {k: float(np.mean(v)) for k, v in stage_acc.items()}
+    kern = {k: v for k, v in stage_avg.items() if k.startswith("k_")}
+    dom = max(kern, key=kern.get)
+    bpl = algo_bytes_per_layer(n, d, maxdim)
+    achieved = bpl * L / (kern[dom] * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        traffic = pmc.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import oracle
+
+        oracle.lib()
+        reps, t_cpu = 0, 0.0
+        tc0 = time.perf_counter()
+        while t_cpu < args.cpu_seconds and reps < 1000:
+            oracle.rips_batch_f32(X_host, maxdim)
+            reps += 1
+            t_cpu = time.perf_counter() - tc0
+        cpu = {"value": L * reps / t_cpu, "unit": "layers/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} x the same {L}-layer batch ({wl_desc}), oracle/rips_oracle.c single thread, "
+                         f"{t_cpu:.1f} s"}
+
+    if rank == 0:
+        out = {
+            "metric": "layers/sec (pairwise-dist + VR persistence H0-H2) at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "layers/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
+            "config": {"workload": wl_desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d),
+                       "maxdim": maxdim, "parallelism": f"layers sharded, {world} process(es) x 1 GPU, RCCL all-gather of records"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algo_bytes_per_layer": bpl, "layers_per_launch": L, "kernel_avg_ms": kern[dom]},
+            "stages_ms": {k: round(v, 5) for k, v in stage_avg.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,118 @@
+/*
+ * tda_rips.h -- C ABI of the MI355X (gfx950) Vietoris-Rips persistence engine.
+ *
+ * Drop-in boundary for the reference's hot path: the third-party call
+ *     result = ripser(cloud_low_dim, maxdim=MAX_DIM); dgms = result['dgms']
+ * at debug_tda_pipeline.py:109-110, analyze_tda_over_layers.py:76 and
+ * experiments/adversarial_compositional_binding/analyze_adversarial_tda.py:100.
+ * The reference binds ripser's C++ core through Cython (package `ripser`,
+ * unpinned, README.md:28; not vendored in the reference) with two entry points,
+ *     rips_dm(float* D, int N, int modulus, int dim_max, float threshold,
+ *             int do_cocycles)                                   [upstream]
+ *     rips_dm_sparse(int* I, int* J, float* V, int NEdges, int N, int modulus,
+ *             int dim_max, float threshold, int do_cocycles)     [upstream]
+ * returning {births_and_deaths_by_dim, cocycles_by_dim, num_edges}.
+ * `tda_rips_dm` below replaces `rips_dm` one-for-one (same argument meaning:
+ * D is the condensed strict-upper-triangle distance vector in row-major (i<j)
+ * order, exactly what ripser.py passes after `dm[I > J]`).  `tda_rips_batch`
+ * is the layer-loop entry (point clouds in, distance + persistence on the
+ * GPU) that the reference's per-layer loop (debug_tda_pipeline.py:92-150)
+ * calls once per sweep instead of once per layer.
+ *
+ * Conventions
+ *  - All functions return 0 on success or a negative TDA_E* code; the message
+ *    is kept in thread-local storage and returned by tda_last_error().
+ *  - Inputs are never owned by the library.  Results are library-owned until
+ *    tda_rips_free().
+ *  - coeff/modulus must be 2 (the reference never overrides ripser's default);
+ *    other values return TDA_E_UNSUPPORTED.  do_cocycles != 0 likewise.
+ *  - No torch types cross this boundary: plain pointers and sizes.
+ */
+#ifndef TDA_RIPS_H
+#define TDA_RIPS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TDA_RIPS_ABI_VERSION 1
+
+/* error codes */
+#define TDA_OK 0
+#define TDA_E_INVALID (-1)      /* bad shape / argument / non-finite input   */
+#define TDA_E_UNSUPPORTED (-2)  /* coeff != 2, cocycles, maxdim > 2, ...     */
+#define TDA_E_HIP (-3)          /* HIP runtime error (message has details)   */
+#define TDA_E_CAPACITY (-4)     /* a device work buffer overflowed           */
+#define TDA_E_NODEVICE (-5)     /* no gfx950 device visible                  */
+
+/* dtype of the point-cloud input */
+#define TDA_F32 0
+#define TDA_F64 1
+
+/* arguments of one batched call: L layers of N points in R^D */
+typedef struct tda_rips_args {
+    const void *x;      /* (L, N, D) row-major points, or (L, N, N) distances   */
+    int32_t dtype;      /* TDA_F32 | TDA_F64                                    */
+    int32_t x_on_device;/* 1: x is a device pointer on `device`; 0: host memory */
+    int64_t L, N, D;    /* D ignored when is_dist                               */
+    int32_t is_dist;    /* 1: x holds (L, N, N) distance matrices (upper used)  */
+    int32_t maxdim;     /* 0, 1 or 2                                            */
+    float thresh;       /* +inf -> enclosing radius (ripser.py default)         */
+    int32_t modulus;    /* must be 2                                            */
+    int32_t device;     /* HIP device ordinal                                   */
+    void *stream;       /* hipStream_t or NULL (library stream)                 */
+    int32_t want_dist;  /* 1: also return the (L, N, N) f32 distance matrices   */
+    int32_t flags;      /* TDA_FLAG_* bits (0 = none)                           */
+} tda_rips_args;
+
+/* per (layer, dim) emitted persistence pairs, in the reference's emission
+ * order: H0 = Kruskal order of the finite deaths then one [0, inf) per
+ * component; Hk = columns in (birth desc, birth-simplex index asc) order.
+ * birth_idx/death_idx are combinatorial-number-system simplex indices
+ * (H0: birth vertex, death edge; essential classes: death_idx = -1). */
+typedef struct tda_rips_result {
+    int64_t L, maxdim, N;
+    const int64_t *count;     /* [L][maxdim+1] pairs per layer and dim          */
+    const int64_t *offset;    /* [L][maxdim+1] offset into the pair arrays      */
+    const float *birth;       /* [total] */
+    const float *death;       /* [total] (+inf for essential)                   */
+    const int64_t *birth_idx; /* [total] */
+    const int64_t *death_idx; /* [total] */
+    const float *thresh;      /* [L] threshold actually used (enclosing radius) */
+    const int64_t *num_edges; /* [L] condensed distances <= thresh              */
+    const uint64_t *checksum; /* [L][maxdim+1] order-free hash of ALL pairs     */
+    const int64_t *n_all_pairs;/* [L][maxdim+1] all pairs incl. zero-persistence*/
+    const int64_t *n_columns; /* [L][maxdim+1] columns considered per dim       */
+    const int64_t *n_residual;/* [L][maxdim+1] columns needing reduction        */
+    const float *dist;        /* [L][N][N] when want_dist, else NULL            */
+    double device_ms;         /* device time of the call (HIP events)           */
+    /* per-stage device times, filled when args.flags & TDA_FLAG_STAGE_TIMES:
+     * stage_ms[i] is the time between consecutive stream events bracketing
+     * stage i (one kernel, memset or copy), named by stage_name[i]. */
+    int32_t n_stages;
+    const char *const *stage_name;
+    const float *stage_ms;
+} tda_rips_result;
+
+#define TDA_FLAG_STAGE_TIMES 1
+
+/* Batched point clouds (or distance matrices) -> persistence diagrams. */
+int tda_rips_batch(const tda_rips_args *args, tda_rips_result **out);
+
+/* One condensed distance vector (length N(N-1)/2, i<j row-major) -> diagrams.
+ * Replaces ripser.py's rips_dm (see header comment). */
+int tda_rips_dm(const float *D, int64_t n_entries, int32_t modulus, int32_t dim_max, float threshold,
+                int32_t do_cocycles, tda_rips_result **out);
+
+void tda_rips_free(tda_rips_result *r);
+const char *tda_last_error(void);
+int tda_version(void);
+/* 1 if a gfx950 device is visible, 0 otherwise (never aborts). */
+int tda_device_ok(int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TDA_RIPS_H */

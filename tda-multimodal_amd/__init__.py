@@ -1,0 +1,29 @@
+"""tda-multimodal_amd: MI355X-native drop-in for the reference's ripser hot path.
+
+Import with ``importlib.import_module("tda-multimodal_amd")`` (the directory
+name carries a hyphen); the package registers itself as ``tda_multimodal_amd``
+too.  Product path = libtda_rips.so (HIP, gfx950) via the C ABI in
+include/tda_rips.h; no CPU fallback.
+"""
+import sys as _sys
+
+from . import distributed, synthetic  # noqa: F401
+from ._lib import EXPORTS, LIB_PATH, build, lib  # noqa: F401
+from .pipeline import get_max_persistence, get_persistence, layer_record, run_sweep  # noqa: F401
+from .ripser import LayerResult, persistence_pairs, ripser, ripser_batch, rips_dm  # noqa: F401
+
+_sys.modules.setdefault("tda_multimodal_amd", _sys.modules[__name__])
+
+__all__ = [
+    "ripser",
+    "ripser_batch",
+    "rips_dm",
+    "persistence_pairs",
+    "LayerResult",
+    "get_persistence",
+    "get_max_persistence",
+    "layer_record",
+    "run_sweep",
+    "build",
+    "lib",
+]

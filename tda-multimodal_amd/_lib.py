@@ -1,0 +1,133 @@
+"""ctypes binding of the C ABI in include/tda_rips.h (libtda_rips.so, gfx950).
+
+The product path has exactly one implementation: the HIP library.  If it is
+missing or no gfx950 device is visible, calls raise -- there is no CPU
+fallback (the CPU restatement under oracle/ is test infrastructure only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD_DIR = os.path.join(_HERE, "_build")
+LIB_PATH = os.path.join(BUILD_DIR, "libtda_rips.so")
+CSRC = os.path.join(_HERE, "csrc")
+INCLUDE = os.path.join(os.path.dirname(_HERE), "include")
+
+TDA_F32, TDA_F64 = 0, 1
+ERRORS = {-1: ValueError, -2: NotImplementedError, -3: RuntimeError, -4: RuntimeError, -5: RuntimeError}
+
+
+class RipsArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("dtype", ctypes.c_int32),
+        ("x_on_device", ctypes.c_int32),
+        ("L", ctypes.c_int64),
+        ("N", ctypes.c_int64),
+        ("D", ctypes.c_int64),
+        ("is_dist", ctypes.c_int32),
+        ("maxdim", ctypes.c_int32),
+        ("thresh", ctypes.c_float),
+        ("modulus", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("stream", ctypes.c_void_p),
+        ("want_dist", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+    ]
+
+
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_f32p = ctypes.POINTER(ctypes.c_float)
+
+
+class RipsResult(ctypes.Structure):
+    _fields_ = [
+        ("L", ctypes.c_int64),
+        ("maxdim", ctypes.c_int64),
+        ("N", ctypes.c_int64),
+        ("count", _i64p),
+        ("offset", _i64p),
+        ("birth", _f32p),
+        ("death", _f32p),
+        ("birth_idx", _i64p),
+        ("death_idx", _i64p),
+        ("thresh", _f32p),
+        ("num_edges", _i64p),
+        ("checksum", ctypes.POINTER(ctypes.c_uint64)),
+        ("n_all_pairs", _i64p),
+        ("n_columns", _i64p),
+        ("n_residual", _i64p),
+        ("dist", _f32p),
+        ("device_ms", ctypes.c_double),
+        ("n_stages", ctypes.c_int32),
+        ("stage_name", ctypes.POINTER(ctypes.c_char_p)),
+        ("stage_ms", _f32p),
+    ]
+
+
+TDA_FLAG_STAGE_TIMES = 1
+
+
+# every symbol declared in include/tda_rips.h
+EXPORTS = ("tda_rips_batch", "tda_rips_dm", "tda_rips_free", "tda_last_error", "tda_version", "tda_device_ok")
+
+_lib = None
+
+
+def build(verbose: bool = False) -> str:
+    """Compile csrc/rips.hip for gfx950 into _build/libtda_rips.so (in-tree)."""
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    src = os.path.join(CSRC, "rips.hip")
+    cmd = [
+        os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"),
+        "--offload-arch=gfx950",
+        "-O3",
+        "-std=c++17",
+        "-shared",
+        "-fPIC",
+        "-I" + INCLUDE,
+        "-o",
+        LIB_PATH + ".tmp",
+        src,
+    ]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + r.stderr[-4000:])
+    if verbose and r.stderr:
+        print(r.stderr, file=sys.stderr)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+def lib():
+    """Load libtda_rips.so; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP extension not built: {LIB_PATH} is missing (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    L.tda_rips_batch.argtypes = [ctypes.POINTER(RipsArgs), ctypes.POINTER(ctypes.POINTER(RipsResult))]
+    L.tda_rips_batch.restype = ctypes.c_int
+    L.tda_rips_dm.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_int32,
+                              ctypes.POINTER(ctypes.POINTER(RipsResult))]
+    L.tda_rips_dm.restype = ctypes.c_int
+    L.tda_rips_free.argtypes = [ctypes.POINTER(RipsResult)]
+    L.tda_rips_free.restype = None
+    L.tda_last_error.argtypes = []
+    L.tda_last_error.restype = ctypes.c_char_p
+    L.tda_version.restype = ctypes.c_int
+    L.tda_device_ok.argtypes = [ctypes.c_int32]
+    L.tda_device_ok.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().tda_last_error().decode(errors="replace")
+        raise ERRORS.get(rc, RuntimeError)(msg)

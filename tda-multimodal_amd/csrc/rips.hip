@@ -1,0 +1,606 @@
+// rips.hip -- host orchestration + C ABI (include/tda_rips.h) of the MI355X
+// Vietoris-Rips persistence engine.  Built for gfx950 only:
+//     hipcc --offload-arch=gfx950 -O3 -shared -fPIC rips.hip -o libtda_rips.so
+//
+// One call processes a batch of L layers (the reference's 32-layer sweep,
+// debug_tda_pipeline.py:92-150) with ~8 + 3*maxdim kernel launches on one
+// stream and a single host synchronisation at the end.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tda_rips.h"
+#include "rips_kernels.h"
+
+using namespace tda;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPC(x)                                                                                   \
+    do {                                                                                          \
+        hipError_t e_ = (x);                                                                      \
+        if (e_ != hipSuccess) return fail(TDA_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+inline uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+inline int ilog2(uint64_t x) {
+    int r = 0;
+    while ((1ull << (r + 1)) <= x) ++r;
+    return r;
+}
+
+constexpr uint64_t kRCapMax = 1ull << 22;    // residual columns per layer and dim
+constexpr uint64_t kPCapMax = 1ull << 16;    // emitted pairs per layer and dim (H>=1)
+constexpr int kLdsMax = 160 * 1024;
+constexpr int kDistLdsMaxN = 96;             // stage the distance matrix in LDS below this
+constexpr uint32_t kWCapLds = 4096, kVCapLds = 1024;
+
+// ------------------------------------------------------------------ plan
+struct Plan {
+    int64_t L = 0, N = 0, D = 0;
+    int maxdim = 0, dtype = 0, is_dist = 0;
+    uint64_t ncand[4] = {0}, piv_words[4] = {0}, rcap[4] = {0}, pcap[4] = {0};
+    uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, sstride = 0;
+    bool lds_mode = false;
+    int dist_in_lds = 0;
+    // byte offsets in the device workspace
+    size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wd = 0, o_wp = 0, o_wl = 0, o_pairs[4] = {0}, o_h0s = 0,
+           o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
+    size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
+};
+
+int make_plan(Plan& p) {
+    const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
+    p.mst_words = (binom(N, 2) + 31) / 32 + 1;
+    for (int d = 1; d <= p.maxdim; ++d) {
+        p.ncand[d] = binom(N, d + 1);
+        p.piv_words[d] = (binom(N, d + 2) + 31) / 32 + 1;
+        p.rcap[d] = std::max<uint64_t>(1, std::min(p.ncand[d], kRCapMax));
+        p.pcap[d] = std::max<uint64_t>(16, std::min(p.ncand[d], kPCapMax));
+        p.max_rcap = std::max(p.max_rcap, p.rcap[d]);
+    }
+    p.pcap[0] = N + 1;
+    p.max_rcap = std::max<uint64_t>(p.max_rcap, 1);
+    p.rmap_stride = next_pow2(2 * p.max_rcap + 16);
+    p.vpool_cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 16, 4 * p.max_rcap), 1ull << 24);
+    p.lds_mode = p.N <= kDistLdsMaxN;
+    p.dist_in_lds = p.lds_mode ? 1 : 0;
+    p.wcap_g = next_pow2(std::max<uint64_t>(1ull << 15, 64 * N));
+    uint64_t maxp = 16;
+    for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
+    p.sstride = 3 * maxp;
+
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t r = o;
+        o = align_up(o + bytes, 256);
+        return r;
+    };
+    const size_t esz = p.dtype == TDA_F64 ? 8 : 4;
+    p.o_x = take(L * N * (p.is_dist ? N : (uint64_t)std::max<int64_t>(p.D, 1)) * esz);
+    p.o_dist = take(L * N * N * 4);
+    p.memset_lo = o;
+    p.o_stats = take(L * sizeof(LayerStats));
+    p.o_mst = take(L * p.mst_words * 4);
+    for (int d = 1; d <= p.maxdim; ++d) p.o_piv[d] = take(L * p.piv_words[d] * 4);
+    p.memset_hi = o;
+    for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
+    p.o_tmp = take(L * p.max_rcap * 8);
+    if (p.maxdim >= 1) {
+        p.o_rmk = take(L * p.rmap_stride * 8);
+        p.o_rmv = take(L * p.rmap_stride * 4);
+        p.o_voff = take(L * p.max_rcap * 4);
+        p.o_vlen = take(L * p.max_rcap * 4);
+        p.o_vpool = take(L * p.vpool_cap * 8);
+        if (!p.lds_mode) {
+            p.o_wk = take(L * p.wcap_g * 8);
+            p.o_wd = take(L * p.wcap_g * 4);
+            p.o_wp = take(L * p.wcap_g * 4);
+            p.o_wl = take(L * p.wcap_g * 4);
+        }
+    }
+    for (int d = 0; d <= p.maxdim; ++d) p.o_pairs[d] = take(L * p.pcap[d] * sizeof(Pair));
+    p.o_h0s = take(L * 2 * N * 8 + 64);
+    p.o_fk = take(L * 2 * p.sstride * 8);
+    p.o_fv = take(L * 2 * p.sstride * 4);
+    p.o_pptr = take(4 * sizeof(void*));
+    p.o_pcap = take(4 * 8);
+    p.o_outoff = take(L * 4 * 8);
+    p.total = o;
+    return 0;
+}
+
+// ------------------------------------------------------------------ workspace
+struct Workspace {
+    int device = -1;
+    bool init = false;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    char* dbuf = nullptr;
+    size_t dcap = 0;
+    OutPair* hout = nullptr;  // host-mapped
+    OutPair* hout_dev = nullptr;
+    size_t hout_cap = 0;      // in pairs
+    LayerStats* hstats = nullptr;  // pinned
+    size_t hstats_cap = 0;
+    int64_t* houtoff = nullptr;
+    size_t houtoff_cap = 0;
+    std::vector<hipEvent_t> stage_ev;  // stage-time events (TDA_FLAG_STAGE_TIMES)
+    std::mutex mu;
+};
+
+// records an event after each stage when stage timing is on
+struct StageTimer {
+    Workspace& w;
+    hipStream_t s;
+    bool on;
+    std::vector<const char*> names;
+    int mark(const char* name) {
+        if (!on) return 0;
+        size_t i = names.size() + 1;
+        while (w.stage_ev.size() <= i) {
+            hipEvent_t e;
+            HIPC(hipEventCreate(&e));
+            w.stage_ev.push_back(e);
+        }
+        HIPC(hipEventRecord(w.stage_ev[i], s));
+        names.push_back(name);
+        return 0;
+    }
+    int begin() {
+        if (!on) return 0;
+        while (w.stage_ev.empty()) {
+            hipEvent_t e;
+            HIPC(hipEventCreate(&e));
+            w.stage_ev.push_back(e);
+        }
+        HIPC(hipEventRecord(w.stage_ev[0], s));
+        return 0;
+    }
+};
+
+std::mutex g_ws_mu;
+std::vector<Workspace*> g_ws;
+
+Workspace* get_ws(int dev) {
+    std::lock_guard<std::mutex> g(g_ws_mu);
+    for (auto* w : g_ws)
+        if (w->device == dev) return w;
+    auto* w = new Workspace();
+    w->device = dev;
+    g_ws.push_back(w);
+    return w;
+}
+
+int ws_prepare(Workspace& w, const Plan& p) {
+    if (!w.init) {
+        HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+        HIPC(hipEventCreate(&w.ev0));
+        HIPC(hipEventCreate(&w.ev1));
+        w.init = true;
+    }
+    if (w.dcap < p.total) {
+        if (w.dbuf) HIPC(hipFree(w.dbuf));
+        w.dbuf = nullptr;
+        size_t cap = std::max<size_t>(p.total, w.dcap + w.dcap / 2);
+        HIPC(hipMalloc(&w.dbuf, cap));
+        w.dcap = cap;
+    }
+    if (w.hstats_cap < (size_t)p.L) {
+        if (w.hstats) HIPC(hipHostFree(w.hstats));
+        HIPC(hipHostMalloc((void**)&w.hstats, sizeof(LayerStats) * p.L, hipHostMallocDefault));
+        w.hstats_cap = p.L;
+    }
+    if (w.houtoff_cap < (size_t)p.L * 4) {
+        if (w.houtoff) HIPC(hipHostFree(w.houtoff));
+        HIPC(hipHostMalloc((void**)&w.houtoff, sizeof(int64_t) * p.L * 4, hipHostMallocDefault));
+        w.houtoff_cap = p.L * 4;
+    }
+    size_t want = std::max<size_t>(1 << 16, (size_t)p.L * 256);
+    if (w.hout_cap < want) {
+        if (w.hout) HIPC(hipHostFree(w.hout));
+        HIPC(hipHostMalloc((void**)&w.hout, sizeof(OutPair) * want, hipHostMallocMapped));
+        HIPC(hipHostGetDevicePointer((void**)&w.hout_dev, w.hout, 0));
+        w.hout_cap = want;
+    }
+    return 0;
+}
+
+int grow_hout(Workspace& w, size_t need) {
+    if (w.hout) HIPC(hipHostFree(w.hout));
+    w.hout = nullptr;
+    size_t cap = std::max(need, 2 * w.hout_cap);
+    HIPC(hipHostMalloc((void**)&w.hout, sizeof(OutPair) * cap, hipHostMallocMapped));
+    HIPC(hipHostGetDevicePointer((void**)&w.hout_dev, w.hout, 0));
+    w.hout_cap = cap;
+    return 0;
+}
+
+bool g_attr_done[64] = {false};
+int set_lds_attrs(int dev) {
+    if (dev < 64 && g_attr_done[dev]) return 0;
+    HIPC(hipFuncSetAttribute((const void*)k_h0, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_sort_resid, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_finalize, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    if (dev < 64) g_attr_done[dev] = true;
+    return 0;
+}
+
+// result owned by the library
+struct ResultImpl {
+    tda_rips_result pub;
+    std::vector<int64_t> count, offset, num_edges, n_all, n_cols, n_res, bidx, didx;
+    std::vector<float> birth, death, thresh, dist, stage_ms;
+    std::vector<const char*> stage_name;
+    std::vector<uint64_t> checksum;
+};
+
+std::string err_flags(int e) {
+    std::string s;
+    if (e & ERR_RESID_CAP) s += " residual-column-capacity";
+    if (e & ERR_PAIR_CAP) s += " pair-capacity";
+    if (e & ERR_WORK_CAP) s += " working-column-capacity";
+    if (e & ERR_VPOOL_CAP) s += " reduction-pool-capacity";
+    if (e & ERR_OUT_CAP) s += " output-capacity";
+    return s;
+}
+
+// ------------------------------------------------------------------ pipeline
+// input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
+int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out) {
+    Plan p;
+    p.L = a.L;
+    p.N = a.N;
+    p.D = a.D;
+    p.maxdim = a.maxdim;
+    p.dtype = a.dtype;
+    p.is_dist = input_kind != 0;
+    make_plan(p);
+    const int dev = a.device;
+    HIPC(hipSetDevice(dev));
+    Workspace& w = *get_ws(dev);
+    std::lock_guard<std::mutex> guard(w.mu);
+    if (int rc = ws_prepare(w, p)) return rc;
+    if (int rc = set_lds_attrs(dev)) return rc;
+    hipStream_t s = a.stream ? (hipStream_t)a.stream : w.stream;
+    char* B = w.dbuf;
+    const int n = (int)p.N, L = (int)p.L;
+    float* dist = (float*)(B + p.o_dist);
+    LayerStats* stats = (LayerStats*)(B + p.o_stats);
+
+    StageTimer tm{w, s, (a.flags & TDA_FLAG_STAGE_TIMES) != 0, {}};
+#define MARK(name) \
+    do {           \
+        if (int rc_ = tm.mark(name)) return rc_; \
+    } while (0)
+    HIPC(hipEventRecord(w.ev0, s));
+    if (int rc = tm.begin()) return rc;
+    HIPC(hipMemsetAsync(B + p.memset_lo, 0, p.memset_hi - p.memset_lo, s));
+    MARK("memset");
+
+    // ---- distances
+    const size_t esz = p.dtype == TDA_F64 ? 8 : 4;
+    if (input_kind == 0) {
+        const void* x = host_or_dev;
+        if (!a.x_on_device) {
+            HIPC(hipMemcpyAsync(B + p.o_x, x, (size_t)L * n * p.D * esz, hipMemcpyHostToDevice, s));
+            x = B + p.o_x;
+        }
+        dim3 grid((n + 15) / 16, (n + 15) / 16, L);
+        if (p.dtype == TDA_F64)
+            hipLaunchKernelGGL(k_distance<double>, grid, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist);
+        else
+            hipLaunchKernelGGL(k_distance<float>, grid, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist);
+    } else if (input_kind == 1) {
+        const void* x = host_or_dev;
+        if (!a.x_on_device) {
+            HIPC(hipMemcpyAsync(B + p.o_x, x, (size_t)L * n * n * esz, hipMemcpyHostToDevice, s));
+            x = B + p.o_x;
+        }
+        unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
+        if (p.dtype == TDA_F64)
+            hipLaunchKernelGGL(k_square_dist<double>, dim3(gx, L), dim3(256), 0, s, (const double*)x, n, dist);
+        else
+            hipLaunchKernelGGL(k_square_dist<float>, dim3(gx, L), dim3(256), 0, s, (const float*)x, n, dist);
+    } else {
+        const uint64_t ne = binom((uint64_t)n, 2);
+        const void* x = host_or_dev;
+        if (ne) {
+            HIPC(hipMemcpyAsync(B + p.o_x, x, ne * 4, hipMemcpyHostToDevice, s));
+        }
+        unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
+        hipLaunchKernelGGL(k_square_from_condensed, dim3(gx), dim3(256), 0, s, (const float*)(B + p.o_x), n, dist);
+    }
+    HIPC(hipGetLastError());
+    MARK(input_kind == 0 ? "k_distance" : "k_square_dist");
+
+    // ---- H0
+    {
+        int T = n <= 64 ? 64 : (n <= 256 ? 256 : 1024);
+        size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
+        base = align_up(base, 16);
+        size_t avail = kLdsMax - base;
+        uint64_t ch = 1;
+        while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
+        size_t lds = base + ch * 8;
+        hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
+                           (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
+        HIPC(hipGetLastError());
+        MARK("k_h0");
+    }
+
+    // ---- H1 .. Hmaxdim
+    ReduceBufs rb;
+    rb.rmap_keys = (uint64_t*)(B + p.o_rmk);
+    rb.rmap_vals = (uint32_t*)(B + p.o_rmv);
+    rb.rmap_stride = p.rmap_stride;
+    rb.voff = (uint32_t*)(B + p.o_voff);
+    rb.vlen = (uint32_t*)(B + p.o_vlen);
+    rb.vpool = (uint64_t*)(B + p.o_vpool);
+    rb.vpool_cap = p.vpool_cap;
+    rb.wkeys = (uint64_t*)(B + p.o_wk);
+    rb.wdiam = (float*)(B + p.o_wd);
+    rb.wpar = (uint32_t*)(B + p.o_wp);
+    rb.wlist = (uint32_t*)(B + p.o_wl);
+    rb.wcap = p.wcap_g;
+    for (int d = 1; d <= p.maxdim; ++d) {
+        DimBufs db;
+        db.cleared = d == 1 ? (const uint32_t*)(B + p.o_mst) : (const uint32_t*)(B + p.o_piv[d - 1]);
+        db.cleared_words = d == 1 ? p.mst_words : p.piv_words[d - 1];
+        db.pivbits = (uint32_t*)(B + p.o_piv[d]);
+        db.piv_words = p.piv_words[d];
+        db.resid = (uint64_t*)(B + p.o_resid[d]);
+        db.rcap = p.rcap[d];
+        db.ncand = p.ncand[d];
+        Pair* pairs = (Pair*)(B + p.o_pairs[d]);
+        uint64_t blocks = (p.ncand[d] + 255) / 256;
+        unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, 4096 / L)));
+        if (d == 1)
+            hipLaunchKernelGGL(k_apparent<1>, dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
+        else
+            hipLaunchKernelGGL(k_apparent<2>, dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
+        HIPC(hipGetLastError());
+        MARK(d == 1 ? "k_apparent<1>" : "k_apparent<2>");
+        hipLaunchKernelGGL(k_sort_resid, dim3(L), dim3(1024), 16384 * 8, s, stats, d, db.resid, db.rcap, (uint64_t*)(B + p.o_tmp),
+                           rb.rmap_keys, rb.rmap_stride, 14);
+        HIPC(hipGetLastError());
+        MARK(d == 1 ? "k_sort_resid<1>" : "k_sort_resid<2>");
+        size_t lds = 16;
+        if (p.lds_mode) {
+            lds += (size_t)kWCapLds * 20 + (size_t)kVCapLds * 20;
+            if (p.dist_in_lds) lds += (size_t)n * n * 4;
+        } else {
+            lds += (size_t)kVCapLds * 20;
+        }
+        if (p.lds_mode) {
+            if (d == 1)
+                hipLaunchKernelGGL((k_reduce<1, true>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], kWCapLds,
+                                   kVCapLds, p.dist_in_lds);
+            else
+                hipLaunchKernelGGL((k_reduce<2, true>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], kWCapLds,
+                                   kVCapLds, p.dist_in_lds);
+        } else {
+            if (d == 1)
+                hipLaunchKernelGGL((k_reduce<1, false>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], 0u,
+                                   kVCapLds, 0);
+            else
+                hipLaunchKernelGGL((k_reduce<2, false>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], 0u,
+                                   kVCapLds, 0);
+        }
+        HIPC(hipGetLastError());
+        MARK(d == 1 ? "k_reduce<1>" : "k_reduce<2>");
+    }
+
+    // ---- emission order + compaction into host-mapped memory
+    Pair* hptr[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t hpcap[4] = {0, 0, 0, 0};
+    for (int d = 0; d <= p.maxdim; ++d) {
+        hptr[d] = (Pair*)(B + p.o_pairs[d]);
+        hpcap[d] = p.pcap[d];
+    }
+    HIPC(hipMemcpyAsync(B + p.o_pptr, hptr, sizeof(hptr), hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(B + p.o_pcap, hpcap, sizeof(hpcap), hipMemcpyHostToDevice, s));
+    if (p.maxdim >= 1) {
+        hipLaunchKernelGGL(k_finalize, dim3(L), dim3(1024), 8192 * 12, s, stats, p.maxdim, (Pair* const*)(B + p.o_pptr),
+                           (const uint64_t*)(B + p.o_pcap), (uint64_t*)(B + p.o_fk), (uint32_t*)(B + p.o_fv), p.sstride, 13);
+        HIPC(hipGetLastError());
+        MARK("k_finalize");
+    }
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
+                       (const uint64_t*)(B + p.o_pcap), (int64_t*)(B + p.o_outoff), w.hout_dev, (uint64_t)w.hout_cap);
+    HIPC(hipGetLastError());
+    MARK("k_compact");
+    HIPC(hipMemcpyAsync(w.hstats, stats, sizeof(LayerStats) * L, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(w.houtoff, B + p.o_outoff, sizeof(int64_t) * L * (p.maxdim + 1), hipMemcpyDeviceToHost, s));
+    MARK("d2h_stats");
+    HIPC(hipEventRecord(w.ev1, s));
+    HIPC(hipStreamSynchronize(s));
+
+    int errs = 0;
+    for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
+    if (errs == ERR_OUT_CAP) {
+        size_t need = 0;
+        for (int l = 0; l < L; ++l)
+            for (int d = 0; d <= p.maxdim; ++d) need += (size_t)std::min<uint64_t>(w.hstats[l].count[d], p.pcap[d]);
+        if (int rc = grow_hout(w, need + 16)) return rc;
+        for (int l = 0; l < L; ++l) w.hstats[l].err = 0;
+        HIPC(hipMemcpyAsync(stats, w.hstats, sizeof(LayerStats) * L, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
+                           (const uint64_t*)(B + p.o_pcap), (int64_t*)(B + p.o_outoff), w.hout_dev, (uint64_t)w.hout_cap);
+        HIPC(hipGetLastError());
+        HIPC(hipMemcpyAsync(w.hstats, stats, sizeof(LayerStats) * L, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(w.houtoff, B + p.o_outoff, sizeof(int64_t) * L * (p.maxdim + 1), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        errs = 0;
+        for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
+    }
+    if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
+
+    // ---- result
+    auto* R = new ResultImpl();
+    const int nd = p.maxdim + 1;
+    R->count.resize((size_t)L * nd);
+    R->offset.resize((size_t)L * nd);
+    R->checksum.resize((size_t)L * nd);
+    R->n_all.resize((size_t)L * nd);
+    R->n_cols.resize((size_t)L * nd);
+    R->n_res.resize((size_t)L * nd);
+    R->thresh.resize(L);
+    R->num_edges.resize(L);
+    size_t total = 0;
+    for (int l = 0; l < L; ++l) {
+        const LayerStats& st = w.hstats[l];
+        R->thresh[l] = st.thresh;
+        R->num_edges[l] = st.num_edges;
+        for (int d = 0; d < nd; ++d) {
+            int64_t c = std::min<int64_t>(st.count[d], (int64_t)p.pcap[d]);
+            R->count[l * nd + d] = c;
+            R->offset[l * nd + d] = w.houtoff[l * nd + d];
+            R->checksum[l * nd + d] = st.checksum[d];
+            R->n_all[l * nd + d] = st.all_pairs[d];
+            R->n_cols[l * nd + d] = st.n_columns[d];
+            R->n_res[l * nd + d] = st.n_residual[d];
+            total += (size_t)c;
+        }
+    }
+    R->birth.resize(total);
+    R->death.resize(total);
+    R->bidx.resize(total);
+    R->didx.resize(total);
+    for (size_t e = 0; e < total; ++e) {
+        R->birth[e] = w.hout[e].birth;
+        R->death[e] = w.hout[e].death;
+        R->bidx[e] = w.hout[e].birth_idx;
+        R->didx[e] = w.hout[e].death_idx;
+    }
+    if (a.want_dist) {
+        R->dist.resize((size_t)L * n * n);
+        HIPC(hipMemcpy(R->dist.data(), dist, sizeof(float) * L * n * n, hipMemcpyDeviceToHost));
+    }
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, w.ev0, w.ev1);
+    tda_rips_result& o = R->pub;
+    o.L = L;
+    o.maxdim = p.maxdim;
+    o.N = n;
+    o.count = R->count.data();
+    o.offset = R->offset.data();
+    o.birth = R->birth.data();
+    o.death = R->death.data();
+    o.birth_idx = R->bidx.data();
+    o.death_idx = R->didx.data();
+    o.thresh = R->thresh.data();
+    o.num_edges = R->num_edges.data();
+    o.checksum = R->checksum.data();
+    o.n_all_pairs = R->n_all.data();
+    o.n_columns = R->n_cols.data();
+    o.n_residual = R->n_res.data();
+    o.dist = a.want_dist ? R->dist.data() : nullptr;
+    o.device_ms = ms;
+    for (size_t i = 0; i < tm.names.size(); ++i) {
+        float t = 0.0f;
+        (void)hipEventElapsedTime(&t, w.stage_ev[i], w.stage_ev[i + 1]);
+        R->stage_ms.push_back(t);
+        R->stage_name.push_back(tm.names[i]);
+    }
+    o.n_stages = (int32_t)tm.names.size();
+    o.stage_name = R->stage_name.data();
+    o.stage_ms = R->stage_ms.data();
+    *out = &R->pub;
+    return 0;
+}
+
+int validate(const tda_rips_args* a) {
+    if (!a) return fail(TDA_E_INVALID, "args is NULL");
+    if (!a->x && a->L * a->N > 0) return fail(TDA_E_INVALID, "x is NULL");
+    if (a->L < 1) return fail(TDA_E_INVALID, "L must be >= 1");
+    if (a->N < 1) return fail(TDA_E_INVALID, "N must be >= 1");
+    if (!a->is_dist && a->D < 1) return fail(TDA_E_INVALID, "D must be >= 1");
+    if (a->dtype != TDA_F32 && a->dtype != TDA_F64) return fail(TDA_E_INVALID, "dtype must be TDA_F32 or TDA_F64");
+    if (a->modulus != 2) return fail(TDA_E_UNSUPPORTED, "only coeff=2 (Z/2) is supported");
+    if (a->maxdim < 0 || a->maxdim > 2) return fail(TDA_E_UNSUPPORTED, "maxdim must be 0, 1 or 2");
+    if (a->N > 8192) return fail(TDA_E_UNSUPPORTED, "N > 8192 is not supported");
+    if (a->maxdim == 2 && a->N > 2900) return fail(TDA_E_UNSUPPORTED, "maxdim=2 requires N <= 2900");
+    if (std::isnan(a->thresh)) return fail(TDA_E_INVALID, "thresh is NaN");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tda_rips_batch(const tda_rips_args* args, tda_rips_result** out) {
+    if (!out) return fail(TDA_E_INVALID, "out is NULL");
+    *out = nullptr;
+    if (int rc = validate(args)) return rc;
+    if (!tda_device_ok(args->device)) return fail(TDA_E_NODEVICE, "no gfx950 device at ordinal " + std::to_string(args->device));
+    return run_pipeline(*args, args->is_dist ? 1 : 0, args->x, out);
+}
+
+int tda_rips_dm(const float* D, int64_t n_entries, int32_t modulus, int32_t dim_max, float threshold, int32_t do_cocycles,
+                tda_rips_result** out) {
+    if (!out) return fail(TDA_E_INVALID, "out is NULL");
+    *out = nullptr;
+    if (do_cocycles) return fail(TDA_E_UNSUPPORTED, "do_cocycles is not supported");
+    if (n_entries < 0 || (n_entries > 0 && !D)) return fail(TDA_E_INVALID, "bad condensed distance vector");
+    // ripser.cpp compressed_distance_matrix: rows = (1 + sqrt(1 + 8 n)) / 2
+    int64_t N = (int64_t)((1.0 + std::sqrt(1.0 + 8.0 * (double)n_entries)) / 2.0);
+    if (N * (N - 1) / 2 != n_entries) return fail(TDA_E_INVALID, "n_entries is not N(N-1)/2");
+    tda_rips_args a;
+    std::memset(&a, 0, sizeof(a));
+    a.x = D;
+    a.dtype = TDA_F32;
+    a.L = 1;
+    a.N = N;
+    a.D = 0;
+    a.is_dist = 1;
+    a.maxdim = dim_max;
+    a.thresh = threshold;
+    a.modulus = modulus;
+    a.device = 0;
+    if (int rc = validate(&a)) return rc;
+    if (!tda_device_ok(0)) return fail(TDA_E_NODEVICE, "no gfx950 device");
+    return run_pipeline(a, 2, D, out);
+}
+
+void tda_rips_free(tda_rips_result* r) {
+    if (!r) return;
+    delete reinterpret_cast<ResultImpl*>(r);  // pub is the first member
+}
+
+const char* tda_last_error(void) { return g_err.c_str(); }
+
+int tda_version(void) { return TDA_RIPS_ABI_VERSION; }
+
+int tda_device_ok(int32_t device) {
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || device < 0 || device >= cnt) return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,169 @@
+// rips_device.h -- device-side helpers shared by the gfx950 Vietoris-Rips kernels.
+//
+// Simplex indexing follows the combinatorial number system that the
+// reference's `ripser` core uses [upstream ripser.cpp: get_simplex_vertices /
+// simplex_coboundary_enumerator]: a k-simplex with vertices v_k > ... > v_0
+// has index sum_i C(v_i, i+1).  Filtration order (the total order that fixes
+// every persistence pair) is (diameter asc, index desc); column order is its
+// reverse (diameter desc, index asc).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tda {
+
+constexpr uint64_t kEmpty64 = 0xFFFFFFFFFFFFFFFFull;
+
+// ---------------------------------------------------------------- binomials
+__host__ __device__ __forceinline__ uint64_t binom(uint64_t n, int k) {
+    switch (k) {
+        case 0: return 1;
+        case 1: return n;
+        case 2: return n < 2 ? 0 : n * (n - 1) / 2;
+        case 3: return n < 3 ? 0 : n * (n - 1) * (n - 2) / 6;
+        case 4: return n < 4 ? 0 : (n * (n - 1) / 2) * ((n - 2) * (n - 3) / 2) / 6;
+        case 5: return n < 5 ? 0 : ((n * (n - 1) / 2) * ((n - 2) * (n - 3) / 2) / 6) * (n - 4) / 5;
+        default: return 0;
+    }
+}
+
+// largest v in [k-1, top] with C(v, k) <= idx
+__device__ __forceinline__ int max_vertex(uint64_t idx, int k, int top) {
+    if (k == 1) return (int)(idx < (uint64_t)top ? idx : (uint64_t)top);
+    double g;
+    double x = (double)idx;
+    if (k == 2)
+        g = 0.5 * (1.0 + sqrt(1.0 + 8.0 * x));
+    else if (k == 3)
+        g = cbrt(6.0 * x) + 1.0;
+    else
+        g = sqrt(sqrt(24.0 * x)) + 1.5;
+    int v = (int)g;
+    if (v > top) v = top;
+    if (v < k - 1) v = k - 1;
+    while (v > k - 1 && binom((uint64_t)v, k) > idx) --v;
+    while (v < top && binom((uint64_t)(v + 1), k) <= idx) ++v;
+    return v;
+}
+
+// index -> vertices, descending (vs[0] largest), DIM+1 vertices
+template <int DIM>
+__device__ __forceinline__ void decode(uint64_t idx, int n, int (&vs)[DIM + 1]) {
+    int top = n - 1;
+#pragma unroll
+    for (int k = DIM + 1; k >= 1; --k) {
+        int v = max_vertex(idx, k, top);
+        vs[DIM + 1 - k] = v;
+        idx -= binom((uint64_t)v, k);
+        top = v - 1;
+    }
+}
+
+template <int DIM>
+__device__ __forceinline__ uint64_t encode(const int (&vs)[DIM + 1]) {
+    uint64_t idx = 0;
+#pragma unroll
+    for (int i = 0; i <= DIM; ++i) idx += binom((uint64_t)vs[i], DIM + 1 - i);
+    return idx;
+}
+
+// index of sigma u {v} (v not in sigma), sigma descending
+template <int DIM>
+__device__ __forceinline__ uint64_t cofacet_index(const int (&vs)[DIM + 1], int v) {
+    uint64_t idx = 0;
+    int pos = DIM + 2;  // binomial order of the next vertex written (descending)
+    bool placed = false;
+#pragma unroll
+    for (int i = 0; i <= DIM; ++i) {
+        if (!placed && v > vs[i]) {
+            idx += binom((uint64_t)v, pos--);
+            placed = true;
+        }
+        idx += binom((uint64_t)vs[i], pos--);
+    }
+    if (!placed) idx += binom((uint64_t)v, 1);
+    return idx;
+}
+
+template <int DIM>
+__device__ __forceinline__ float simplex_diam(const float* __restrict__ D, int n, const int (&vs)[DIM + 1]) {
+    float d = 0.0f;
+#pragma unroll
+    for (int i = 0; i <= DIM; ++i)
+#pragma unroll
+        for (int j = i + 1; j <= DIM; ++j) d = fmaxf(d, D[(size_t)vs[i] * n + vs[j]]);
+    return d;
+}
+
+// ---------------------------------------------------------------- hashing
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+// order-free pair hash; the CPU checker under oracle/ uses the same definition
+__host__ __device__ __forceinline__ uint64_t pair_hash(uint64_t s, uint64_t t) {
+    return mix64(s * 0x9E3779B97F4A7C15ull ^ mix64(t + 0x632BE59BD9B4E019ull));
+}
+
+// column key: ascending u64 order == column order (diam desc, idx asc)
+__host__ __device__ __forceinline__ uint64_t col_key(float diam, uint64_t idx) {
+    uint32_t b = __float_as_uint(diam + 0.0f);
+    return ((uint64_t)(0xFFFFFFFFu - b) << 32) | (idx & 0xFFFFFFFFull);
+}
+__host__ __device__ __forceinline__ float key_diam(uint64_t key) { return __uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32)); }
+__host__ __device__ __forceinline__ uint64_t key_idx(uint64_t key) { return key & 0xFFFFFFFFull; }
+// edge key in filtration order (diam asc, idx desc) for the H0 spanning forest
+__host__ __device__ __forceinline__ uint64_t filt_key(float diam, uint64_t idx) {
+    return ((uint64_t)__float_as_uint(diam + 0.0f) << 32) | (0xFFFFFFFFull - (idx & 0xFFFFFFFFull));
+}
+
+// ---------------------------------------------------------------- wave ops
+__device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    uint32_t lo = __shfl_xor((unsigned)(uint32_t)v, m, 64);
+    uint32_t hi = __shfl_xor((unsigned)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    uint32_t lo = __shfl((unsigned)(uint32_t)v, src, 64);
+    uint32_t hi = __shfl((unsigned)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t o = shfl_xor_u64(v, m);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint64_t o = shfl_xor_u64(v, m);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint32_t o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+}  // namespace tda

@@ -1,0 +1,223 @@
+"""ripser-compatible Python entry points backed by the MI355X HIP library.
+
+Drop-in for the reference's hot path ``result = ripser(cloud_low_dim,
+maxdim=MAX_DIM); dgms = result['dgms']`` (debug_tda_pipeline.py:109-110,
+analyze_tda_over_layers.py:76, analyze_adversarial_tda.py:100).  The signature
+and the result dict mirror the third-party ``ripser.ripser`` (scikit-tda
+ripser.py, unpinned at README.md:28) [upstream]:
+
+    ripser(X, maxdim=1, thresh=np.inf, coeff=2, distance_matrix=False,
+           do_cocycles=False, metric='euclidean', n_perm=None)
+    -> {'dgms', 'cocycles', 'num_edges', 'dperm2all', 'idx_perm', 'r_cover'}
+
+``ripser_batch`` is the layer-loop entry: (L, N, D) clouds (numpy, or a torch
+tensor already resident on the GPU) -> one result per layer, one library call.
+"""
+from __future__ import annotations
+
+import ctypes
+import warnings
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+
+
+@dataclass
+class LayerResult:
+    """Persistence of one layer (all arrays on the host)."""
+
+    dgms: list
+    birth_idx: list
+    death_idx: list
+    num_edges: int
+    thresh: float
+    checksum: list = field(default_factory=list)
+    n_all_pairs: list = field(default_factory=list)
+    n_columns: list = field(default_factory=list)
+    n_residual: list = field(default_factory=list)
+    dist: np.ndarray | None = None
+
+
+def _unpack(res_p, want_dist: bool) -> tuple[list, float]:
+    r = res_p.contents
+    L, md, N = int(r.L), int(r.maxdim), int(r.N)
+    nd = md + 1
+    cnt = np.ctypeslib.as_array(r.count, shape=(L * nd,)).copy()
+    off = np.ctypeslib.as_array(r.offset, shape=(L * nd,)).copy()
+    total = int(cnt.sum())
+    if total:
+        birth = np.ctypeslib.as_array(r.birth, shape=(total,)).astype(np.float64)
+        death = np.ctypeslib.as_array(r.death, shape=(total,)).astype(np.float64)
+        bidx = np.ctypeslib.as_array(r.birth_idx, shape=(total,)).copy()
+        didx = np.ctypeslib.as_array(r.death_idx, shape=(total,)).copy()
+    else:
+        birth = death = np.zeros(0)
+        bidx = didx = np.zeros(0, dtype=np.int64)
+    thr = np.ctypeslib.as_array(r.thresh, shape=(L,)).copy()
+    ne = np.ctypeslib.as_array(r.num_edges, shape=(L,)).copy()
+    cs = np.ctypeslib.as_array(r.checksum, shape=(L * nd,)).copy()
+    na = np.ctypeslib.as_array(r.n_all_pairs, shape=(L * nd,)).copy()
+    nc = np.ctypeslib.as_array(r.n_columns, shape=(L * nd,)).copy()
+    nr = np.ctypeslib.as_array(r.n_residual, shape=(L * nd,)).copy()
+    dist = None
+    if want_dist and bool(r.dist):
+        dist = np.ctypeslib.as_array(r.dist, shape=(L, N, N)).copy()
+    out = []
+    for l in range(L):
+        dg, bi, di = [], [], []
+        for d in range(nd):
+            c, o = int(cnt[l * nd + d]), int(off[l * nd + d])
+            dg.append(np.stack([birth[o:o + c], death[o:o + c]], axis=1) if c else np.zeros((0, 2)))
+            bi.append(bidx[o:o + c])
+            di.append(didx[o:o + c])
+        out.append(LayerResult(
+            dgms=dg, birth_idx=bi, death_idx=di, num_edges=int(ne[l]), thresh=float(thr[l]),
+            checksum=[int(x) for x in cs[l * nd:(l + 1) * nd]],
+            n_all_pairs=[int(x) for x in na[l * nd:(l + 1) * nd]],
+            n_columns=[int(x) for x in nc[l * nd:(l + 1) * nd]],
+            n_residual=[int(x) for x in nr[l * nd:(l + 1) * nd]],
+            dist=None if dist is None else dist[l],
+        ))
+    stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(int(r.n_stages))]
+    return out, {"device_ms": float(r.device_ms), "stages": stages}
+
+
+def _call_batch(args: _lib.RipsArgs, want_dist: bool):
+    L = _lib.lib()
+    res = ctypes.POINTER(_lib.RipsResult)()
+    _lib.check(L.tda_rips_batch(ctypes.byref(args), ctypes.byref(res)))
+    try:
+        return _unpack(res, want_dist)
+    finally:
+        L.tda_rips_free(res)
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _check_common(maxdim, coeff, do_cocycles, n_perm, metric):
+    if coeff != 2:
+        raise NotImplementedError("only coeff=2 (Z/2) is implemented (the reference never overrides it)")
+    if do_cocycles:
+        raise NotImplementedError("do_cocycles=True is not implemented")
+    if n_perm is not None:
+        raise NotImplementedError("greedy subsampling (n_perm) is not implemented")
+    if metric != "euclidean":
+        raise NotImplementedError("only metric='euclidean' is implemented")
+    if int(maxdim) != maxdim or maxdim < 0:
+        raise ValueError("maxdim must be a non-negative integer")
+    if maxdim > 2:
+        raise NotImplementedError("maxdim > 2 is not implemented")
+
+
+def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
+                 want_dist: bool = False, return_time: bool = False, stage_times: bool = False):
+    """Persistence of L layers in one call.
+
+    X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
+       numpy array on the host, or a contiguous torch CUDA tensor (consumed in
+       place, ordered on torch's current stream).
+    Returns a list of ``LayerResult``; with return_time also a dict
+    {"device_ms", "stages": [(name, ms), ...]} (stages filled when stage_times,
+    timed with HIP events on the library's stream).
+    """
+    _check_common(maxdim, 2, False, None, "euclidean")
+    a = _lib.RipsArgs()
+    if _is_torch(X) and X.is_cuda:
+        import torch
+
+        if X.dim() != 3:
+            raise ValueError("X must be (L, N, D)")
+        if X.dtype not in (torch.float32, torch.float64):
+            X = X.to(torch.float64)
+        keep = X.contiguous()
+        a.x = keep.data_ptr()
+        a.x_on_device = 1
+        device = keep.device.index if keep.device.index is not None else torch.cuda.current_device()
+        a.stream = torch.cuda.current_stream(keep.device).cuda_stream
+        dtype_is64 = keep.dtype == torch.float64
+    else:
+        if _is_torch(X):
+            X = X.detach().cpu().numpy()
+        X = np.asarray(X)
+        if X.ndim != 3:
+            raise ValueError("X must be (L, N, D)")
+        if X.dtype not in (np.float32, np.float64):
+            X = X.astype(np.float64)
+        keep = np.ascontiguousarray(X)
+        if not np.all(np.isfinite(keep)):
+            raise ValueError("Input contains NaN or infinity.")
+        a.x = keep.ctypes.data
+        a.x_on_device = 0
+        dtype_is64 = keep.dtype == np.float64
+    L, N = int(keep.shape[0]), int(keep.shape[1])
+    if distance_matrix and keep.shape[2] != N:
+        raise ValueError("Distance matrix is not square")
+    a.dtype = _lib.TDA_F64 if dtype_is64 else _lib.TDA_F32
+    a.L, a.N, a.D = L, N, int(keep.shape[2])
+    a.is_dist = 1 if distance_matrix else 0
+    a.maxdim = int(maxdim)
+    a.thresh = float(thresh) if np.isfinite(thresh) else float("inf")
+    a.modulus = 2
+    a.device = int(device)
+    a.want_dist = 1 if want_dist else 0
+    a.flags = _lib.TDA_FLAG_STAGE_TIMES if stage_times else 0
+    out, info = _call_batch(a, want_dist)
+    return (out, info) if return_time else out
+
+
+def ripser(X, maxdim: int = 1, thresh: float = np.inf, coeff: int = 2, distance_matrix: bool = False,
+           do_cocycles: bool = False, metric: str = "euclidean", n_perm=None):
+    """Drop-in for ``ripser.ripser`` (Vietoris-Rips persistence over Z/2).
+
+    Returns the same dict as ripser.py: ``dgms`` (list of (n_k, 2) float64
+    arrays, f32 values widened, ``inf`` for essential classes), ``cocycles``
+    (empty lists), ``num_edges``, ``dperm2all`` (N x N float32 distances),
+    ``idx_perm`` (arange N) and ``r_cover`` (0.0).
+    """
+    _check_common(maxdim, coeff, do_cocycles, n_perm, metric)
+    if hasattr(X, "tocoo"):
+        raise NotImplementedError("sparse distance matrices are not implemented")
+    X = np.asarray(X)
+    if X.ndim != 2:
+        raise ValueError("X must be a 2-D array")
+    if distance_matrix:
+        if X.shape[0] != X.shape[1]:
+            raise ValueError("Distance matrix is not square")
+        if np.any(np.diagonal(X) != 0):
+            raise NotImplementedError("non-zero diagonal (lower-star filtration) is not implemented")
+    elif X.shape[1] > X.shape[0]:
+        warnings.warn("The input point cloud has more columns than rows; did you mean to transpose?")
+    res = ripser_batch(X[None], maxdim=maxdim, thresh=thresh, distance_matrix=distance_matrix, want_dist=True)[0]
+    N = X.shape[0]
+    return {
+        "dgms": res.dgms,
+        "cocycles": [[] for _ in range(maxdim + 1)],
+        "num_edges": res.num_edges,
+        "dperm2all": res.dist,
+        "idx_perm": np.arange(N),
+        "r_cover": 0.0,
+    }
+
+
+def persistence_pairs(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False) -> LayerResult:
+    """Like ``ripser`` but returns the LayerResult with simplex pair indices."""
+    X = np.asarray(X)
+    return ripser_batch(X[None], maxdim=maxdim, thresh=thresh, distance_matrix=distance_matrix, want_dist=True)[0]
+
+
+def rips_dm(D_condensed, maxdim: int = 1, thresh: float = np.inf) -> LayerResult:
+    """Condensed f32 distance vector (i<j row-major) -> LayerResult via the
+    C entry ``tda_rips_dm`` that replaces ripser.py's ``rips_dm``."""
+    D = np.ascontiguousarray(D_condensed, dtype=np.float32)
+    L = _lib.lib()
+    res = ctypes.POINTER(_lib.RipsResult)()
+    thr = float(thresh) if np.isfinite(thresh) else float("inf")
+    _lib.check(L.tda_rips_dm(D.ctypes.data_as(_lib._f32p), D.shape[0], 2, int(maxdim), thr, 0, ctypes.byref(res)))
+    try:
+        return _unpack(res, False)[0][0]
+    finally:
+        L.tda_rips_free(res)

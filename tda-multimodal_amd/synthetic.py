@@ -1,0 +1,59 @@
+"""Synthetic workloads of BASELINE.json configs.
+
+There is no network and no Qwen-VL-Chat checkpoint, so the activation-derived
+clouds are the reference's own committed UMAP outputs
+(tda-output/point_clouds_3d/layer_{l}_cloud.npy, 36 x 3 float32, copied to
+tests/golden/reference_clouds.npz) and generators derived from them.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(_ROOT, "tests", "golden")
+
+
+def reference_clouds() -> np.ndarray:
+    """(32, 36, 3) float32: the exact ripser inputs of the reference run
+    (saved at debug_tda_pipeline.py:106-107, right before :109)."""
+    z = np.load(os.path.join(GOLDEN, "reference_clouds.npz"))
+    return np.stack([z[f"layer_{l}"] for l in range(32)]).astype(np.float32)
+
+
+def layer48(l: int, clouds: np.ndarray | None = None) -> np.ndarray:
+    """C1/C2/C3: 48-point layer = cloud_l[i % 36] + N(0, (0.02 std(cloud_l))^2), seed 1000+l."""
+    c = reference_clouds()[l] if clouds is None else clouds[l]
+    rng = np.random.default_rng(1000 + l)
+    idx = np.arange(48) % 36
+    return (c[idx] + rng.normal(0.0, 0.02 * c.std(), (48, 3))).astype(np.float32)
+
+
+def sweep48(n_layers: int = 32) -> np.ndarray:
+    clouds = reference_clouds()
+    return np.stack([layer48(l % 32, clouds) for l in range(n_layers)])
+
+
+def torus(n: int = 1024, seed: int = 0, R: float = 2.0, r: float = 1.0) -> np.ndarray:
+    """C4: uniform angles on S^1 x S^1 embedded in R^3."""
+    rng = np.random.default_rng(seed)
+    th = rng.uniform(0, 2 * np.pi, n)
+    ph = rng.uniform(0, 2 * np.pi, n)
+    return np.stack([(R + r * np.cos(ph)) * np.cos(th), (R + r * np.cos(ph)) * np.sin(th), r * np.sin(ph)], 1).astype(np.float32)
+
+
+def grid144(l: int) -> np.ndarray:
+    """C5: 12 x 12 torus grid + N(0, 0.02^2) + random rotation, seed l."""
+    rng = np.random.default_rng(l)
+    i, j = np.meshgrid(np.arange(12), np.arange(12), indexing="ij")
+    th = 2 * np.pi * i.ravel() / 12
+    ph = 2 * np.pi * j.ravel() / 12
+    X = np.stack([(2 + np.cos(ph)) * np.cos(th), (2 + np.cos(ph)) * np.sin(th), np.sin(ph)], 1)
+    X = X + rng.normal(0, 0.02, (144, 3))
+    Q, _ = np.linalg.qr(rng.standard_normal((3, 3)))
+    return (X @ Q).astype(np.float32)
+
+
+def sweep144(n_layers: int = 32) -> np.ndarray:
+    return np.stack([grid144(l) for l in range(n_layers)])

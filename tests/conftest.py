@@ -1,0 +1,54 @@
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; runs through the C ABI")
+
+
+def load_pkg():
+    return importlib.import_module("tda-multimodal_amd")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    return load_pkg()
+
+
+@pytest.fixture(scope="session")
+def built_lib(pkg):
+    """Path of libtda_rips.so, built with hipcc if it is not there yet."""
+    if not os.path.exists(pkg.LIB_PATH):
+        pkg.build()
+    return pkg.LIB_PATH
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as o
+
+    o.lib()
+    return o
+
+
+@pytest.fixture(scope="session")
+def ref_clouds():
+    z = np.load(os.path.join(GOLDEN, "reference_clouds.npz"))
+    return np.stack([z[f"layer_{l}"] for l in range(32)])
+
+
+@pytest.fixture(scope="session")
+def summary_stats():
+    import json
+
+    with open(os.path.join(GOLDEN, "summary_stats.json")) as f:
+        return json.load(f)

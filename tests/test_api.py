@@ -1,0 +1,73 @@
+"""CPU tests of the host-side mirror of the reference interface (no GPU)."""
+import numpy as np
+import pytest
+
+
+def test_ripser_signature_errors_match_reference_behaviour(pkg):
+    X = np.random.default_rng(0).standard_normal((10, 3)).astype(np.float32)
+    with pytest.raises(NotImplementedError):
+        pkg.ripser(X, coeff=3)
+    with pytest.raises(NotImplementedError):
+        pkg.ripser(X, do_cocycles=True)
+    with pytest.raises(NotImplementedError):
+        pkg.ripser(X, n_perm=5)
+    with pytest.raises(NotImplementedError):
+        pkg.ripser(X, metric="cosine")
+    with pytest.raises(ValueError):
+        pkg.ripser(np.zeros((3, 4)), distance_matrix=True)  # not square
+    with pytest.raises(ValueError):
+        pkg.ripser(np.zeros(5))
+    with pytest.raises(NotImplementedError):
+        pkg.ripser(np.eye(3), distance_matrix=True)  # non-zero diagonal
+    Xn = X.copy()
+    Xn[0, 0] = np.nan
+    with pytest.raises(ValueError):
+        pkg.ripser(Xn)
+
+
+def test_get_persistence_semantics(pkg):
+    gp = pkg.get_persistence
+    p, m = gp(np.zeros((0, 2)))
+    assert p.size == 0 and m == 0.0
+    p, m = gp(np.array([[0.0, np.inf]]))
+    assert p.size == 0 and m == 0.0
+    p, m = gp(np.array([[0.0, 1.5], [0.25, 0.5], [0.0, np.inf]]))
+    assert p.tolist() == [1.5, 0.25] and m == 1.5
+    assert pkg.get_max_persistence(np.zeros((0, 2))) == 0
+
+
+def test_layer_record_keys(pkg):
+    dgms = [np.array([[0.0, 2.0], [0.0, np.inf]]), np.array([[1.0, 1.5]]), np.zeros((0, 2))]
+    rec = pkg.layer_record(3, dgms)
+    assert rec["n_h0_features"] == 1 and rec["max_h0_persistence"] == 2.0
+    assert rec["all_h1_persistence_values"] == [0.5] and rec["n_h2_features"] == 0
+
+
+def test_pack_unpack_roundtrip(pkg):
+    pipe = pkg.pipeline
+    rec = {"layer": 7, "n_h1_features": 2, "max_h1_persistence": 0.5, "all_h1_persistence_values": [0.5, 0.125],
+           "n_h0_features": 1, "max_h0_persistence": 3.0, "n_h2_features": 1, "max_h2_persistence": 0.25,
+           "all_h2_persistence_values": [0.25]}
+    back = pipe.unpack_record(pipe.pack_record(rec))
+    assert back.pop("_truncated") is False
+    assert back == rec
+
+
+def test_shard_range_covers_all_layers(pkg):
+    shard = pkg.distributed.shard_range
+    for L in (1, 7, 32, 33):
+        for W in (1, 2, 3, 8):
+            got = []
+            for r in range(W):
+                lo, hi = shard(L, r, W)
+                got.extend(range(lo, hi))
+            assert got == list(range(L))
+
+
+def test_synthetic_generators(pkg):
+    syn = pkg.synthetic
+    X = syn.sweep48(32)
+    assert X.shape == (32, 48, 3) and X.dtype == np.float32
+    assert np.array_equal(syn.layer48(3), X[3])
+    assert syn.torus(64).shape == (64, 3)
+    assert syn.sweep144(2).shape == (2, 144, 3)

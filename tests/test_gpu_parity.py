@@ -1,0 +1,200 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle, the
+reference's golden data and size-independent invariants.
+
+Bar (north_star): pair indices bit-exact, filtration values bit-exact (the
+stated tolerance is 1e-5; we assert equality of the f32 values and check the
+1e-5 bound separately where a value is compared to a float64 reference).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5  # north_star tolerance on filtration values
+
+
+@pytest.fixture(scope="module")
+def gpu(pkg, built_lib):
+    L = pkg.lib()
+    assert L.tda_device_ok(0) == 1, "no gfx950 device visible"
+    return pkg
+
+
+def _pairs(res, d):
+    return [(float(b), float(e), int(bi), int(di)) for (b, e), bi, di in
+            zip(res.dgms[d], res.birth_idx[d], res.death_idx[d])]
+
+
+def _opairs(o, d):
+    return [(float(b), float(e), int(bi), int(di)) for (b, e), bi, di in
+            zip(o["dgms"][d], o["birth_idx"][d], o["death_idx"][d])]
+
+
+def assert_same(res, o, maxdim, tag=""):
+    assert np.float32(res.thresh) == np.float32(o["thresh"]), tag
+    assert res.num_edges == o["num_edges"], tag
+    for d in range(maxdim + 1):
+        assert _pairs(res, d) == _opairs(o, d), (tag, d)
+        assert res.n_all_pairs[d] == o["n_all_pairs"][d], (tag, d)
+        assert res.checksum[d] == o["checksum"][d], (tag, d)
+
+
+def test_reference_fixture_sweep_bit_exact(gpu, ref_clouds, summary_stats):
+    """The 32 committed reference clouds (maxdim=1, one batched call) reproduce
+    the reference's summary_stats.json exactly (values + emission order)."""
+    res = gpu.ripser_batch(ref_clouds, maxdim=1)
+    for l in range(32):
+        assert gpu.layer_record(l, res[l].dgms) == summary_stats[l], l
+
+
+def test_distance_stage_matches_sklearn(gpu):
+    z = np.load(os.path.join(GOLDEN, "sklearn_dist.npz"))
+    for name in sorted({k.split("__")[0] for k in z.files}):
+        X, ref = z[name + "__X"], z[name + "__condensed"]
+        res = gpu.ripser_batch(X[None], maxdim=0, want_dist=True)[0]
+        iu = np.triu_indices(X.shape[0], 1)
+        assert np.array_equal(res.dist[iu].view(np.uint32), ref.view(np.uint32)), name
+        assert np.array_equal(res.dist, res.dist.T)
+
+
+def test_naive_golden_pairs(gpu):
+    with open(os.path.join(GOLDEN, "naive_pairs.json")) as f:
+        cases = json.load(f)
+    for case in cases:
+        X = np.array(case["X"], dtype=np.float32)
+        md = case["maxdim"]
+        res = gpu.ripser_batch(X[None], maxdim=md)[0]
+        for d in range(md + 1):
+            exp = [tuple(x) for x in case["pairs"][str(d)]]
+            got = _pairs(res, d)
+            if d == 0:
+                exp = [(x[0], x[1], x[3]) for x in exp]
+                got = [(x[0], x[1], x[3]) for x in got]
+            assert got == exp, (case["name"], d)
+            assert res.n_all_pairs[d] == case["n_all_pairs"][str(d)]
+
+
+def test_sweep48_maxdim2_vs_oracle(gpu, oracle):
+    """C2/C3 workload (32 layers x 48 points, H0-H2): every pair, its simplex
+    indices, the count and checksum of ALL pairs (incl. zero persistence)."""
+    X = gpu.synthetic.sweep48(32)
+    res = gpu.ripser_batch(X, maxdim=2)
+    orc = oracle.rips_batch_f32(X, 2)
+    for l in range(32):
+        assert_same(res[l], orc[l], 2, f"layer{l}")
+
+
+def test_grid144_maxdim2_vs_oracle(gpu, oracle):
+    X = gpu.synthetic.sweep144(3)
+    res = gpu.ripser_batch(X, maxdim=2)
+    for l in range(3):
+        assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, f"grid{l}")
+
+
+def test_torus512_maxdim1_vs_oracle(gpu, oracle):
+    X = gpu.synthetic.torus(512, seed=3)
+    res = gpu.ripser_batch(X[None], maxdim=1)[0]
+    assert_same(res, oracle.rips(X, maxdim=1), 1, "torus512")
+
+
+def test_torus1024_c4(gpu, oracle):
+    """C4: torus N=1024 maxdim 1: bit-parity with the oracle, one essential H0
+    class, two dominant H1 classes (S^1 x S^1 has Betti_1 = 2)."""
+    X = gpu.synthetic.torus(1024, seed=0)
+    res = gpu.ripser_batch(X[None], maxdim=1)[0]
+    assert_same(res, oracle.rips(X, maxdim=1), 1, "torus1024")
+    assert np.isinf(res.dgms[0][:, 1]).sum() == 1
+    pers = np.sort(res.dgms[1][:, 1] - res.dgms[1][:, 0])[::-1]
+    assert pers[1] > 2.0 * pers[2]
+
+
+def test_invariants_full_size(gpu):
+    """Size-independent properties at the bench size (no oracle needed):
+    every dim-1 column is either paired or essential; the spanning forest has
+    N - #components edges; repeated calls are bitwise identical."""
+    X = gpu.synthetic.sweep48(32)
+    a = gpu.ripser_batch(X, maxdim=2)
+    b = gpu.ripser_batch(X, maxdim=2)
+    for ra, rb in zip(a, b):
+        for d in range(3):
+            assert _pairs(ra, d) == _pairs(rb, d) and ra.checksum[d] == rb.checksum[d]
+        n_inf0 = int(np.isinf(ra.dgms[0][:, 1]).sum())
+        assert ra.n_all_pairs[0] == 48 - n_inf0
+        assert ra.n_columns[1] == ra.num_edges - ra.n_all_pairs[0]
+        for d in (1, 2):
+            n_ess = int(np.isinf(ra.dgms[d][:, 1]).sum())
+            assert ra.n_columns[d] == ra.n_all_pairs[d] + n_ess
+
+
+def test_input_variants(gpu, oracle, ref_clouds):
+    X = ref_clouds[7]
+    base = gpu.ripser_batch(X[None], maxdim=2)[0]
+    o = oracle.rips(X, maxdim=2)
+    assert_same(base, o, 2, "f32")
+    # distance-matrix input (square f32) and the condensed C entry tda_rips_dm
+    Dm = o["dperm2all"]
+    dm = gpu.ripser_batch(Dm[None], maxdim=2, distance_matrix=True)[0]
+    assert_same(dm, o, 2, "dm")
+    iu = np.triu_indices(Dm.shape[0], 1)
+    cond = gpu.rips_dm(Dm[iu], maxdim=2)
+    assert_same(cond, o, 2, "condensed")
+    # float64 points (sklearn f64 path: sqrt in f64, then f32)
+    X64 = X.astype(np.float64) * 1.0000001
+    r64 = gpu.ripser_batch(X64[None], maxdim=1)[0]
+    assert_same(r64, oracle.rips(X64, maxdim=1), 1, "f64")
+    # finite threshold
+    t = float(np.float32(np.median(Dm[iu])))
+    rt = gpu.ripser_batch(X[None], maxdim=2, thresh=t)[0]
+    assert_same(rt, oracle.rips(X, maxdim=2, thresh=t), 2, "thresh")
+    # ripser() dict
+    d = gpu.ripser(X, maxdim=1)
+    assert set(d) == {"dgms", "cocycles", "num_edges", "dperm2all", "idx_perm", "r_cover"}
+    assert d["num_edges"] == o["num_edges"] and np.array_equal(d["dperm2all"], Dm)
+
+
+def test_edge_cases(gpu, oracle):
+    for X in (np.zeros((1, 3), np.float32), np.array([[0, 0], [3, 4]], np.float32),
+              np.array([[0, 0, 0], [0, 0, 0], [1, 0, 0]], np.float32),
+              np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float32)):
+        r = gpu.ripser_batch(X[None], maxdim=2)[0]
+        assert_same(r, oracle.rips(X, maxdim=2), 2, str(X.shape))
+    # ragged batch sizes: L not a multiple of anything, one layer with duplicates
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((5, 30, 3)).astype(np.float32)
+    X[2, 1] = X[2, 0]
+    res = gpu.ripser_batch(X, maxdim=2)
+    for l in range(5):
+        assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, f"ragged{l}")
+
+
+def test_torch_device_input(gpu, oracle):
+    import torch
+
+    X = gpu.synthetic.sweep48(4)
+    t = torch.from_numpy(X).to("cuda:0")
+    res = gpu.ripser_batch(t, maxdim=2)
+    for l in range(4):
+        assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, f"torch{l}")
+
+
+def test_random_clouds_vs_oracle(gpu, oracle):
+    rng = np.random.default_rng(11)
+    for n, D, md in ((20, 2, 2), (40, 5, 2), (64, 3, 2), (100, 3, 2), (200, 4, 1), (97, 16, 1)):
+        X = rng.standard_normal((2, n, D)).astype(np.float32)
+        res = gpu.ripser_batch(X, maxdim=md)
+        for l in range(2):
+            assert_same(res[l], oracle.rips(X[l], maxdim=md), md, f"n{n}D{D}")
+
+
+def test_values_within_tolerance_of_sklearn(gpu, ref_clouds):
+    """Filtration values vs a float64 recomputation from sklearn distances."""
+    from sklearn.metrics import pairwise_distances
+
+    X = ref_clouds[25]
+    r = gpu.ripser_batch(X[None], maxdim=1, want_dist=True)[0]
+    Dref = pairwise_distances(X).astype(np.float64)
+    assert np.max(np.abs(r.dist.astype(np.float64) - Dref)) <= TOL

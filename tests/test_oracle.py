@@ -1,0 +1,117 @@
+"""CPU tests: pin the oracle (oracle/) against the reference's golden data.
+
+* summary_stats.json (reference ripser outputs on its 32 committed clouds)
+* sklearn distance goldens (the distance stage ripser runs first)
+* an independent naive Z/2 boundary reduction (oracle/naive.py), with pair
+  indices, on small clouds and on reference layers at maxdim 2
+* known-answer cases (circle, duplicates, ties, tiny N)
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_pkg
+
+
+def test_oracle_reproduces_reference_summary_stats(oracle, ref_clouds, summary_stats):
+    pipe = load_pkg().pipeline
+    for l in range(32):
+        r = oracle.rips(ref_clouds[l], maxdim=1)
+        rec = pipe.layer_record(l, r["dgms"])
+        exp = summary_stats[l]
+        # bit-exact: float64 persistence of f32 births/deaths, emission order included
+        assert rec == exp, (l, rec, exp)
+
+
+def test_oracle_distance_matches_sklearn_goldens(oracle):
+    z = np.load(os.path.join(GOLDEN, "sklearn_dist.npz"))
+    names = sorted({k.split("__")[0] for k in z.files})
+    for name in names:
+        X, ref = z[name + "__X"], z[name + "__condensed"]
+        D = oracle.distances(X)
+        iu = np.triu_indices(X.shape[0], 1)
+        # bit-exact (sequential-k f64 accumulation == OpenBLAS/einsum for D <= 8)
+        assert np.array_equal(D[iu].view(np.uint32), ref.view(np.uint32)), name
+        assert np.array_equal(D, D.T) and np.all(np.diag(D) == 0)
+
+
+def _load_naive():
+    with open(os.path.join(GOLDEN, "naive_pairs.json")) as f:
+        return json.load(f)
+
+
+def test_oracle_matches_naive_reduction_with_indices(oracle):
+    for case in _load_naive():
+        X = np.array(case["X"], dtype=np.float32)
+        md = case["maxdim"]
+        r = oracle.rips(X, maxdim=md)
+        assert np.float32(r["thresh"]) == np.float32(case["thresh"])
+        for d in range(md + 1):
+            exp = case["pairs"][str(d)]
+            got = [[float(b), float(e), int(bi), int(di)] for (b, e), bi, di in
+                   zip(r["dgms"][d], r["birth_idx"][d], r["death_idx"][d])]
+            if d == 0:  # naive does not track the elder-rule birth vertex
+                exp = [[x[0], x[1], x[3]] for x in exp]
+                got = [[x[0], x[1], x[3]] for x in got]
+            assert got == exp, (case["name"], d)
+            assert r["n_all_pairs"][d] == case["n_all_pairs"][str(d)], (case["name"], d)
+
+
+def test_oracle_h2_reference_crosscheck(oracle, ref_clouds):
+    # one H2 bar on layers 5, 17, 19 (values in f32); none on layer 0
+    exp = {5: (0.5088863, 0.51204515), 17: (0.5333502, 0.5628882), 19: (0.45109242, 0.5353451)}
+    for l in (0, 5, 17, 19):
+        r = oracle.rips(ref_clouds[l], maxdim=2)
+        d2 = r["dgms"][2]
+        if l in exp:
+            assert d2.shape == (1, 2)
+            assert (np.float32(d2[0, 0]), np.float32(d2[0, 1])) == tuple(np.float32(v) for v in exp[l])
+        else:
+            assert d2.shape == (0, 2)
+
+
+def test_known_answer_circle(oracle):
+    t = np.linspace(0, 2 * np.pi, 40, endpoint=False)
+    X = np.stack([np.cos(t), np.sin(t), np.zeros_like(t)], 1).astype(np.float32)
+    r = oracle.rips(X, maxdim=1)
+    h1 = r["dgms"][1]
+    assert len(r["dgms"][0]) == 40 and np.isinf(r["dgms"][0][-1, 1])
+    pers = h1[:, 1] - h1[:, 0]
+    assert np.sum(pers > 0.5) == 1
+
+
+def test_known_answer_duplicates_and_tiny(oracle):
+    X = np.array([[0, 0, 0], [0, 0, 0], [1, 0, 0]], dtype=np.float32)
+    r = oracle.rips(X, maxdim=1)
+    # zero-length H0 bar omitted: one finite [0,1) and one [0,inf)
+    assert r["dgms"][0].tolist() == [[0.0, 1.0], [0.0, np.inf]]
+    assert r["dgms"][1].shape == (0, 2)
+    r1 = oracle.rips(np.zeros((1, 3), np.float32), maxdim=1)
+    assert r1["dgms"][0].tolist() == [[0.0, np.inf]] and r1["num_edges"] == 0
+    r2 = oracle.rips(np.array([[0, 0], [3, 4]], np.float32), maxdim=2)
+    assert r2["dgms"][0].tolist() == [[0.0, 5.0], [0.0, np.inf]]
+
+
+def test_known_answer_square_ties(oracle):
+    # 4-cycle with equal sides: ties broken by the combinatorial index
+    X = np.array([[0, 0], [1, 0], [1, 1], [0, 1]], dtype=np.float32)
+    r = oracle.rips(X, maxdim=1)
+    assert r["dgms"][1].shape == (1, 2)
+    assert r["dgms"][1][0, 0] == 1.0 and np.float32(r["dgms"][1][0, 1]) == np.float32(np.sqrt(2))
+
+
+@pytest.mark.parametrize("n,md", [(12, 2), (24, 1)])
+def test_oracle_random_vs_naive_live(oracle, n, md):
+    from oracle import naive
+
+    rng = np.random.default_rng(n * 7 + md)
+    for _ in range(3):
+        X = rng.standard_normal((n, 4)).astype(np.float32)
+        r = oracle.rips(X, maxdim=md)
+        em, allp, th = naive.naive_pairs(r["dperm2all"], md)
+        for d in range(1, md + 1):
+            got = [(float(b), float(e), int(bi), int(di)) for (b, e), bi, di in
+                   zip(r["dgms"][d], r["birth_idx"][d], r["death_idx"][d])]
+            assert got == [(float(b), float(e), bi, di) for b, e, bi, di in em[d]]
