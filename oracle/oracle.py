@@ -33,6 +33,7 @@ class _Result(ctypes.Structure):
         ("checksum", ctypes.c_uint64 * MAXD),
         ("n_columns", ctypes.c_int64 * MAXD),
         ("n_apparent", ctypes.c_int64 * MAXD),
+        ("n_adds", ctypes.c_int64 * MAXD),
         ("num_edges", ctypes.c_int64),
         ("thresh", ctypes.c_float),
     ]
@@ -108,6 +109,7 @@ def _unpack(r: _Result, maxdim: int) -> dict:
         "checksum": [int(r.checksum[d]) for d in range(maxdim + 1)],
         "n_columns": [int(r.n_columns[d]) for d in range(maxdim + 1)],
         "n_apparent": [int(r.n_apparent[d]) for d in range(maxdim + 1)],
+        "n_adds": [int(r.n_adds[d]) for d in range(maxdim + 1)],
     }
 
 

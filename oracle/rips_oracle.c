@@ -57,6 +57,7 @@ typedef struct {
     uint64_t checksum[OR_MAXDIM + 1];   /* order-free hash over all pairs       */
     int64_t n_columns[OR_MAXDIM + 1];   /* columns reduced per dim              */
     int64_t n_apparent[OR_MAXDIM + 1];  /* columns that are apparent pairs      */
+    int64_t n_adds[OR_MAXDIM + 1];      /* column additions performed           */
     int64_t num_edges;
     float thresh;
 } oracle_result;
@@ -526,6 +527,7 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
                 }
                 int64_t o = hm_get(&piv, p.idx);
                 if (o >= 0) {
+                    res->n_adds[dim]++;
                     /* add column o: its simplex plus its V entries */
                     int64_t cnt = 1 + (voff[o + 1] - voff[o]);
                     for (int64_t t = 0; t < cnt; ++t) {

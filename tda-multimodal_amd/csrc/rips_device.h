@@ -95,6 +95,25 @@ __device__ __forceinline__ float simplex_diam(const float* __restrict__ D, int n
     return d;
 }
 
+// ---------------------------------------------------------------- sqrt
+// Correctly rounded f32 sqrt, independent of the accuracy of the hardware
+// sqrt: start from the f64 sqrt rounded to f32 (within 1 ulp) and fix the
+// rounding with exact midpoint tests (a 25-bit midpoint squares exactly in
+// f64; sqrt of a float never lands on a midpoint).  numpy's np.sqrt on f32
+// (sklearn pairwise.py:441) is correctly rounded.
+__device__ __forceinline__ float sqrt_rn_f32(float x) {
+    if (!(x > 0.0f) || isinf(x)) return x == 0.0f ? 0.0f : (x > 0.0f ? x : __builtin_nanf(""));
+    float f = (float)__builtin_sqrt((double)x);
+    const double xd = (double)x;
+    const float up = __uint_as_float(__float_as_uint(f) + 1u);  // f > 0 finite
+    const double mu = 0.5 * ((double)f + (double)up);
+    if (mu * mu <= xd) return up;
+    const float dn = __uint_as_float(__float_as_uint(f) - 1u);
+    const double md = 0.5 * ((double)f + (double)dn);
+    if (md * md > xd) return dn;
+    return f;
+}
+
 // ---------------------------------------------------------------- hashing
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x ^= x >> 33;

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
     if constexpr (sizeof(T) == 4) {
         f = (float)d;
         f = (f != f) ? f : fmaxf(f, 0.0f);
-        f = __fsqrt_rn(f);
+        f = sqrt_rn_f32(f);
     } else {
         d = (d != d) ? d : fmax(d, 0.0);
         f = (float)__dsqrt_rn(d);
