@@ -86,6 +86,7 @@ typedef struct tda_rips_result {
     const int64_t *n_all_pairs;/* [L][maxdim+1] all pairs incl. zero-persistence*/
     const int64_t *n_columns; /* [L][maxdim+1] columns considered per dim       */
     const int64_t *n_residual;/* [L][maxdim+1] columns needing reduction        */
+    const int64_t *n_adds;    /* [L][maxdim+1] column additions (serial part)   */
     const float *dist;        /* [L][N][N] when want_dist, else NULL            */
     double device_ms;         /* device time of the call (HIP events)           */
     /* per-stage device times, filled when args.flags & TDA_FLAG_STAGE_TIMES:

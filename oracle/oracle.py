@@ -34,6 +34,9 @@ class _Result(ctypes.Structure):
         ("n_columns", ctypes.c_int64 * MAXD),
         ("n_apparent", ctypes.c_int64 * MAXD),
         ("n_adds", ctypes.c_int64 * MAXD),
+        ("max_heap", ctypes.c_int64 * MAXD),
+        ("max_live", ctypes.c_int64 * MAXD),
+        ("sum_live", ctypes.c_int64 * MAXD),
         ("num_edges", ctypes.c_int64),
         ("thresh", ctypes.c_float),
     ]
@@ -110,6 +113,9 @@ def _unpack(r: _Result, maxdim: int) -> dict:
         "n_columns": [int(r.n_columns[d]) for d in range(maxdim + 1)],
         "n_apparent": [int(r.n_apparent[d]) for d in range(maxdim + 1)],
         "n_adds": [int(r.n_adds[d]) for d in range(maxdim + 1)],
+        "max_heap": [int(r.max_heap[d]) for d in range(maxdim + 1)],
+        "max_live": [int(r.max_live[d]) for d in range(maxdim + 1)],
+        "sum_live": [int(r.sum_live[d]) for d in range(maxdim + 1)],
     }
 
 

@@ -58,6 +58,9 @@ typedef struct {
     int64_t n_columns[OR_MAXDIM + 1];   /* columns reduced per dim              */
     int64_t n_apparent[OR_MAXDIM + 1];  /* columns that are apparent pairs      */
     int64_t n_adds[OR_MAXDIM + 1];      /* column additions performed           */
+    int64_t max_heap[OR_MAXDIM + 1];    /* largest working heap (entries)       */
+    int64_t max_live[OR_MAXDIM + 1];    /* largest reduced column |R_j| (debug) */
+    int64_t sum_live[OR_MAXDIM + 1];
     int64_t num_edges;
     float thresh;
 } oracle_result;
@@ -286,6 +289,11 @@ static splx_t heap_get_pivot(heap_t *h) {
         return p;
     }
     return none;
+}
+
+int cmpu(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
 }
 
 /* ---------- the complex ------------------------------------------------ */
@@ -520,6 +528,7 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
             }
             for (;;) {
                 splx_t p = heap_get_pivot(&work);
+                if (work.n > res->max_heap[dim]) res->max_heap[dim] = work.n;
                 if (p.idx == HM_EMPTY) {
                     pairs_push(&P[dim], sg.diam, INFINITY, (int64_t)sg.idx, -1);
                     voff[j + 1] = vn;
@@ -543,6 +552,22 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
                         heap_push(&vwork, ve);
                     }
                 } else {
+                    if (getenv("ORACLE_DEBUG_LIVE")) {
+                        uint64_t *tmpk = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(work.n + 1));
+                        for (int64_t q = 0; q < work.n; ++q) tmpk[q] = work.a[q].idx;
+                        int cmpu(const void *a, const void *b);
+                        qsort(tmpk, (size_t)work.n, sizeof(uint64_t), cmpu);
+                        int64_t live = 0;
+                        for (int64_t q = 0; q < work.n;) {
+                            int64_t r = q;
+                            while (r < work.n && tmpk[r] == tmpk[q]) ++r;
+                            live += (r - q) & 1;
+                            q = r;
+                        }
+                        free(tmpk);
+                        if (live > res->max_live[dim]) res->max_live[dim] = live;
+                        res->sum_live[dim] += live;
+                    }
                     if (p.diam > sg.diam) pairs_push(&P[dim], sg.diam, p.diam, (int64_t)sg.idx, (int64_t)p.idx);
                     hm_put(&piv, p.idx, j);
                     res->n_all_pairs[dim]++;

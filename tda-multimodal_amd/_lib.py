@@ -13,7 +13,7 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(_HERE, "_build")
-LIB_PATH = os.path.join(BUILD_DIR, "libtda_rips.so")
+LIB_PATH = os.environ.get("TDA_RIPS_LIB") or os.path.join(BUILD_DIR, "libtda_rips.so")
 CSRC = os.path.join(_HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(_HERE), "include")
 
@@ -61,6 +61,7 @@ class RipsResult(ctypes.Structure):
         ("n_all_pairs", _i64p),
         ("n_columns", _i64p),
         ("n_residual", _i64p),
+        ("n_adds", _i64p),
         ("dist", _f32p),
         ("device_ms", ctypes.c_double),
         ("n_stages", ctypes.c_int32),

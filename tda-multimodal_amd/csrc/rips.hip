@@ -17,6 +17,7 @@
 
 #include "../../include/tda_rips.h"
 #include "rips_kernels.h"
+#include "rips_reduce.h"
 
 using namespace tda;
 
@@ -50,25 +51,42 @@ inline int ilog2(uint64_t x) {
 constexpr uint64_t kRCapMax = 1ull << 22;    // residual columns per layer and dim
 constexpr uint64_t kPCapMax = 1ull << 16;    // emitted pairs per layer and dim (H>=1)
 constexpr int kLdsMax = 160 * 1024;
-constexpr int kDistLdsMaxN = 96;             // stage the distance matrix in LDS below this
-constexpr uint32_t kWCapLds = 4096, kVCapLds = 1024;
+constexpr int kSmallN = 64;                  // one-wave H0 + LDS-resident reduction up to here
+constexpr int kAppLdsMaxN = 128;             // k_apparent stages the distance matrix in LDS up to here
 
 // ------------------------------------------------------------------ plan
 struct Plan {
     int64_t L = 0, N = 0, D = 0;
     int maxdim = 0, dtype = 0, is_dist = 0;
     uint64_t ncand[4] = {0}, piv_words[4] = {0}, rcap[4] = {0}, pcap[4] = {0};
-    uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, sstride = 0;
+    uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, vcap_g = 0, sstride = 0;
     bool lds_mode = false;
-    int dist_in_lds = 0;
+    Reduce2Cfg rcfg[4] = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wd = 0, o_wp = 0, o_wl = 0, o_pairs[4] = {0}, o_h0s = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0,
+           o_hsig = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
 };
 
-int make_plan(Plan& p) {
+// LDS carve of k_reduce2 in LDS mode (mirrors the kernel's take() order)
+Reduce2Cfg reduce_cfg(int n, uint64_t piv_words) {
+    Reduce2Cfg c{};
+    auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
+    c.rmap_lds_cap = 1024;
+    c.dist_lds = 1;
+    auto wbytes = [&](uint64_t w) { return al(8 * w) + al(16 * w); };
+    const uint64_t fixed = 16 + al(8ull * c.rmap_lds_cap) + al(4ull * c.rmap_lds_cap) + al(4ull * n * n);
+    const uint64_t piv = al(4ull * piv_words);
+    c.wcap = 8192;
+    c.piv_lds = fixed + piv + wbytes(c.wcap) <= (uint64_t)kLdsMax ? 1 : 0;
+    while (c.wcap > 1024 && fixed + (c.piv_lds ? piv : 0) + wbytes(c.wcap) > (uint64_t)kLdsMax) c.wcap >>= 1;
+    c.bytes = (uint32_t)(fixed + (c.piv_lds ? piv : 0) + wbytes(c.wcap));
+    return c;
+}
+
+int make_plan(Plan& p, bool force_global, int scale) {
     const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
     p.mst_words = (binom(N, 2) + 31) / 32 + 1;
     for (int d = 1; d <= p.maxdim; ++d) {
@@ -81,10 +99,18 @@ int make_plan(Plan& p) {
     p.pcap[0] = N + 1;
     p.max_rcap = std::max<uint64_t>(p.max_rcap, 1);
     p.rmap_stride = next_pow2(2 * p.max_rcap + 16);
-    p.vpool_cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 16, 4 * p.max_rcap), 1ull << 24);
-    p.lds_mode = p.N <= kDistLdsMaxN;
-    p.dist_in_lds = p.lds_mode ? 1 : 0;
-    p.wcap_g = next_pow2(std::max<uint64_t>(1ull << 15, 64 * N));
+    p.vpool_cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 16, 32 * p.max_rcap), 1ull << 27) << scale;
+    p.lds_mode = p.N <= kSmallN && !force_global;
+    for (int d = 1; d <= p.maxdim; ++d) {
+        if (p.lds_mode) {
+            p.rcfg[d] = reduce_cfg((int)N, p.piv_words[d]);
+        } else {
+            p.rcfg[d] = Reduce2Cfg{};
+            p.rcfg[d].dist_lds = N <= 96 ? 1 : 0;
+            p.rcfg[d].bytes = 16 + (p.rcfg[d].dist_lds ? (uint32_t)(4 * N * N) : 0);
+        }
+    }
+    p.wcap_g = (N <= 256 ? 1ull << 17 : (N <= 640 ? 1ull << 21 : 1ull << 23)) << (2 * scale);
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
     p.sstride = 3 * maxp;
@@ -108,14 +134,14 @@ int make_plan(Plan& p) {
     if (p.maxdim >= 1) {
         p.o_rmk = take(L * p.rmap_stride * 8);
         p.o_rmv = take(L * p.rmap_stride * 4);
-        p.o_voff = take(L * p.max_rcap * 4);
         p.o_vlen = take(L * p.max_rcap * 4);
         p.o_vpool = take(L * p.vpool_cap * 8);
+        p.o_voff = take(L * p.max_rcap * 8);
+        uint64_t wmax = p.lds_mode ? 8192 : p.wcap_g;
+        p.o_wt = take(L * wmax * 8 * 2);  // slot scratch + compaction keys
         if (!p.lds_mode) {
-            p.o_wk = take(L * p.wcap_g * 8);
-            p.o_wd = take(L * p.wcap_g * 4);
-            p.o_wp = take(L * p.wcap_g * 4);
-            p.o_wl = take(L * p.wcap_g * 4);
+            p.o_wk = take(L * p.wcap_g * 8);       // key log
+            p.o_wl = take(L * p.wcap_g * 2 * 8);   // u64 index, 2 * wcap slots
         }
     }
     for (int d = 0; d <= p.maxdim; ++d) p.o_pairs[d] = take(L * p.pcap[d] * sizeof(Pair));
@@ -241,10 +267,19 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_h0, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_sort_resid, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_finalize, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    HIPC(hipFuncSetAttribute((const void*)k_reduce<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    HIPC(hipFuncSetAttribute((const void*)k_reduce<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    HIPC(hipFuncSetAttribute((const void*)k_reduce<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    HIPC(hipFuncSetAttribute((const void*)k_reduce<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+#define TDA_ATTR_RED(D, LW, PK) \
+    HIPC(hipFuncSetAttribute((const void*)k_reduce2<D, LW, PK>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax))
+    TDA_ATTR_RED(1, true, true);
+    TDA_ATTR_RED(1, true, false);
+    TDA_ATTR_RED(1, false, true);
+    TDA_ATTR_RED(1, false, false);
+    TDA_ATTR_RED(2, true, true);
+    TDA_ATTR_RED(2, true, false);
+    TDA_ATTR_RED(2, false, true);
+    TDA_ATTR_RED(2, false, false);
+#undef TDA_ATTR_RED
+    HIPC(hipFuncSetAttribute((const void*)k_apparent<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_apparent<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     if (dev < 64) g_attr_done[dev] = true;
     return 0;
 }
@@ -252,7 +287,7 @@ int set_lds_attrs(int dev) {
 // result owned by the library
 struct ResultImpl {
     tda_rips_result pub;
-    std::vector<int64_t> count, offset, num_edges, n_all, n_cols, n_res, bidx, didx;
+    std::vector<int64_t> count, offset, num_edges, n_all, n_cols, n_res, n_add, bidx, didx;
     std::vector<float> birth, death, thresh, dist, stage_ms;
     std::vector<const char*> stage_name;
     std::vector<uint64_t> checksum;
@@ -270,7 +305,8 @@ std::string err_flags(int e) {
 
 // ------------------------------------------------------------------ pipeline
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
-int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out) {
+int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
+                 bool force_global = false, int scale = 0) {
     Plan p;
     p.L = a.L;
     p.N = a.N;
@@ -278,7 +314,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     p.maxdim = a.maxdim;
     p.dtype = a.dtype;
     p.is_dist = input_kind != 0;
-    make_plan(p);
+    make_plan(p, force_global, scale);
     const int dev = a.device;
     HIPC(hipSetDevice(dev));
     Workspace& w = *get_ws(dev);
@@ -338,8 +374,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     MARK(input_kind == 0 ? "k_distance" : "k_square_dist");
 
     // ---- H0
-    {
-        int T = n <= 64 ? 64 : (n <= 256 ? 256 : 1024);
+    if (n <= kSmallN) {
+        hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s, dist, n, a.thresh, stats,
+                           (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
+        HIPC(hipGetLastError());
+        MARK("k_h0");
+    } else {
+        int T = n <= 256 ? 256 : 1024;
         size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
         base = align_up(base, 16);
         size_t avail = kLdsMax - base;
@@ -353,18 +394,18 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 
     // ---- H1 .. Hmaxdim
-    ReduceBufs rb;
+    Reduce2Bufs rb;
     rb.rmap_keys = (uint64_t*)(B + p.o_rmk);
     rb.rmap_vals = (uint32_t*)(B + p.o_rmv);
     rb.rmap_stride = p.rmap_stride;
-    rb.voff = (uint32_t*)(B + p.o_voff);
-    rb.vlen = (uint32_t*)(B + p.o_vlen);
-    rb.vpool = (uint64_t*)(B + p.o_vpool);
-    rb.vpool_cap = p.vpool_cap;
-    rb.wkeys = (uint64_t*)(B + p.o_wk);
-    rb.wdiam = (float*)(B + p.o_wd);
-    rb.wpar = (uint32_t*)(B + p.o_wp);
-    rb.wlist = (uint32_t*)(B + p.o_wl);
+    rb.roff = (uint64_t*)(B + p.o_voff);
+    rb.rlen = (uint32_t*)(B + p.o_vlen);
+    rb.rpool = (uint64_t*)(B + p.o_vpool);
+    rb.rpool_cap = p.vpool_cap;
+    rb.wtmp = (uint64_t*)(B + p.o_wt);
+    rb.wtmp_stride = 2 * (p.lds_mode ? 8192 : p.wcap_g);
+    rb.wlog = (uint64_t*)(B + p.o_wk);
+    rb.windex = (uint64_t*)(B + p.o_wl);
     rb.wcap = p.wcap_g;
     for (int d = 1; d <= p.maxdim; ++d) {
         DimBufs db;
@@ -378,38 +419,46 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         Pair* pairs = (Pair*)(B + p.o_pairs[d]);
         uint64_t blocks = (p.ncand[d] + 255) / 256;
         unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, 4096 / L)));
-        if (d == 1)
-            hipLaunchKernelGGL(k_apparent<1>, dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
-        else
-            hipLaunchKernelGGL(k_apparent<2>, dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
+        const bool dl = n <= kAppLdsMaxN;
+        const size_t alds = dl ? (size_t)n * n * 4 : 0;
+        if (d == 1) {
+            if (dl)
+                hipLaunchKernelGGL((k_apparent<1, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db, pairs, p.pcap[d]);
+            else
+                hipLaunchKernelGGL((k_apparent<1, false>), dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
+        } else {
+            if (dl)
+                hipLaunchKernelGGL((k_apparent<2, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db, pairs, p.pcap[d]);
+            else
+                hipLaunchKernelGGL((k_apparent<2, false>), dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
+        }
         HIPC(hipGetLastError());
         MARK(d == 1 ? "k_apparent<1>" : "k_apparent<2>");
         hipLaunchKernelGGL(k_sort_resid, dim3(L), dim3(1024), 16384 * 8, s, stats, d, db.resid, db.rcap, (uint64_t*)(B + p.o_tmp),
                            rb.rmap_keys, rb.rmap_stride, 14);
         HIPC(hipGetLastError());
         MARK(d == 1 ? "k_sort_resid<1>" : "k_sort_resid<2>");
-        size_t lds = 16;
-        if (p.lds_mode) {
-            lds += (size_t)kWCapLds * 20 + (size_t)kVCapLds * 20;
-            if (p.dist_in_lds) lds += (size_t)n * n * 4;
-        } else {
-            lds += (size_t)kVCapLds * 20;
+        const Reduce2Cfg& rc = p.rcfg[d];
+        if (!p.lds_mode) {
+            HIPC(hipMemsetAsync(rb.windex, 0, (size_t)L * p.wcap_g * 2 * 8, s));
         }
-        if (p.lds_mode) {
-            if (d == 1)
-                hipLaunchKernelGGL((k_reduce<1, true>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], kWCapLds,
-                                   kVCapLds, p.dist_in_lds);
-            else
-                hipLaunchKernelGGL((k_reduce<2, true>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], kWCapLds,
-                                   kVCapLds, p.dist_in_lds);
+        const bool packed = (d == 1 && n <= 1024) || (d == 2 && n <= 256);
+#define TDA_LAUNCH_RED(D, LW, PK)                                                                                      \
+    hipLaunchKernelGGL((k_reduce2<D, LW, PK>), dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db, rb, rc, pairs, p.pcap[d])
+        if (d == 1) {
+            if (p.lds_mode) {
+                if (packed) TDA_LAUNCH_RED(1, true, true); else TDA_LAUNCH_RED(1, true, false);
+            } else {
+                if (packed) TDA_LAUNCH_RED(1, false, true); else TDA_LAUNCH_RED(1, false, false);
+            }
         } else {
-            if (d == 1)
-                hipLaunchKernelGGL((k_reduce<1, false>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], 0u,
-                                   kVCapLds, 0);
-            else
-                hipLaunchKernelGGL((k_reduce<2, false>), dim3(L), dim3(64), lds, s, dist, n, stats, db, rb, pairs, p.pcap[d], 0u,
-                                   kVCapLds, 0);
+            if (p.lds_mode) {
+                if (packed) TDA_LAUNCH_RED(2, true, true); else TDA_LAUNCH_RED(2, true, false);
+            } else {
+                if (packed) TDA_LAUNCH_RED(2, false, true); else TDA_LAUNCH_RED(2, false, false);
+            }
         }
+#undef TDA_LAUNCH_RED
         HIPC(hipGetLastError());
         MARK(d == 1 ? "k_reduce<1>" : "k_reduce<2>");
     }
@@ -429,7 +478,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipGetLastError());
         MARK("k_finalize");
     }
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
+    const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
                        (const uint64_t*)(B + p.o_pcap), (int64_t*)(B + p.o_outoff), w.hout_dev, (uint64_t)w.hout_cap);
     HIPC(hipGetLastError());
     MARK("k_compact");
@@ -448,7 +498,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         if (int rc = grow_hout(w, need + 16)) return rc;
         for (int l = 0; l < L; ++l) w.hstats[l].err = 0;
         HIPC(hipMemcpyAsync(stats, w.hstats, sizeof(LayerStats) * L, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
+        const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
                            (const uint64_t*)(B + p.o_pcap), (int64_t*)(B + p.o_outoff), w.hout_dev, (uint64_t)w.hout_cap);
         HIPC(hipGetLastError());
         HIPC(hipMemcpyAsync(w.hstats, stats, sizeof(LayerStats) * L, hipMemcpyDeviceToHost, s));
@@ -457,7 +508,29 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         errs = 0;
         for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
     }
+    if ((errs & ERR_LDS_SPILL) && !force_global) {
+        // a working column outgrew LDS: redo the batch with global-memory tables
+        return run_pipeline(a, input_kind, host_or_dev, out, true, scale);
+    }
+    if ((errs & ~(ERR_LDS_SPILL)) == (errs & (ERR_WORK_CAP | ERR_VPOOL_CAP)) && errs && scale < 2) {
+        // working column / reduced-column pool too small: retry with larger buffers
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1);
+    }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
+#ifdef TDA_PROFILE
+    for (int d = 1; d <= p.maxdim; ++d) {
+        uint64_t mx[8] = {0};
+        int arg = 0;
+        for (int l = 0; l < L; ++l)
+            if (w.hstats[l].prof[d][7] > mx[7]) {
+                arg = l;
+                for (int i = 0; i < 8; ++i) mx[i] = w.hstats[l].prof[d][i];
+            }
+        fprintf(stderr, "[tda-prof] dim %d slowest layer %d adds %lld: scan %llu lookup %llu dec+facet %llu cob_app %llu cob_res %llu reset %llu compact %llu total %llu cycles\n",
+                d, arg, (long long)w.hstats[arg].n_adds[d], (unsigned long long)mx[0], (unsigned long long)mx[1], (unsigned long long)mx[2],
+                (unsigned long long)mx[3], (unsigned long long)mx[4], (unsigned long long)mx[5], (unsigned long long)mx[6], (unsigned long long)mx[7]);
+    }
+#endif
 
     // ---- result
     auto* R = new ResultImpl();
@@ -468,6 +541,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     R->n_all.resize((size_t)L * nd);
     R->n_cols.resize((size_t)L * nd);
     R->n_res.resize((size_t)L * nd);
+    R->n_add.resize((size_t)L * nd);
     R->thresh.resize(L);
     R->num_edges.resize(L);
     size_t total = 0;
@@ -483,6 +557,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             R->n_all[l * nd + d] = st.all_pairs[d];
             R->n_cols[l * nd + d] = st.n_columns[d];
             R->n_res[l * nd + d] = st.n_residual[d];
+            R->n_add[l * nd + d] = st.n_adds[d];
             total += (size_t)c;
         }
     }
@@ -518,6 +593,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     o.n_all_pairs = R->n_all.data();
     o.n_columns = R->n_cols.data();
     o.n_residual = R->n_res.data();
+    o.n_adds = R->n_add.data();
     o.dist = a.want_dist ? R->dist.data() : nullptr;
     o.device_ms = ms;
     for (size_t i = 0; i < tm.names.size(); ++i) {
@@ -543,7 +619,9 @@ int validate(const tda_rips_args* a) {
     if (a->modulus != 2) return fail(TDA_E_UNSUPPORTED, "only coeff=2 (Z/2) is supported");
     if (a->maxdim < 0 || a->maxdim > 2) return fail(TDA_E_UNSUPPORTED, "maxdim must be 0, 1 or 2");
     if (a->N > 8192) return fail(TDA_E_UNSUPPORTED, "N > 8192 is not supported");
-    if (a->maxdim == 2 && a->N > 2900) return fail(TDA_E_UNSUPPORTED, "maxdim=2 requires N <= 2900");
+    // filtration keys pack a 32-bit row-simplex index: C(N, maxdim+2) < 2^32
+    if (a->maxdim == 1 && a->N > 2900) return fail(TDA_E_UNSUPPORTED, "maxdim=1 requires N <= 2900");
+    if (a->maxdim == 2 && a->N > 568) return fail(TDA_E_UNSUPPORTED, "maxdim=2 requires N <= 568");
     if (std::isnan(a->thresh)) return fail(TDA_E_INVALID, "thresh is NaN");
     return 0;
 }

@@ -15,16 +15,24 @@ namespace tda {
 constexpr uint64_t kEmpty64 = 0xFFFFFFFFFFFFFFFFull;
 
 // ---------------------------------------------------------------- binomials
-__host__ __device__ __forceinline__ uint64_t binom(uint64_t n, int k) {
-    switch (k) {
-        case 0: return 1;
-        case 1: return n;
-        case 2: return n < 2 ? 0 : n * (n - 1) / 2;
-        case 3: return n < 3 ? 0 : n * (n - 1) * (n - 2) / 6;
-        case 4: return n < 4 ? 0 : (n * (n - 1) / 2) * ((n - 2) * (n - 3) / 2) / 6;
-        case 5: return n < 5 ? 0 : ((n * (n - 1) / 2) * ((n - 2) * (n - 3) / 2) / 6) * (n - 4) / 5;
-        default: return 0;
-    }
+// C(n, k) for k <= 5 without 64-bit division: 32-bit exact-division steps
+// (C(n,k) = C(n,k-1) * (n-k+1) / k, split so every quotient is exact) and one
+// 32x32->64 multiply at the end.  Valid for n < 65536 (checked on the host).
+__host__ __device__ __forceinline__ uint64_t binom(uint64_t n64, int k) {
+    const uint32_t n = (uint32_t)n64;
+    if (k == 0) return 1;
+    if (n < (uint32_t)k) return 0;
+    if (k == 1) return n;
+    const uint32_t c2 = (n & 1) ? n * ((n - 1) >> 1) : (n >> 1) * (n - 1);  // < 2^31 for n < 65536
+    if (k == 2) return c2;
+    // C3 = c2 * (n-2) / 3, c2 = 3q + r
+    const uint32_t q2 = c2 / 3u, r2 = c2 - 3u * q2;
+    const uint64_t c3 = (uint64_t)q2 * (n - 2) + (r2 * (n - 2)) / 3u;
+    if (k == 3) return c3;
+    const uint64_t c4 = (c3 >> 2) * (n - 3) + ((uint32_t)(c3 & 3) * (n - 3)) / 4u;
+    if (k == 4) return c4;
+    const uint64_t q4 = c4 / 5u, r4 = c4 - 5u * q4;
+    return q4 * (n - 4) + (r4 * (n - 4)) / 5u;
 }
 
 // largest v in [k-1, top] with C(v, k) <= idx
@@ -114,6 +122,36 @@ __device__ __forceinline__ float sqrt_rn_f32(float x) {
     return f;
 }
 
+// ---------------------------------------------------------------- staging
+// Copy nbytes (multiple of 4) global -> LDS with 16-B loads, 8 in flight per
+// lane before the first LDS store (a single wave otherwise serialises one
+// HBM/L2 round trip per 64 elements).
+__device__ __forceinline__ void stage_to_lds(void* dst, const void* src, size_t nbytes, int t, int T) {
+    const size_t n16 = (((uintptr_t)src | (uintptr_t)dst) & 15) ? 0 : nbytes / 16;
+    const uint4* s4 = (const uint4*)src;
+    uint4* d4 = (uint4*)dst;
+    size_t e = t;
+    for (; e + 7 * (size_t)T < n16; e += 8 * (size_t)T) {
+        uint4 r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = s4[e + u * (size_t)T];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d4[e + u * (size_t)T] = r[u];
+    }
+    for (; e < n16; e += T) d4[e] = s4[e];
+    const uint32_t* s1 = (const uint32_t*)src;
+    uint32_t* d1 = (uint32_t*)dst;
+    size_t w = n16 * 4 + t;
+    for (; w + 7 * (size_t)T < nbytes / 4; w += 8 * (size_t)T) {
+        uint32_t r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = s1[w + u * (size_t)T];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) d1[w + u * (size_t)T] = r[u];
+    }
+    for (; w < nbytes / 4; w += T) d1[w] = s1[w];
+}
+
 // ---------------------------------------------------------------- hashing
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
@@ -121,6 +159,15 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
     x *= 0xc4ceb9fe1a85ec53ull;
     x ^= x >> 33;
+    return x;
+}
+// cheap 32-bit mixer for hash-table slots (keys' low 32 bits are unique)
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
     return x;
 }
 // order-free pair hash; the CPU checker under oracle/ uses the same definition
@@ -155,34 +202,48 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
     uint32_t hi = __shfl((unsigned)(uint32_t)(v >> 32), src, 64);
     return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);
-    return v;
+// Wave-64 reductions with DPP (row_shr 1/2/4/8 + row_bcast15/31, the
+// GFX9 scan pattern) instead of ds_bpermute shuffles: ~6 VALU steps, no LDS
+// round trips.  Call with the whole wave active; every lane gets the result.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWMASK, 0xf, false);
 }
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint64_t o = shfl_xor_u64(v, m);
-        v = o < v ? o : v;
-    }
-    return v;
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t v) {
+    uint32_t lo = dpp32<CTRL, ROWMASK>((uint32_t)old, (uint32_t)v);
+    uint32_t hi = dpp32<CTRL, ROWMASK>((uint32_t)(old >> 32), (uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint64_t o = shfl_xor_u64(v, m);
-        v = o > v ? o : v;
-    }
-    return v;
+__device__ __forceinline__ uint64_t readlane63_u64(uint64_t v) {
+    uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
 }
+#define TDA_WAVE_REDUCE64(OP, ID)                     \
+    v = OP(v, dpp64<0x111, 0xf>(ID, v));              \
+    v = OP(v, dpp64<0x112, 0xf>(ID, v));              \
+    v = OP(v, dpp64<0x114, 0xf>(ID, v));              \
+    v = OP(v, dpp64<0x118, 0xf>(ID, v));              \
+    v = OP(v, dpp64<0x142, 0xa>(ID, v));              \
+    v = OP(v, dpp64<0x143, 0xc>(ID, v));              \
+    return readlane63_u64(v);
+
+__device__ __forceinline__ uint64_t op_min64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint64_t op_max64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint64_t op_add64(uint64_t a, uint64_t b) { return a + b; }
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) { TDA_WAVE_REDUCE64(op_add64, 0ull) }
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) { TDA_WAVE_REDUCE64(op_min64, ~0ull) }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) { TDA_WAVE_REDUCE64(op_max64, 0ull) }
+#undef TDA_WAVE_REDUCE64
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        uint32_t o = __shfl_xor(v, m, 64);
-        v = o < v ? o : v;
-    }
-    return v;
+    v = min(v, dpp32<0x111, 0xf>(~0u, v));
+    v = min(v, dpp32<0x112, 0xf>(~0u, v));
+    v = min(v, dpp32<0x114, 0xf>(~0u, v));
+    v = min(v, dpp32<0x118, 0xf>(~0u, v));
+    v = min(v, dpp32<0x142, 0xa>(~0u, v));
+    v = min(v, dpp32<0x143, 0xc>(~0u, v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 }  // namespace tda

@@ -6,10 +6,10 @@
 //
 //   k_distance      pairwise L2 in FP64, sklearn-f32 rounding   
 //   k_square_dist   condensed/square distance input             (a2' / is_dist)
-//   k_h0            enclosing radius, num_edges, spanning forest, H0 pairs (a3, a4)
+//   k_h0 / k_h0_wave enclosing radius, num_edges, spanning forest, H0 pairs (a3, a4)
 //   k_apparent<d>   column enumeration + apparent-pair test     (a5, parallel part)
 //   k_sort_resid    per-layer sort of the residual columns
-//   k_reduce<d>     Z/2 cohomology reduction of residual columns (a5, serial part)
+//   k_reduce2<d>    Z/2 cohomology reduction of residual columns (a5, serial part; rips_reduce.h)
 //   k_finalize      per-layer emission order of the pairs        (a6)
 //   k_compact       pack all layers' pairs into the host-mapped result
 #pragma once
@@ -32,6 +32,8 @@ struct LayerStats {  // zeroed every call; copied to the host result
     int64_t all_pairs[4];
     int64_t n_columns[4];
     int64_t n_residual[4];
+    int64_t n_adds[4];     // column additions in the serial reduction
+    uint64_t prof[3][8];   // -DTDA_PROFILE builds: cycle counters of k_reduce2 per dim
 };
 enum : int32_t { ERR_RESID_CAP = 1, ERR_PAIR_CAP = 2, ERR_WORK_CAP = 4, ERR_VPOOL_CAP = 8, ERR_OUT_CAP = 16 };
 
@@ -404,6 +406,112 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     }
 }
 
+// Small-N H0 (N <= 64): one wave per layer, distance matrix in LDS, lane v
+// owns vertex v; Prim's frontier keys live in registers, the arg-min vertex is
+// found by ballot (no index decode); the <= 63 forest edges are sorted with an
+// in-register bitonic network.  Same results as k_h0.
+__global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, int n, float user_thresh,
+                                                LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
+                                                uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, v = threadIdx.x;
+    float* D = (float*)smem;              // n*n
+    const float* Dg = dist + (size_t)l * n * n;
+    stage_to_lds(D, Dg, sizeof(float) * n * n, v, 64);
+    __syncthreads();
+    LayerStats* st = stats + l;
+    const bool real = v < n;
+    float thr = user_thresh;
+    if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) {
+        float rm = real ? 0.0f : INFINITY;
+        if (real)
+            for (int j = 0; j < n; ++j) rm = fmaxf(rm, D[v * n + j]);
+        for (int m = 32; m >= 1; m >>= 1) rm = fminf(rm, __shfl_xor(rm, m, 64));
+        thr = rm;
+    }
+    uint64_t ne = 0;
+    if (real)
+        for (int j = v + 1; j < n; ++j) ne += D[v * n + j] <= thr;
+    ne = wave_sum_u64(ne);
+    bool intree = v == 0;
+    uint64_t best = kEmpty64;
+    int cur = 0;
+    uint64_t mykey = kEmpty64;  // forest edge discovered at step == lane
+    int nmst = 0;
+    for (int it = 1; it < n; ++it) {
+        if (real && !intree) {
+            float d = D[cur * n + v];
+            if (d <= thr) {
+                int a = cur > v ? cur : v, bb = cur > v ? v : cur;
+                uint64_t k = filt_key(d, binom((uint64_t)a, 2) + bb);
+                best = k < best ? k : best;
+            }
+        }
+        uint64_t cand = (real && !intree) ? best : kEmpty64;
+        uint64_t m = wave_min_u64(cand);
+        int nv;
+        if (m == kEmpty64) {
+            nv = __builtin_ctzll(__ballot(real && !intree));  // new component
+        } else {
+            nv = __builtin_ctzll(__ballot(real && !intree && cand == m));
+            if (v == nmst) mykey = m;
+            ++nmst;
+        }
+        if (v == nv) intree = true;
+        cur = nv;
+    }
+    // bitonic sort of the forest keys (one per lane, EMPTY padding)
+    uint64_t k = mykey;
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            uint64_t o = shfl_xor_u64(k, stride);
+            bool up = (v & size) == 0;
+            bool lower = (v & stride) == 0;
+            uint64_t lo = o < k ? o : k, hi = o < k ? k : o;
+            k = (lower == up) ? lo : hi;
+        }
+    }
+    // lane e now holds the e-th forest edge in Kruskal order (diam asc, idx desc)
+    const bool has = v < nmst;
+    const uint64_t eidx = has ? 0xFFFFFFFFull - (k & 0xFFFFFFFFull) : 0;
+    const float d = has ? __uint_as_float((uint32_t)(k >> 32)) : 0.0f;
+    int ea = 0, eb = 0;
+    if (has) {
+        ea = max_vertex(eidx, 2, n - 1);
+        eb = (int)(eidx - binom((uint64_t)ea, 2));
+        atomicOr(&mst_bits[(size_t)l * mst_words + (eidx >> 5)], 1u << (eidx & 31));
+    }
+    // elder-rule union-find in registers: lane u holds the label (= max
+    // vertex) of its component; each merge is two readlanes + a select.
+    int label = v;
+    int young_e = -1;
+    for (int e = 0; e < nmst; ++e) {
+        const int a = __builtin_amdgcn_readlane(ea, e), bb = __builtin_amdgcn_readlane(eb, e);
+        const int ra = __builtin_amdgcn_readlane(label, a), rb = __builtin_amdgcn_readlane(label, bb);
+        const int young = ra < rb ? ra : rb, old = ra < rb ? rb : ra;
+        if (label == young) label = old;
+        if (v == e) young_e = young;
+    }
+    // emission: finite bars (d > 0) in Kruskal order, then [0, inf) per root
+    Pair* P = pairs0 + (size_t)l * pcap0;
+    const uint64_t posm = __ballot(has && d > 0.0f);
+    const int nfin = __popcll(posm);
+    if (has && d > 0.0f) P[lanes_below(posm)] = Pair{0.0f, d, (int64_t)young_e, (int64_t)eidx};
+    const uint64_t rootm = __ballot(real && label == v);
+    if (real && label == v) P[nfin + lanes_below(rootm)] = Pair{0.0f, INFINITY, (int64_t)v, -1};
+    const uint64_t cs = wave_sum_u64(has ? pair_hash((uint64_t)young_e, eidx) : 0ull);
+    if (v == 0) {
+        st->thresh = thr;
+        st->num_edges = (int64_t)ne;
+        st->count[0] = nfin + __popcll(rootm);
+        st->checksum[0] = cs;
+        st->all_pairs[0] = nmst;
+        st->n_columns[0] = n;
+    }
+}
+
 // ------------------------------------------------------------------ apparent
 // Parallel part of compute_pairs [upstream]: every d-simplex s <= thresh that
 // is not cleared (an H_{d-1} death) is a column.  Its coboundary pivot (the
@@ -414,11 +522,18 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
 // reduces to: every facet t\{u} with u > v has diam < diam(s).  Apparent
 // pairs are persistence pairs (zero persistence: never emitted), columns with
 // an empty coboundary are essential (emitted here), the rest go to k_reduce.
-template <int DIM>
+template <int DIM, bool DLDS>
 __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
                                                   DimBufs b, Pair* __restrict__ pairs, uint64_t pcap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.y;
     const float* Dl = dist + (size_t)l * n * n;
+    if (DLDS) {  // stage this layer's distance matrix in LDS (N <= 128: <= 64 KB)
+        float* sd = (float*)smem;
+        stage_to_lds(sd, Dl, sizeof(float) * n * n, threadIdx.x, blockDim.x);
+        __syncthreads();
+        Dl = sd;
+    }
     LayerStats* st = stats + l;
     const float r = st->thresh;
     const uint32_t* cleared = b.cleared + (size_t)l * b.cleared_words;
@@ -540,350 +655,6 @@ __global__ __launch_bounds__(1024) void k_sort_resid(LayerStats* __restrict__ st
     for (uint64_t e = threadIdx.x; e < cap; e += blockDim.x) rk[e] = kEmpty64;
 }
 
-// ------------------------------------------------------------------ reduce
-// Serial part of compute_pairs [upstream ripser.cpp compute_pairs /
-// add_coboundary]: the residual columns of one layer, in column order, reduced
-// by ONE wave.  The working coboundary W and the working reduction column V are
-// Z/2 toggle-sets (open addressing, parity bit per slot); the coboundary of a
-// simplex is enumerated wave-parallel (one lane per new vertex); the pivot is a
-// wave min over the live slots.  Pivot owners: residual columns in a global
-// hash map (written by this kernel), apparent columns via the pivot bitmap
-// (owner = youngest facet of the pivot, no lookup table needed).
-struct ReduceBufs {
-    uint64_t* rmap_keys;  // [L][rmap_stride]
-    uint32_t* rmap_vals;
-    uint64_t rmap_stride;
-    uint32_t* voff;       // [L][rcap] offset of V_j in vpool
-    uint32_t* vlen;
-    uint64_t* vpool;      // [L][vpool_cap]
-    uint64_t vpool_cap;
-    // global working tables (used when not in LDS mode)
-    uint64_t* wkeys;
-    float* wdiam;
-    uint32_t* wpar;
-    uint32_t* wlist;
-    uint64_t wcap;        // per layer, pow2
-};
-
-template <bool LDS>
-struct ToggleSet {
-    uint64_t* keys;
-    float* diam;
-    uint32_t* par;
-    uint32_t* list;
-    uint32_t* count;  // LDS scalar
-    uint32_t mask;
-
-    __device__ void clear_all(int t, int T) {
-        for (uint32_t e = t; e <= mask; e += T) {
-            keys[e] = kEmpty64;
-            par[e] = 0;
-        }
-    }
-    // clear only the touched slots (call with all lanes, then sync)
-    __device__ void reset(int t, int T, uint32_t cnt) {
-        for (uint32_t e = t; e < cnt; e += T) {
-            uint32_t s = list[e];
-            keys[s] = kEmpty64;
-            par[s] = 0;
-        }
-    }
-    // toggle key (unique among concurrent callers)
-    __device__ void toggle(uint64_t k, float d) {
-        uint32_t h = (uint32_t)mix64(k) & mask;
-        for (;;) {
-            uint64_t cur = keys[h];
-            if (cur == k) break;
-            if (cur == kEmpty64) {
-                unsigned long long old = atomicCAS((unsigned long long*)&keys[h], (unsigned long long)kEmpty64, (unsigned long long)k);
-                if (old == kEmpty64) {
-                    diam[h] = d;
-                    uint32_t pos = atomicAdd(count, 1u);
-                    list[pos] = h;
-                    break;
-                }
-                if (old == k) break;
-            }
-            h = (h + 1) & mask;
-        }
-        par[h] ^= 1u;
-    }
-};
-
-template <int DIM>
-__device__ __forceinline__ void youngest_facet(const float* __restrict__ D, int n, uint64_t tidx, uint64_t& fidx, float& fd) {
-    int tv[DIM + 2];
-    decode<DIM + 1>(tidx, n, tv);
-    fd = -1.0f;
-    fidx = 0;
-#pragma unroll
-    for (int u = 0; u <= DIM + 1; ++u) {
-        int fv[DIM + 1];
-        int q = 0;
-#pragma unroll
-        for (int i = 0; i <= DIM + 1; ++i)
-            if (i != u) fv[q++] = tv[i];
-        float d = simplex_diam<DIM>(D, n, fv);
-        uint64_t ix = encode<DIM>(fv);
-        if (d > fd || (d == fd && ix < fidx)) {
-            fd = d;
-            fidx = ix;
-        }
-    }
-}
-
-template <int DIM, bool LDS>
-__global__ __launch_bounds__(64) void k_reduce(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats, DimBufs b,
-                                               ReduceBufs rb, Pair* __restrict__ pairs, uint64_t pcap, uint32_t wcap_lds,
-                                               uint32_t vcap_lds, int dist_in_lds) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, ln = threadIdx.x;
-    LayerStats* st = stats + l;
-    const float r = st->thresh;
-    uint64_t nres = (uint64_t)st->n_residual[DIM];
-    if (nres > b.rcap) nres = b.rcap;
-    if (nres == 0) return;
-    const uint64_t* resid = b.resid + (size_t)l * b.rcap;
-    uint32_t* piv = b.pivbits + (size_t)l * b.piv_words;
-
-    // carve LDS (all scratch in the dynamic region, 16-B aligned)
-    uint32_t& wcount = *(uint32_t*)smem;
-    uint32_t& vcount = *(uint32_t*)(smem + 4);
-    uint32_t& s_err = *(uint32_t*)(smem + 8);
-    unsigned char* p = smem + 16;
-    ToggleSet<LDS> W, V;
-    uint32_t wcap, vcap;
-    if (LDS) {
-        wcap = wcap_lds;
-        vcap = vcap_lds;
-        W.keys = (uint64_t*)p; p += sizeof(uint64_t) * wcap;
-        V.keys = (uint64_t*)p; p += sizeof(uint64_t) * vcap;
-        W.diam = (float*)p; p += sizeof(float) * wcap;
-        W.par = (uint32_t*)p; p += sizeof(uint32_t) * wcap;
-        W.list = (uint32_t*)p; p += sizeof(uint32_t) * wcap;
-        V.diam = (float*)p; p += sizeof(float) * vcap;
-        V.par = (uint32_t*)p; p += sizeof(uint32_t) * vcap;
-        V.list = (uint32_t*)p; p += sizeof(uint32_t) * vcap;
-    } else {
-        wcap = (uint32_t)rb.wcap;
-        vcap = vcap_lds;
-        W.keys = rb.wkeys + (size_t)l * wcap;
-        W.diam = rb.wdiam + (size_t)l * wcap;
-        W.par = rb.wpar + (size_t)l * wcap;
-        W.list = rb.wlist + (size_t)l * wcap;
-        V.keys = (uint64_t*)p; p += sizeof(uint64_t) * vcap;
-        V.diam = (float*)p; p += sizeof(float) * vcap;
-        V.par = (uint32_t*)p; p += sizeof(uint32_t) * vcap;
-        V.list = (uint32_t*)p; p += sizeof(uint32_t) * vcap;
-    }
-    const float* D = dist + (size_t)l * n * n;
-    if (dist_in_lds) {
-        float* dl = (float*)p;
-        for (int e = ln; e < n * n; e += 64) dl[e] = D[e];
-        D = dl;
-    }
-    W.mask = wcap - 1;
-    V.mask = vcap - 1;
-    W.count = &wcount;
-    V.count = &vcount;
-    W.clear_all(ln, 64);
-    V.clear_all(ln, 64);
-    if (ln == 0) {
-        wcount = 0;
-        vcount = 0;
-        s_err = 0;
-    }
-    __syncthreads();
-
-    uint64_t* rk = rb.rmap_keys + (size_t)l * rb.rmap_stride;
-    uint32_t* rvl = rb.rmap_vals + (size_t)l * rb.rmap_stride;
-    uint64_t rcap2 = 16;
-    while (rcap2 < 2 * nres + 16) rcap2 <<= 1;
-    if (rcap2 > rb.rmap_stride) rcap2 = rb.rmap_stride;
-    const uint64_t rmask = rcap2 - 1;
-    uint32_t* voff = rb.voff + (size_t)l * b.rcap;
-    uint32_t* vlen = rb.vlen + (size_t)l * b.rcap;
-    uint64_t* vpool = rb.vpool + (size_t)l * rb.vpool_cap;
-    uint64_t vused = 0;  // uniform
-    Pair* P = pairs + (size_t)l * pcap;
-    uint64_t cs = 0, npairs = 0;
-
-    // toggle the coboundary of simplex s (diam sd) into W: one pass
-    auto add_cob = [&](uint64_t s, float sd) {
-        if (wcount + (uint32_t)n > (wcap >> 1) + (wcap >> 2)) {
-            __syncthreads();
-            if (ln == 0) s_err = 1;
-            __syncthreads();
-            return;
-        }
-        int vs[DIM + 1];
-        decode<DIM>(s, n, vs);
-        for (int v = ln; v < n; v += 64) {
-            bool mem = false;
-#pragma unroll
-            for (int i = 0; i <= DIM; ++i) mem |= (vs[i] == v);
-            if (mem) continue;
-            float cd = sd;
-            const float* row = D + (size_t)v * n;
-#pragma unroll
-            for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, row[vs[i]]);
-            if (cd <= r) W.toggle(cofacet_index<DIM>(vs, v), cd);
-        }
-        __syncthreads();
-    };
-    auto vtoggle = [&](uint64_t s) {
-        if (vcount + 2 > (vcap >> 1) + (vcap >> 2)) {
-            __syncthreads();
-            if (ln == 0) s_err = 1;
-            __syncthreads();
-            return;
-        }
-        if (ln == 0) V.toggle(s, 0.0f);
-        __syncthreads();
-    };
-
-    for (uint64_t j = 0; j < nres; ++j) {
-        const uint64_t key = resid[j];
-        const uint64_t sidx = key_idx(key);
-        const float sdm = key_diam(key);
-        add_cob(sidx, sdm);
-        bool done = false;
-        while (!done) {
-            if (s_err) break;
-            // pivot: min diam, then max index, over live slots
-            const uint32_t cnt = wcount;
-            float bd = INFINITY;
-            uint64_t bi = 0;
-            bool has = false;
-            for (uint32_t e = ln; e < cnt; e += 64) {
-                uint32_t sl = W.list[e];
-                if (W.par[sl]) {
-                    float d = W.diam[sl];
-                    uint64_t k = W.keys[sl];
-                    if (!has || d < bd || (d == bd && k > bi)) {
-                        bd = d;
-                        bi = k;
-                        has = true;
-                    }
-                }
-            }
-            uint32_t db = has ? __float_as_uint(bd) : 0xFFFFFFFFu;
-            uint32_t dmin = wave_min_u32(db);
-            uint64_t cand = (has && db == dmin) ? bi : 0;
-            uint64_t imax = wave_max_u64(cand);
-            bool anyw = dmin != 0xFFFFFFFFu;
-            if (!anyw) {
-                // zero column: essential class
-                if (ln == 0) {
-                    uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-                    if (pos < pcap) P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
-                    else atomicOr(&st->err, ERR_PAIR_CAP);
-                    voff[j] = 0;
-                    vlen[j] = 0;
-                }
-                done = true;
-                break;
-            }
-            const float pd = __uint_as_float(dmin);
-            const uint64_t pidx = imax;
-            // owner lookup (lane 0)
-            int64_t owner = -1;
-            if (ln == 0) {
-                uint64_t h = mix64(pidx) & rmask;
-                while (rk[h] != kEmpty64) {
-                    if (rk[h] == pidx) {
-                        owner = rvl[h];
-                        break;
-                    }
-                    h = (h + 1) & rmask;
-                }
-            }
-            owner = (int64_t)shfl_u64((uint64_t)owner, 0);
-            if (owner >= 0) {
-                const uint64_t ok = resid[owner];
-                add_cob(key_idx(ok), key_diam(ok));
-                vtoggle(key_idx(ok));
-                const uint32_t o0 = voff[owner], ol = vlen[owner];
-                for (uint32_t q = 0; q < ol; ++q) {
-                    uint64_t s = vpool[o0 + q];
-                    int vs[DIM + 1];
-                    decode<DIM>(s, n, vs);
-                    add_cob(s, simplex_diam<DIM>(D, n, vs));
-                    vtoggle(s);
-                }
-            } else if ((piv[pidx >> 5] >> (pidx & 31)) & 1u) {
-                uint64_t fidx;
-                float fd;
-                youngest_facet<DIM>(D, n, pidx, fidx, fd);
-                add_cob(fidx, fd);
-                vtoggle(fidx);
-            } else {
-                // new pair (sigma_j, pivot)
-                if (ln == 0) {
-                    if (pd > sdm) {
-                        uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-                        if (pos < pcap) P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
-                        else atomicOr(&st->err, ERR_PAIR_CAP);
-                    }
-                    uint64_t h = mix64(pidx) & rmask;
-                    while (rk[h] != kEmpty64) h = (h + 1) & rmask;
-                    rk[h] = pidx;
-                    rvl[h] = (uint32_t)j;
-                    atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
-                }
-                cs += pair_hash(sidx, pidx);
-                npairs += 1;
-                // store V_j (live entries of V)
-                const uint32_t vc = vcount;
-                uint64_t wr = 0;
-                for (uint32_t e0 = 0; e0 < vc; e0 += 64) {
-                    uint32_t e = e0 + ln;
-                    bool live = false;
-                    uint64_t k = 0;
-                    if (e < vc) {
-                        uint32_t sl = V.list[e];
-                        live = V.par[sl] != 0;
-                        k = V.keys[sl];
-                    }
-                    uint64_t m = __ballot(live);
-                    if (live) {
-                        uint64_t pos = vused + wr + lanes_below(m);
-                        if (pos < rb.vpool_cap) vpool[pos] = k;
-                    }
-                    wr += __popcll(m);
-                }
-                if (vused + wr > rb.vpool_cap) {
-                    if (ln == 0) s_err = 2;
-                    wr = 0;
-                }
-                if (ln == 0) {
-                    voff[j] = (uint32_t)vused;
-                    vlen[j] = (uint32_t)wr;
-                }
-                vused += wr;
-                done = true;
-            }
-        }
-        __syncthreads();
-        if (s_err) break;
-        // reset the tables for the next column
-        W.reset(ln, 64, wcount);
-        V.reset(ln, 64, vcount);
-        __syncthreads();
-        if (ln == 0) {
-            wcount = 0;
-            vcount = 0;
-        }
-        __syncthreads();
-    }
-    if (ln == 0) {
-        if (s_err == 1) atomicOr(&st->err, ERR_WORK_CAP);
-        if (s_err == 2) atomicOr(&st->err, ERR_VPOOL_CAP);
-        atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)cs);
-        atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)npairs);
-    }
-}
-
 // ------------------------------------------------------------------ finalize
 // Emission order of dims >= 1 (reference: births_and_deaths_by_dim filled in
 // column order, i.e. birth desc / column index asc; pinned 32/32 by
@@ -927,31 +698,33 @@ struct OutPair {
 __global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats, int L, int maxdim, Pair* const* __restrict__ pairs,
                                                   const uint64_t* __restrict__ pcap, int64_t* __restrict__ out_off,
                                                   OutPair* __restrict__ out, uint64_t out_cap) {
-    __shared__ int64_t s_total;
-    const int nd = maxdim + 1;
-    if (threadIdx.x == 0) {
-        int64_t acc = 0;
-        for (int l = 0; l < L; ++l)
-            for (int d = 0; d < nd; ++d) {
-                int64_t c = stats[l].count[d];
-                if ((uint64_t)c > pcap[d]) c = (int64_t)pcap[d];
-                out_off[l * nd + d] = acc;
-                acc += c;
-            }
-        s_total = acc;
-        if ((uint64_t)acc > out_cap)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int64_t* off = (int64_t*)smem;  // L*nd + 1
+    const int nd = maxdim + 1, S = L * nd, t = threadIdx.x;
+    for (int i = t; i < S; i += blockDim.x) {
+        int l = i / nd, d = i % nd;
+        int64_t c = stats[l].count[d];
+        if ((uint64_t)c > pcap[d]) c = (int64_t)pcap[d];
+        off[i + 1] = c;
+    }
+    __syncthreads();
+    if (t == 0) {
+        off[0] = 0;
+        for (int i = 1; i <= S; ++i) off[i] += off[i - 1];
+        if ((uint64_t)off[S] > out_cap)
             for (int l = 0; l < L; ++l) stats[l].err |= ERR_OUT_CAP;
     }
     __syncthreads();
-    if ((uint64_t)s_total > out_cap) return;
-    for (int l = 0; l < L; ++l)
-        for (int d = 0; d < nd; ++d) {
-            int64_t c = stats[l].count[d];
-            if ((uint64_t)c > pcap[d]) c = (int64_t)pcap[d];
-            const Pair* P = pairs[d] + (size_t)l * pcap[d];
-            OutPair* o = out + out_off[l * nd + d];
-            for (int64_t e = threadIdx.x; e < c; e += blockDim.x) o[e] = OutPair{P[e].birth, P[e].death, P[e].birth_idx, P[e].death_idx};
-        }
+    for (int i = t; i < S; i += blockDim.x) out_off[i] = off[i];
+    if ((uint64_t)off[S] > out_cap) return;
+    const int w = t >> 6, ln = t & 63, nw = blockDim.x >> 6;
+    for (int i = w; i < S; i += nw) {
+        const int l = i / nd, d = i % nd;
+        const int64_t c = off[i + 1] - off[i];
+        const Pair* P = pairs[d] + (size_t)l * pcap[d];
+        OutPair* o = out + off[i];
+        for (int64_t e = ln; e < c; e += 64) o[e] = OutPair{P[e].birth, P[e].death, P[e].birth_idx, P[e].death_idx};
+    }
 }
 
 }  // namespace tda

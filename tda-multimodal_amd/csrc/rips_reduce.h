@@ -1,0 +1,535 @@
+// rips_reduce.h -- serial part of the cohomology reduction on gfx950.
+//
+// [upstream ripser.cpp compute_pairs / add_coboundary / get_pivot]: the
+// residual (non-apparent) columns of one layer are reduced in column order by
+// ONE wave (64 lanes, no cross-wave barriers).  The run time is a dependency
+// chain of pivot steps (one column addition each), so every step is built to
+// issue few dependent LDS round trips:
+//   * working coboundary W: Z/2 toggle-set of u64 filtration keys
+//     (diam_bits << 32 | ~lo32), pivot = plain u64 wave-min (DPP).  lo32 is
+//     the row simplex's PACKED vertex tuple when it fits 32 bits (colex order
+//     == lexicographic order of descending vertex tuples, so the key order is
+//     Ripser's (diam asc, index desc)); the pivot's vertices are then shifts,
+//     not a combinatorial decode.  Otherwise lo32 is the index itself.
+//   * W layout: insertion-ordered key log (parity = bit 63 of the entry) +
+//     64-bit index (lo32 << 32 | log pos + 1): a pivot scan is a bare u64 min
+//     over the log with 16-B loads, a toggle is one index read + one CAS (or
+//     one 64-bit XOR); the log length lives in a wave-uniform register, so
+//     reservations need no LDS atomics;
+//   * a residual column's reduced coboundary R_j is stored explicitly (HBM
+//     pool) when it pairs; re-adding it is one toggle pass over |R_j| keys
+//     (Ripser keeps V_j instead and re-enumerates every coboundary);
+//   * apparent columns are re-added implicitly: the owner of an apparent pivot
+//     is its youngest facet (pivot bitmap from k_apparent), whose coboundary
+//     is enumerated wave-parallel (one lane per new vertex, reading the
+//     symmetric distance matrix column-wise: conflict-free LDS access);
+//   * distance matrix, pivot bitmap and the residual pivot map live in LDS.
+#pragma once
+#include "rips_kernels.h"
+
+namespace tda {
+
+#ifdef TDA_PROFILE
+#define TDA_STAMP(var) const uint64_t var = clock64()
+#define TDA_ACC(i, t0) prof[i] += clock64() - (t0)
+#else
+#define TDA_STAMP(var)
+#define TDA_ACC(i, t0)
+#endif
+
+// wave-parallel decode: all 64 lanes cooperate, every lane gets the result
+template <int DIM>
+__device__ __forceinline__ void decode_wave(uint64_t idx, int n, int (&vs)[DIM + 1], int ln) {
+    int top = n - 1;
+#pragma unroll
+    for (int k = DIM + 1; k >= 1; --k) {
+        int v = k - 1;
+        for (int base = top;; base -= 64) {
+            int cand = base - ln;
+            bool ok = cand >= k - 1 && binom((uint64_t)cand, k) <= idx;
+            uint64_t m = __ballot(ok);
+            if (m) {
+                v = base - __builtin_ctzll(m);
+                break;
+            }
+            if (base - 63 <= k - 1) break;
+        }
+        vs[DIM + 1 - k] = v;
+        idx -= binom((uint64_t)v, k);
+        top = v - 1;
+    }
+}
+
+// row-simplex key payload: packed descending vertices
+template <int NV>
+struct RowLo {
+    static constexpr int B = NV == 3 ? 10 : 8;  // triangles: N <= 1024, tetrahedra: N <= 256
+    __device__ static uint32_t pack(const int (&t)[NV]) {
+        uint32_t h = 0;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) h = (h << B) | (uint32_t)t[i];
+        return h;
+    }
+    __device__ static void unpack(uint32_t h, int (&t)[NV]) {
+#pragma unroll
+        for (int i = NV - 1; i >= 0; --i) {
+            t[i] = (int)(h & ((1u << B) - 1));
+            h >>= B;
+        }
+    }
+};
+
+// ---------------------------------------------------------------- toggle set
+// Z/2 set of u64 keys for ONE wave: key log (insertion order) + open-
+// addressing index (entry = lo32 << 32 | pos + 1).  A key's parity lives in
+// bit 63 of its log entry (keys have bit 63 clear: non-negative f32 diameter
+// bits), set = dead, so a dead entry is never the minimum and a pivot scan is
+// a bare u64 min over the log (16-B loads, no side table).  toggle_pass()
+// toggles one set of DISTINCT keys with the whole wave; new keys take
+// consecutive log positions [cnt, cnt + new) from the wave-uniform counter.
+constexpr uint64_t kDead = 1ull << 63;
+struct KeySet {
+    uint64_t* index;  // icap entries, 0 = free
+    uint64_t* log;    // cap keys (| kDead when cancelled)
+    uint64_t* tmp;    // scratch >= 2 * cap keys (HBM)
+    uint32_t imask;   // icap - 1
+    uint32_t cnt;     // log length (wave-uniform register)
+
+    __device__ __forceinline__ void toggle_pass(uint64_t k, bool valid, int ln) {
+        const uint32_t fp = (uint32_t)k;
+        uint32_t h = mix32(fp) & imask;
+        uint32_t mine = 0;  // reserved log position + 1
+        bool pending = valid;
+        while (__ballot(pending)) {
+            bool want = false;
+            if (pending) {
+                const uint64_t cur = index[h];
+                if (cur == 0) {
+                    want = true;
+                } else if ((uint32_t)(cur >> 32) == fp) {
+                    atomicXor((unsigned long long*)&log[(uint32_t)cur - 1], (unsigned long long)kDead);  // flip parity
+                    pending = false;
+                } else {
+                    h = (h + 1) & imask;
+                }
+            }
+            const uint64_t need = __ballot(want && !mine);
+            if (want && !mine) {
+                mine = cnt + lanes_below(need) + 1;
+                log[mine - 1] = k;  // new entry: live
+            }
+            cnt += (uint32_t)__popcll(need);
+            if (want) {
+                const unsigned long long nv = ((unsigned long long)fp << 32) | mine;
+                if (atomicCAS((unsigned long long*)&index[h], 0ull, nv) == 0ull)
+                    pending = false;
+                else
+                    h = (h + 1) & imask;  // lost the slot to another key
+            }
+        }
+    }
+    // zero the index, cnt = 0 (whole wave)
+    __device__ void reset(int ln) {
+        const uint32_t c = cnt;
+        if (c * 4 >= imask) {
+            for (uint32_t e = ln; e <= imask; e += 64) index[e] = 0;
+        } else {
+            // probe each logged key's slot, then zero (two phases)
+            uint32_t* slots = (uint32_t*)tmp;
+            for (uint32_t e = ln; e < c; e += 64) {
+                const uint32_t fp = (uint32_t)log[e];
+                uint32_t h = mix32(fp) & imask;
+                for (;;) {
+                    const uint64_t cur = index[h];
+                    if (cur == 0 || (uint32_t)(cur >> 32) == fp) break;
+                    h = (h + 1) & imask;
+                }
+                slots[e] = h;
+            }
+            __syncthreads();
+            for (uint32_t e = ln; e < c; e += 64) index[slots[e]] = 0;
+        }
+        cnt = 0;
+        __syncthreads();
+    }
+    // min live key + live count (wave-uniform)
+    __device__ void scan(int ln, uint64_t& best, uint32_t& nlive) const {
+        const uint32_t c = cnt;
+        uint64_t b = kEmpty64;
+        uint32_t nl = 0;
+        uint32_t e = 2 * ln;
+        for (; e + 384 + 1 < c; e += 512) {  // 4 x 16-B loads in flight
+            const ulonglong2 a0 = *(const ulonglong2*)&log[e], a1 = *(const ulonglong2*)&log[e + 128];
+            const ulonglong2 a2 = *(const ulonglong2*)&log[e + 256], a3 = *(const ulonglong2*)&log[e + 384];
+            nl += (a0.x < kDead) + (a0.y < kDead) + (a1.x < kDead) + (a1.y < kDead) + (a2.x < kDead) + (a2.y < kDead) +
+                  (a3.x < kDead) + (a3.y < kDead);
+            uint64_t m0 = a0.x < a0.y ? a0.x : a0.y, m1 = a1.x < a1.y ? a1.x : a1.y;
+            uint64_t m2 = a2.x < a2.y ? a2.x : a2.y, m3 = a3.x < a3.y ? a3.x : a3.y;
+            m0 = m0 < m1 ? m0 : m1;
+            m2 = m2 < m3 ? m2 : m3;
+            m0 = m0 < m2 ? m0 : m2;
+            b = m0 < b ? m0 : b;
+        }
+        for (; e < c; e += 128) {
+            const uint64_t k0 = log[e];
+            const uint64_t k1 = e + 1 < c ? log[e + 1] : kEmpty64;
+            nl += (k0 < kDead) + (k1 < kDead);
+            const uint64_t m = k0 < k1 ? k0 : k1;
+            b = m < b ? m : b;
+        }
+        b = b < kDead ? b : kEmpty64;
+        best = wave_min_u64(b);
+        nlive = (uint32_t)wave_sum_u64(nl);
+    }
+    // write the live keys to out[] (whole wave), returns how many
+    __device__ uint32_t gather_live(int ln, uint64_t* out) const {
+        const uint32_t c = cnt;
+        uint32_t pos = 0;
+        for (uint32_t e0 = 0; e0 < c; e0 += 64) {
+            uint32_t e = e0 + ln;
+            const uint64_t k = e < c ? log[e] : kEmpty64;
+            const bool lv = k < kDead;
+            uint64_t m = __ballot(lv);
+            if (lv) out[pos + lanes_below(m)] = k;
+            pos += (uint32_t)__popcll(m);
+        }
+        return pos;
+    }
+    // keep only live keys (whole wave)
+    __device__ void compact(int ln) {
+        uint64_t* kept = tmp + (imask + 1) / 2;  // after the slot scratch
+        const uint32_t pos = gather_live(ln, kept);
+        __syncthreads();
+        reset(ln);
+        for (uint32_t e0 = 0; e0 < pos; e0 += 64) {
+            const uint32_t e = e0 + ln;
+            toggle_pass(e < pos ? kept[e] : 0, e < pos, ln);
+        }
+        __syncthreads();
+    }
+};
+
+struct Reduce2Bufs {
+    uint64_t* rmap_keys;  // [L][rmap_stride] (when the map does not fit LDS)
+    uint32_t* rmap_vals;
+    uint64_t rmap_stride;
+    uint64_t* roff;       // [L][rcap] offset of R_j in rpool
+    uint32_t* rlen;       // [L][rcap]
+    uint64_t* rpool;      // [L][rpool_cap] reduced coboundary keys
+    uint64_t rpool_cap;
+    uint64_t* wtmp;       // [L][wtmp_stride] scratch
+    uint64_t wtmp_stride;
+    // global working tables (global mode)
+    uint64_t* windex;  // [L][2 wcap]
+    uint64_t* wlog;    // [L][wcap]
+    uint64_t wcap;
+};
+
+struct Reduce2Cfg {  // LDS carve, decided on the host
+    uint32_t wcap, rmap_lds_cap;  // rmap_lds_cap = 0 -> global map
+    int dist_lds, piv_lds;
+    uint32_t bytes;
+};
+
+enum : int32_t { ERR_LDS_SPILL = 32 };
+
+template <int DIM, bool LDSW, bool PACKED>
+__global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats, DimBufs b,
+                                                Reduce2Bufs rb, Reduce2Cfg cfg, Pair* __restrict__ pairs, uint64_t pcap) {
+    constexpr int NV = DIM + 2;  // vertices of a row simplex
+    using Lo = RowLo<NV>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, ln = threadIdx.x;
+    LayerStats* st = stats + l;
+    const float r = st->thresh;
+    uint64_t nres = (uint64_t)st->n_residual[DIM];
+    if (nres > b.rcap) nres = b.rcap;
+    if (nres == 0) return;
+    const uint64_t* resid = b.resid + (size_t)l * b.rcap;
+    uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
+
+    // ---- LDS carve (16-B aligned pieces)
+    unsigned char* p = smem + 16;
+    KeySet W;
+    auto take = [&](size_t bytes) {
+        unsigned char* q = p;
+        p += (bytes + 15) & ~(size_t)15;
+        return q;
+    };
+    uint32_t wcap;
+    if (LDSW) {
+        wcap = cfg.wcap;
+        W.log = (uint64_t*)take(8ull * wcap);
+        W.index = (uint64_t*)take(16ull * wcap);
+    } else {
+        wcap = (uint32_t)rb.wcap;
+        W.log = rb.wlog + (size_t)l * wcap;
+        W.index = rb.windex + (size_t)l * 2 * wcap;
+    }
+    W.tmp = rb.wtmp + (size_t)l * rb.wtmp_stride;
+    W.imask = 2 * wcap - 1;
+    W.cnt = 0;
+    // residual pivot map (keyed by the row payload lo32)
+    uint64_t rcap2 = 16;
+    while (rcap2 < 2 * nres + 16) rcap2 <<= 1;
+    uint64_t* rk;
+    uint32_t* rv;
+    if (cfg.rmap_lds_cap && rcap2 <= cfg.rmap_lds_cap) {
+        rcap2 = cfg.rmap_lds_cap;
+        rk = (uint64_t*)take(8ull * rcap2);
+        rv = (uint32_t*)take(4ull * rcap2);
+        for (uint64_t e = ln; e < rcap2; e += 64) rk[e] = kEmpty64;
+    } else {
+        if (cfg.rmap_lds_cap) {
+            take(8ull * cfg.rmap_lds_cap);
+            take(4ull * cfg.rmap_lds_cap);
+        }
+        if (rcap2 > rb.rmap_stride) rcap2 = rb.rmap_stride;
+        rk = rb.rmap_keys + (size_t)l * rb.rmap_stride;  // cleared by k_sort_resid
+        rv = rb.rmap_vals + (size_t)l * rb.rmap_stride;
+    }
+    const uint64_t rmask = rcap2 - 1;
+    const float* D = dist + (size_t)l * n * n;
+    if (cfg.dist_lds) {
+        float* dl = (float*)take(4ull * n * n);
+        stage_to_lds(dl, D, 4ull * n * n, ln, 64);
+        D = dl;
+    }
+    uint32_t* piv = pivg;
+    if (cfg.piv_lds) {
+        uint32_t* pl = (uint32_t*)take(4ull * b.piv_words);
+        stage_to_lds(pl, pivg, 4ull * b.piv_words, ln, 64);
+        piv = pl;
+    }
+    if (LDSW) {  // global-mode tables are zeroed by the host (hipMemsetAsync)
+        for (uint32_t e = ln; e <= W.imask; e += 64) W.index[e] = 0;
+    }
+    __syncthreads();
+
+    uint64_t* roff = rb.roff + (size_t)l * b.rcap;
+    uint32_t* rlen = rb.rlen + (size_t)l * b.rcap;
+    uint64_t* rpool = rb.rpool + (size_t)l * rb.rpool_cap;
+    uint64_t rused = 0;
+    Pair* P = pairs + (size_t)l * pcap;
+    uint64_t cs = 0, npairs = 0, nadds = 0;
+    int err = 0;  // wave-uniform
+#ifdef TDA_PROFILE
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // scan, lookup, facet, cob-app, cob-res, reset, compact, total
+    const uint64_t t_all = clock64();
+#endif
+    const uint32_t wlim = (wcap >> 1) + (wcap >> 2);
+
+    // make room for `need` new log entries; false on overflow
+    auto room = [&](uint32_t need) -> bool {
+        if (W.cnt + need <= wlim) return true;
+        W.compact(ln);
+        if (W.cnt + need <= wlim) return true;
+        err = 1;
+        return false;
+    };
+    // toggle the coboundary of the simplex with vertices vs (diam sd) into W
+    auto cob = [&](const int (&vs)[DIM + 1], float sd) {
+        for (int v0 = 0; v0 < n; v0 += 64) {
+            const int v = v0 + ln;
+            bool ok = v < n;
+#pragma unroll
+            for (int i = 0; i <= DIM; ++i) ok &= (vs[i] != v);
+            float cd = sd;
+            uint64_t key = 0;
+            if (ok) {
+#pragma unroll
+                for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, D[(size_t)vs[i] * n + v]);  // D symmetric: column read
+                ok = cd <= r;
+                uint32_t lo;
+                if (PACKED) {
+                    int t[NV];
+                    int q = 0;
+                    bool placed = false;
+#pragma unroll
+                    for (int i = 0; i <= DIM; ++i) {
+                        if (!placed && v > vs[i]) {
+                            t[q++] = v;
+                            placed = true;
+                        }
+                        t[q++] = vs[i];
+                    }
+                    if (!placed) t[NV - 1] = v;
+                    lo = Lo::pack(t);
+                } else {
+                    lo = (uint32_t)cofacet_index<DIM>(vs, v);
+                }
+                key = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | (0xFFFFFFFFu - lo);
+            }
+            W.toggle_pass(key, ok, ln);
+        }
+    };
+
+    for (uint64_t j = 0; j < nres && !err; ++j) {
+        const uint64_t key = resid[j];
+        const uint64_t sidx = key_idx(key);
+        const float sdm = key_diam(key);
+        int vs[DIM + 1];
+        decode_wave<DIM>(sidx, n, vs, ln);
+        if (!room((uint32_t)n)) break;
+        cob(vs, sdm);
+        __syncthreads();
+        for (;;) {
+            uint64_t pk;
+            uint32_t nlive;
+            TDA_STAMP(t0);
+            W.scan(ln, pk, nlive);
+            TDA_ACC(0, t0);
+            if (W.cnt > 2 * nlive + 256) {
+                TDA_STAMP(t6);
+                W.compact(ln);
+                TDA_ACC(6, t6);
+            }
+            if (pk == kEmpty64) {
+                // zero column: essential class (birth = diam sigma_j)
+                if (ln == 0) {
+                    uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
+                    if (pos < pcap)
+                        P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
+                    else
+                        atomicOr(&st->err, ERR_PAIR_CAP);
+                    rlen[j] = 0;
+                }
+                break;
+            }
+            TDA_STAMP(t1);
+            const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
+            const float pd = __uint_as_float((uint32_t)(pk >> 32));
+            int t[NV];
+            uint64_t pidx;
+            if (PACKED) {
+                Lo::unpack(plo, t);
+                pidx = encode<DIM + 1>(t);
+            } else {
+                pidx = plo;
+                decode_wave<DIM + 1>(pidx, n, t, ln);
+            }
+            // owner lookup: 64 consecutive probe slots per round, ballot
+            const bool app = (piv[pidx >> 5] >> (pidx & 31)) & 1u;
+            int64_t owner = -1;
+            for (uint64_t h0 = mix32(plo);; h0 += 64) {
+                const uint64_t kk = rk[(h0 + ln) & rmask];
+                const uint64_t mhit = __ballot(kk == plo), mend = __ballot(kk == kEmpty64);
+                const uint64_t below_end = mend ? ((mend & (~mend + 1)) - 1) : ~0ull;
+                if (mhit & below_end) {
+                    owner = (int64_t)rv[(h0 + __builtin_ctzll(mhit & below_end)) & rmask];
+                    break;
+                }
+                if (mend) break;
+            }
+            TDA_ACC(1, t1);
+            TDA_STAMP(t2);
+            if (owner >= 0) {
+                // add the stored reduced column R_owner
+                const uint64_t o0 = roff[owner];
+                const uint32_t ol = rlen[owner];
+                if (!room(ol)) break;
+                for (uint32_t e0 = 0; e0 < ol; e0 += 8 * 64) {
+                    uint64_t rk8[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const uint32_t e = e0 + u * 64 + ln;
+                        rk8[u] = e < ol ? rpool[o0 + e] : 0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (e0 + u * 64 >= ol) break;
+                        W.toggle_pass(rk8[u], e0 + u * 64 + ln < ol, ln);
+                    }
+                }
+                ++nadds;
+                TDA_ACC(4, t2);
+            } else if (app) {
+                // apparent pair (phi, pivot): phi = youngest facet of the pivot,
+                // i.e. max diameter, ties -> smallest index = smallest u (the
+                // facet dropping t[u] grows in colex order with u)
+                float dd[NV][NV];
+#pragma unroll
+                for (int i = 0; i < NV; ++i)
+#pragma unroll
+                    for (int k = i + 1; k < NV; ++k) dd[i][k] = D[(size_t)t[i] * n + t[k]];
+                float fd = -1.0f;
+                int fu = 0;
+#pragma unroll
+                for (int u = 0; u < NV; ++u) {
+                    float d = 0.0f;
+#pragma unroll
+                    for (int i = 0; i < NV; ++i)
+#pragma unroll
+                        for (int k = i + 1; k < NV; ++k)
+                            if (i != u && k != u) d = fmaxf(d, dd[i][k]);
+                    if (d > fd) {
+                        fd = d;
+                        fu = u;
+                    }
+                }
+                int fv[DIM + 1];
+#pragma unroll
+                for (int u = 0; u < NV; ++u) {
+                    if (u != fu) continue;
+#pragma unroll
+                    for (int i = 0, q = 0; i < NV; ++i)
+                        if (i != u) fv[q++] = t[i];
+                }
+                TDA_ACC(2, t2);
+                TDA_STAMP(t3);
+                if (!room((uint32_t)n)) break;
+                cob(fv, fd);
+                ++nadds;
+                TDA_ACC(3, t3);
+            } else {
+                // new persistence pair (sigma_j, pivot); R_j = live keys of W
+                if (ln == 0) {
+                    if (pd > sdm) {
+                        uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
+                        if (pos < pcap)
+                            P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
+                        else
+                            atomicOr(&st->err, ERR_PAIR_CAP);
+                    }
+                    uint64_t h = mix32(plo) & rmask;
+                    while (rk[h] != kEmpty64) h = (h + 1) & rmask;
+                    rk[h] = plo;
+                    rv[h] = (uint32_t)j;
+                    atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
+                    if (piv != pivg) atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
+                }
+                cs += pair_hash(sidx, pidx);
+                npairs += 1;
+                if (rused + nlive > rb.rpool_cap) {
+                    err = 2;
+                    break;
+                }
+                const uint32_t wr = W.gather_live(ln, rpool + rused);
+                if (ln == 0) {
+                    roff[j] = rused;
+                    rlen[j] = wr;
+                }
+                rused += wr;
+                break;
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+        TDA_STAMP(t5);
+        W.reset(ln);
+        TDA_ACC(5, t5);
+    }
+    if (ln == 0) {
+        if (err == 1) atomicOr(&st->err, LDSW ? (int32_t)ERR_LDS_SPILL : (int32_t)ERR_WORK_CAP);
+        if (err == 2) atomicOr(&st->err, ERR_VPOOL_CAP);
+        atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)cs);
+        atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)npairs);
+        atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)nadds);
+#ifdef TDA_PROFILE
+        prof[7] = clock64() - t_all;
+        for (int i = 0; i < 8; ++i) st->prof[DIM][i] = prof[i];
+#endif
+    }
+}
+
+}  // namespace tda

@@ -37,6 +37,7 @@ class LayerResult:
     n_all_pairs: list = field(default_factory=list)
     n_columns: list = field(default_factory=list)
     n_residual: list = field(default_factory=list)
+    n_adds: list = field(default_factory=list)
     dist: np.ndarray | None = None
 
 
@@ -61,6 +62,7 @@ def _unpack(res_p, want_dist: bool) -> tuple[list, float]:
     na = np.ctypeslib.as_array(r.n_all_pairs, shape=(L * nd,)).copy()
     nc = np.ctypeslib.as_array(r.n_columns, shape=(L * nd,)).copy()
     nr = np.ctypeslib.as_array(r.n_residual, shape=(L * nd,)).copy()
+    na2 = np.ctypeslib.as_array(r.n_adds, shape=(L * nd,)).copy()
     dist = None
     if want_dist and bool(r.dist):
         dist = np.ctypeslib.as_array(r.dist, shape=(L, N, N)).copy()
@@ -78,6 +80,7 @@ def _unpack(res_p, want_dist: bool) -> tuple[list, float]:
             n_all_pairs=[int(x) for x in na[l * nd:(l + 1) * nd]],
             n_columns=[int(x) for x in nc[l * nd:(l + 1) * nd]],
             n_residual=[int(x) for x in nr[l * nd:(l + 1) * nd]],
+            n_adds=[int(x) for x in na2[l * nd:(l + 1) * nd]],
             dist=None if dist is None else dist[l],
         ))
     stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(int(r.n_stages))]
