@@ -37,6 +37,7 @@ class _Result(ctypes.Structure):
         ("max_heap", ctypes.c_int64 * MAXD),
         ("max_live", ctypes.c_int64 * MAXD),
         ("sum_live", ctypes.c_int64 * MAXD),
+        ("sum_heap_steps", ctypes.c_int64 * MAXD),
         ("num_edges", ctypes.c_int64),
         ("thresh", ctypes.c_float),
     ]
@@ -116,6 +117,7 @@ def _unpack(r: _Result, maxdim: int) -> dict:
         "max_heap": [int(r.max_heap[d]) for d in range(maxdim + 1)],
         "max_live": [int(r.max_live[d]) for d in range(maxdim + 1)],
         "sum_live": [int(r.sum_live[d]) for d in range(maxdim + 1)],
+        "sum_heap_steps": [int(r.sum_heap_steps[d]) for d in range(maxdim + 1)],
     }
 
 

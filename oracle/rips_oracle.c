@@ -61,6 +61,7 @@ typedef struct {
     int64_t max_heap[OR_MAXDIM + 1];    /* largest working heap (entries)       */
     int64_t max_live[OR_MAXDIM + 1];    /* largest reduced column |R_j| (debug) */
     int64_t sum_live[OR_MAXDIM + 1];
+    int64_t sum_heap_steps[OR_MAXDIM + 1]; /* sum over pivot steps of heap size */
     int64_t num_edges;
     float thresh;
 } oracle_result;
@@ -529,6 +530,7 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
             for (;;) {
                 splx_t p = heap_get_pivot(&work);
                 if (work.n > res->max_heap[dim]) res->max_heap[dim] = work.n;
+                res->sum_heap_steps[dim] += work.n;
                 if (p.idx == HM_EMPTY) {
                     pairs_push(&P[dim], sg.diam, INFINITY, (int64_t)sg.idx, -1);
                     voff[j + 1] = vn;

@@ -61,28 +61,43 @@ struct Plan {
     uint64_t ncand[4] = {0}, piv_words[4] = {0}, rcap[4] = {0}, pcap[4] = {0};
     uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, vcap_g = 0, sstride = 0;
     bool lds_mode = false;
-    Reduce2Cfg rcfg[4] = {};
+    ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
            o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0,
-           o_hsig = 0, o_pairs[4] = {0}, o_h0s = 0,
+           o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
 };
 
-// LDS carve of k_reduce2 in LDS mode (mirrors the kernel's take() order)
-Reduce2Cfg reduce_cfg(int n, uint64_t piv_words) {
-    Reduce2Cfg c{};
+// LDS carve of k_reduce_all (mirrors the kernel): [16][dist][map H1][per-dim:
+// map H2 (dim 2 only) + W (log 8 B + index 16 B per entry) + pivot bitmap]
+ReduceAllCfg reduce_cfg(int n, int maxdim, const uint64_t* piv_words, bool lds_mode) {
+    ReduceAllCfg c{};
     auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
-    c.rmap_lds_cap = 1024;
-    c.dist_lds = 1;
-    auto wbytes = [&](uint64_t w) { return al(8 * w) + al(16 * w); };
-    const uint64_t fixed = 16 + al(8ull * c.rmap_lds_cap) + al(4ull * c.rmap_lds_cap) + al(4ull * n * n);
-    const uint64_t piv = al(4ull * piv_words);
-    c.wcap = 8192;
-    c.piv_lds = fixed + piv + wbytes(c.wcap) <= (uint64_t)kLdsMax ? 1 : 0;
-    while (c.wcap > 1024 && fixed + (c.piv_lds ? piv : 0) + wbytes(c.wcap) > (uint64_t)kLdsMax) c.wcap >>= 1;
-    c.bytes = (uint32_t)(fixed + (c.piv_lds ? piv : 0) + wbytes(c.wcap));
+    const uint32_t mapcap = 1024;
+    c.dist_lds = lds_mode ? 1 : 0;
+    const uint64_t prefix = 16 + (c.dist_lds ? al(4ull * n * n) : 0) + 12ull * mapcap;
+    uint64_t need = prefix;
+    for (int d = 1; d <= maxdim; ++d) {
+        Reduce2Cfg& r = c.dim[d];
+        r.rmap_lds_cap = mapcap;
+        const uint64_t map = d == 2 ? 12ull * mapcap : 0;
+        const uint64_t piv = al(4ull * piv_words[d]);
+        if (!lds_mode) {
+            r.wcap = 0;
+            r.piv_lds = 0;
+            need = std::max<uint64_t>(need, prefix + map);
+            continue;
+        }
+        r.wcap = 4096;
+        r.piv_lds = 1;
+        auto bytes = [&]() { return prefix + map + 24ull * r.wcap + r.wcap + (r.piv_lds ? piv : 0); };
+        if (bytes() > (uint64_t)kLdsMax) r.piv_lds = 0;
+        while (r.wcap > 1024 && bytes() > (uint64_t)kLdsMax) r.wcap >>= 1;
+        need = std::max<uint64_t>(need, bytes());
+    }
+    c.bytes = (uint32_t)need;
     return c;
 }
 
@@ -101,15 +116,7 @@ int make_plan(Plan& p, bool force_global, int scale) {
     p.rmap_stride = next_pow2(2 * p.max_rcap + 16);
     p.vpool_cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 16, 32 * p.max_rcap), 1ull << 27) << scale;
     p.lds_mode = p.N <= kSmallN && !force_global;
-    for (int d = 1; d <= p.maxdim; ++d) {
-        if (p.lds_mode) {
-            p.rcfg[d] = reduce_cfg((int)N, p.piv_words[d]);
-        } else {
-            p.rcfg[d] = Reduce2Cfg{};
-            p.rcfg[d].dist_lds = N <= 96 ? 1 : 0;
-            p.rcfg[d].bytes = 16 + (p.rcfg[d].dist_lds ? (uint32_t)(4 * N * N) : 0);
-        }
-    }
+    p.rcfg = reduce_cfg((int)N, p.maxdim, p.piv_words, p.lds_mode);
     p.wcap_g = (N <= 256 ? 1ull << 17 : (N <= 640 ? 1ull << 21 : 1ull << 23)) << (2 * scale);
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
@@ -128,12 +135,13 @@ int make_plan(Plan& p, bool force_global, int scale) {
     p.o_stats = take(L * sizeof(LayerStats));
     p.o_mst = take(L * p.mst_words * 4);
     for (int d = 1; d <= p.maxdim; ++d) p.o_piv[d] = take(L * p.piv_words[d] * 4);
+    p.o_rowmax = take(L * N * 4);
     p.memset_hi = o;
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
-    p.o_tmp = take(L * p.max_rcap * 8);
+    p.o_tmp = take(L * 2 * p.max_rcap * 8);
     if (p.maxdim >= 1) {
-        p.o_rmk = take(L * p.rmap_stride * 8);
-        p.o_rmv = take(L * p.rmap_stride * 4);
+        p.o_rmk = take(L * 2 * p.rmap_stride * 8);
+        p.o_rmv = take(L * 2 * p.rmap_stride * 4);
         p.o_vlen = take(L * p.max_rcap * 4);
         p.o_vpool = take(L * p.vpool_cap * 8);
         p.o_voff = take(L * p.max_rcap * 8);
@@ -142,6 +150,7 @@ int make_plan(Plan& p, bool force_global, int scale) {
         if (!p.lds_mode) {
             p.o_wk = take(L * p.wcap_g * 8);       // key log
             p.o_wl = take(L * p.wcap_g * 2 * 8);   // u64 index, 2 * wcap slots
+            p.o_wp = take(L * p.wcap_g / 4 * 4);   // bucket fill counters
         }
     }
     for (int d = 0; d <= p.maxdim; ++d) p.o_pairs[d] = take(L * p.pcap[d] * sizeof(Pair));
@@ -159,8 +168,8 @@ int make_plan(Plan& p, bool force_global, int scale) {
 struct Workspace {
     int device = -1;
     bool init = false;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr;
     char* dbuf = nullptr;
     size_t dcap = 0;
     OutPair* hout = nullptr;  // host-mapped
@@ -171,35 +180,36 @@ struct Workspace {
     int64_t* houtoff = nullptr;
     size_t houtoff_cap = 0;
     std::vector<hipEvent_t> stage_ev;  // stage-time events (TDA_FLAG_STAGE_TIMES)
+    std::vector<hipEvent_t> stage_ev2; // ... on the side stream
     std::mutex mu;
 };
 
 // records an event after each stage when stage timing is on
 struct StageTimer {
-    Workspace& w;
+    std::vector<hipEvent_t>& ev;
     hipStream_t s;
     bool on;
     std::vector<const char*> names;
     int mark(const char* name) {
         if (!on) return 0;
         size_t i = names.size() + 1;
-        while (w.stage_ev.size() <= i) {
+        while (ev.size() <= i) {
             hipEvent_t e;
             HIPC(hipEventCreate(&e));
-            w.stage_ev.push_back(e);
+            ev.push_back(e);
         }
-        HIPC(hipEventRecord(w.stage_ev[i], s));
+        HIPC(hipEventRecord(ev[i], s));
         names.push_back(name);
         return 0;
     }
     int begin() {
         if (!on) return 0;
-        while (w.stage_ev.empty()) {
+        while (ev.empty()) {
             hipEvent_t e;
             HIPC(hipEventCreate(&e));
-            w.stage_ev.push_back(e);
+            ev.push_back(e);
         }
-        HIPC(hipEventRecord(w.stage_ev[0], s));
+        HIPC(hipEventRecord(ev[0], s));
         return 0;
     }
 };
@@ -220,8 +230,11 @@ Workspace* get_ws(int dev) {
 int ws_prepare(Workspace& w, const Plan& p) {
     if (!w.init) {
         HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+        HIPC(hipStreamCreateWithFlags(&w.stream2, hipStreamNonBlocking));
         HIPC(hipEventCreate(&w.ev0));
         HIPC(hipEventCreate(&w.ev1));
+        HIPC(hipEventCreateWithFlags(&w.evf, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&w.evj, hipEventDisableTiming));
         w.init = true;
     }
     if (w.dcap < p.total) {
@@ -267,17 +280,17 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_h0, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_sort_resid, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_finalize, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-#define TDA_ATTR_RED(D, LW, PK) \
-    HIPC(hipFuncSetAttribute((const void*)k_reduce2<D, LW, PK>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax))
-    TDA_ATTR_RED(1, true, true);
-    TDA_ATTR_RED(1, true, false);
-    TDA_ATTR_RED(1, false, true);
-    TDA_ATTR_RED(1, false, false);
-    TDA_ATTR_RED(2, true, true);
-    TDA_ATTR_RED(2, true, false);
-    TDA_ATTR_RED(2, false, true);
-    TDA_ATTR_RED(2, false, false);
+#define TDA_ATTR_RED(LW, P1, P2) \
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_all<LW, P1, P2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax))
+    TDA_ATTR_RED(true, true, true);
+    TDA_ATTR_RED(true, true, false);
+    TDA_ATTR_RED(true, false, false);
+    TDA_ATTR_RED(false, true, true);
+    TDA_ATTR_RED(false, true, false);
+    TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
+    HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_apparent<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     if (dev < 64) g_attr_done[dev] = true;
@@ -327,7 +340,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     float* dist = (float*)(B + p.o_dist);
     LayerStats* stats = (LayerStats*)(B + p.o_stats);
 
-    StageTimer tm{w, s, (a.flags & TDA_FLAG_STAGE_TIMES) != 0, {}};
+    StageTimer tm{w.stage_ev, s, (a.flags & TDA_FLAG_STAGE_TIMES) != 0, {}};
+    std::vector<hipEvent_t>& w2ev = w.stage_ev2;
 #define MARK(name) \
     do {           \
         if (int rc_ = tm.mark(name)) return rc_; \
@@ -337,8 +351,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(hipMemsetAsync(B + p.memset_lo, 0, p.memset_hi - p.memset_lo, s));
     MARK("memset");
 
-    // ---- distances
+    // ---- distances (+ row maxima for the enclosing radius)
     const size_t esz = p.dtype == TDA_F64 ? 8 : 4;
+    uint32_t* rowmax = (uint32_t*)(B + p.o_rowmax);
     if (input_kind == 0) {
         const void* x = host_or_dev;
         if (!a.x_on_device) {
@@ -347,38 +362,43 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         }
         dim3 grid((n + 15) / 16, (n + 15) / 16, L);
         if (p.dtype == TDA_F64)
-            hipLaunchKernelGGL(k_distance<double>, grid, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist);
+            hipLaunchKernelGGL(k_distance<double>, grid, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax);
         else
-            hipLaunchKernelGGL(k_distance<float>, grid, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist);
-    } else if (input_kind == 1) {
-        const void* x = host_or_dev;
-        if (!a.x_on_device) {
-            HIPC(hipMemcpyAsync(B + p.o_x, x, (size_t)L * n * n * esz, hipMemcpyHostToDevice, s));
-            x = B + p.o_x;
-        }
-        unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
-        if (p.dtype == TDA_F64)
-            hipLaunchKernelGGL(k_square_dist<double>, dim3(gx, L), dim3(256), 0, s, (const double*)x, n, dist);
-        else
-            hipLaunchKernelGGL(k_square_dist<float>, dim3(gx, L), dim3(256), 0, s, (const float*)x, n, dist);
+            hipLaunchKernelGGL(k_distance<float>, grid, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax);
     } else {
-        const uint64_t ne = binom((uint64_t)n, 2);
         const void* x = host_or_dev;
-        if (ne) {
-            HIPC(hipMemcpyAsync(B + p.o_x, x, ne * 4, hipMemcpyHostToDevice, s));
-        }
         unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
-        hipLaunchKernelGGL(k_square_from_condensed, dim3(gx), dim3(256), 0, s, (const float*)(B + p.o_x), n, dist);
+        if (input_kind == 1) {
+            if (!a.x_on_device) {
+                HIPC(hipMemcpyAsync(B + p.o_x, x, (size_t)L * n * n * esz, hipMemcpyHostToDevice, s));
+                x = B + p.o_x;
+            }
+            if (p.dtype == TDA_F64)
+                hipLaunchKernelGGL(k_square_dist<double>, dim3(gx, L), dim3(256), 0, s, (const double*)x, n, dist);
+            else
+                hipLaunchKernelGGL(k_square_dist<float>, dim3(gx, L), dim3(256), 0, s, (const float*)x, n, dist);
+        } else {
+            const uint64_t ne = binom((uint64_t)n, 2);
+            if (ne) HIPC(hipMemcpyAsync(B + p.o_x, x, ne * 4, hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(k_square_from_condensed, dim3(gx), dim3(256), 0, s, (const float*)(B + p.o_x), n, dist);
+        }
+        HIPC(hipGetLastError());
+        hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
     }
     HIPC(hipGetLastError());
     MARK(input_kind == 0 ? "k_distance" : "k_square_dist");
 
-    // ---- H0
+    // ---- H0 on the side stream: it overlaps the apparent-pair kernels, which
+    // do not need the spanning forest (a forest edge is an H0 death, never an
+    // apparent column; k_reduce_all skips forest edges among the residuals).
+    HIPC(hipEventRecord(w.evf, s));
+    hipStream_t s2 = w.stream2;
+    HIPC(hipStreamWaitEvent(s2, w.evf, 0));
+    StageTimer tm2{w2ev, s2, tm.on, {}};
+    if (int rc = tm2.begin()) return rc;
     if (n <= kSmallN) {
-        hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s, dist, n, a.thresh, stats,
+        hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s2, dist, n, a.thresh, stats,
                            (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
-        HIPC(hipGetLastError());
-        MARK("k_h0");
     } else {
         int T = n <= 256 ? 256 : 1024;
         size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
@@ -387,13 +407,41 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         uint64_t ch = 1;
         while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
         size_t lds = base + ch * 8;
-        hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
+        hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s2, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
                            (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
-        HIPC(hipGetLastError());
-        MARK("k_h0");
     }
+    HIPC(hipGetLastError());
+    if (int rc = tm2.mark("k_h0")) return rc;
+    HIPC(hipEventRecord(w.evj, s2));
 
-    // ---- H1 .. Hmaxdim
+    // ---- H1 .. Hmaxdim: apparent pairs (parallel), residual sort, serial reduction
+    DimBufs db[3] = {};
+    for (int d = 1; d <= p.maxdim; ++d) {
+        db[d].cleared = d == 1 ? nullptr : (const uint32_t*)(B + p.o_piv[d - 1]);
+        db[d].cleared_words = d == 1 ? 0 : p.piv_words[d - 1];
+        db[d].pivbits = (uint32_t*)(B + p.o_piv[d]);
+        db[d].piv_words = p.piv_words[d];
+        db[d].resid = (uint64_t*)(B + p.o_resid[d]);
+        db[d].rcap = p.rcap[d];
+        db[d].ncand = p.ncand[d];
+        uint64_t blocks = (p.ncand[d] + 255) / 256;
+        unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, 4096 / L)));
+        const bool dl = n <= kAppLdsMaxN;
+        const size_t alds = 16 + (dl ? (size_t)n * n * 4 : 0);
+        if (d == 1) {
+            if (dl)
+                hipLaunchKernelGGL((k_apparent<1, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+            else
+                hipLaunchKernelGGL((k_apparent<1, false>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+        } else {
+            if (dl)
+                hipLaunchKernelGGL((k_apparent<2, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+            else
+                hipLaunchKernelGGL((k_apparent<2, false>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+        }
+        HIPC(hipGetLastError());
+        MARK(d == 1 ? "k_apparent<1>" : "k_apparent<2>");
+    }
     Reduce2Bufs rb;
     rb.rmap_keys = (uint64_t*)(B + p.o_rmk);
     rb.rmap_vals = (uint32_t*)(B + p.o_rmv);
@@ -406,61 +454,42 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     rb.wtmp_stride = 2 * (p.lds_mode ? 8192 : p.wcap_g);
     rb.wlog = (uint64_t*)(B + p.o_wk);
     rb.windex = (uint64_t*)(B + p.o_wl);
+    rb.wfill = (uint32_t*)(B + p.o_wp);
     rb.wcap = p.wcap_g;
-    for (int d = 1; d <= p.maxdim; ++d) {
-        DimBufs db;
-        db.cleared = d == 1 ? (const uint32_t*)(B + p.o_mst) : (const uint32_t*)(B + p.o_piv[d - 1]);
-        db.cleared_words = d == 1 ? p.mst_words : p.piv_words[d - 1];
-        db.pivbits = (uint32_t*)(B + p.o_piv[d]);
-        db.piv_words = p.piv_words[d];
-        db.resid = (uint64_t*)(B + p.o_resid[d]);
-        db.rcap = p.rcap[d];
-        db.ncand = p.ncand[d];
-        Pair* pairs = (Pair*)(B + p.o_pairs[d]);
-        uint64_t blocks = (p.ncand[d] + 255) / 256;
-        unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, 4096 / L)));
-        const bool dl = n <= kAppLdsMaxN;
-        const size_t alds = dl ? (size_t)n * n * 4 : 0;
-        if (d == 1) {
-            if (dl)
-                hipLaunchKernelGGL((k_apparent<1, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db, pairs, p.pcap[d]);
-            else
-                hipLaunchKernelGGL((k_apparent<1, false>), dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
-        } else {
-            if (dl)
-                hipLaunchKernelGGL((k_apparent<2, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db, pairs, p.pcap[d]);
-            else
-                hipLaunchKernelGGL((k_apparent<2, false>), dim3(gx, L), dim3(256), 0, s, dist, n, stats, db, pairs, p.pcap[d]);
+    rb.mst = (const uint32_t*)(B + p.o_mst);
+    rb.mst_words = p.mst_words;
+    if (p.maxdim >= 1) {
+        SortArgs sa = {};
+        for (int d = 1; d <= p.maxdim; ++d) {
+            sa.resid[d] = db[d].resid;
+            sa.rcap[d] = db[d].rcap;
         }
+        hipLaunchKernelGGL(k_sort_resid, dim3(L, p.maxdim), dim3(1024), 16384 * 8, s, stats, sa, (uint64_t*)(B + p.o_tmp),
+                           p.max_rcap, rb.rmap_keys, rb.rmap_stride, 14);
         HIPC(hipGetLastError());
-        MARK(d == 1 ? "k_apparent<1>" : "k_apparent<2>");
-        hipLaunchKernelGGL(k_sort_resid, dim3(L), dim3(1024), 16384 * 8, s, stats, d, db.resid, db.rcap, (uint64_t*)(B + p.o_tmp),
-                           rb.rmap_keys, rb.rmap_stride, 14);
-        HIPC(hipGetLastError());
-        MARK(d == 1 ? "k_sort_resid<1>" : "k_sort_resid<2>");
-        const Reduce2Cfg& rc = p.rcfg[d];
+        MARK("k_sort_resid");
         if (!p.lds_mode) {
             HIPC(hipMemsetAsync(rb.windex, 0, (size_t)L * p.wcap_g * 2 * 8, s));
+            HIPC(hipMemsetAsync(rb.wfill, 0, (size_t)L * p.wcap_g / 4 * 4, s));
         }
-        const bool packed = (d == 1 && n <= 1024) || (d == 2 && n <= 256);
-#define TDA_LAUNCH_RED(D, LW, PK)                                                                                      \
-    hipLaunchKernelGGL((k_reduce2<D, LW, PK>), dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db, rb, rc, pairs, p.pcap[d])
-        if (d == 1) {
-            if (p.lds_mode) {
-                if (packed) TDA_LAUNCH_RED(1, true, true); else TDA_LAUNCH_RED(1, true, false);
-            } else {
-                if (packed) TDA_LAUNCH_RED(1, false, true); else TDA_LAUNCH_RED(1, false, false);
-            }
+        HIPC(hipStreamWaitEvent(s, w.evj, 0));  // join: forest edges (clearing of H1 columns)
+        const bool p1 = n <= 1024, p2 = n <= 256;
+        Pair* pairs1 = (Pair*)(B + p.o_pairs[1]);
+        Pair* pairs2 = p.maxdim >= 2 ? (Pair*)(B + p.o_pairs[2]) : pairs1;
+        const ReduceAllCfg& rc = p.rcfg;
+#define TDA_LAUNCH_RED(LW, P1, P2)                                                                                        \
+    hipLaunchKernelGGL((k_reduce_all<LW, P1, P2>), dim3(L), dim3(64), rc.bytes, s, dist, n, p.maxdim, stats, db[1], db[2], rb, rc, \
+                       pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
+        if (p.lds_mode) {
+            if (p2) TDA_LAUNCH_RED(true, true, true); else if (p1) TDA_LAUNCH_RED(true, true, false); else TDA_LAUNCH_RED(true, false, false);
         } else {
-            if (p.lds_mode) {
-                if (packed) TDA_LAUNCH_RED(2, true, true); else TDA_LAUNCH_RED(2, true, false);
-            } else {
-                if (packed) TDA_LAUNCH_RED(2, false, true); else TDA_LAUNCH_RED(2, false, false);
-            }
+            if (p2) TDA_LAUNCH_RED(false, true, true); else if (p1) TDA_LAUNCH_RED(false, true, false); else TDA_LAUNCH_RED(false, false, false);
         }
 #undef TDA_LAUNCH_RED
         HIPC(hipGetLastError());
-        MARK(d == 1 ? "k_reduce<1>" : "k_reduce<2>");
+        MARK("k_reduce_all");
+    } else {
+        HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
 
     // ---- emission order + compaction into host-mapped memory
@@ -526,7 +555,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 arg = l;
                 for (int i = 0; i < 8; ++i) mx[i] = w.hstats[l].prof[d][i];
             }
-        fprintf(stderr, "[tda-prof] dim %d slowest layer %d adds %lld: scan %llu lookup %llu dec+facet %llu cob_app %llu cob_res %llu reset %llu compact %llu total %llu cycles\n",
+        fprintf(stderr, "[tda-prof] dim %d slowest layer %d adds %lld: scan %llu lookup %llu dec+facet %llu cob_app %llu toggles %llu reset %llu compact %llu total %llu cycles\n",
                 d, arg, (long long)w.hstats[arg].n_adds[d], (unsigned long long)mx[0], (unsigned long long)mx[1], (unsigned long long)mx[2],
                 (unsigned long long)mx[3], (unsigned long long)mx[4], (unsigned long long)mx[5], (unsigned long long)mx[6], (unsigned long long)mx[7]);
     }
@@ -601,6 +630,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         (void)hipEventElapsedTime(&t, w.stage_ev[i], w.stage_ev[i + 1]);
         R->stage_ms.push_back(t);
         R->stage_name.push_back(tm.names[i]);
+    }
+    if (tm.on) {  // side stream: H0
+        float t = 0.0f;
+        (void)hipEventElapsedTime(&t, w.stage_ev2[0], w.stage_ev2[1]);
+        R->stage_ms.push_back(t);
+        R->stage_name.push_back("k_h0");
     }
     o.n_stages = (int32_t)tm.names.size();
     o.stage_name = R->stage_name.data();

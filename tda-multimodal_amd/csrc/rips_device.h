@@ -122,6 +122,16 @@ __device__ __forceinline__ float sqrt_rn_f32(float x) {
     return f;
 }
 
+// ---------------------------------------------------------------- address spaces
+// Pointers kept in structs lose their address space and become FLAT accesses
+// (slower, and they tie up both vmcnt and lgkmcnt); hot loops re-type them.
+#define TDA_LDS __attribute__((address_space(3)))
+#define TDA_GLB __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ T ld_lds(const T* p, size_t i) { return ((const TDA_LDS T*)p)[i]; }
+template <typename T>
+__device__ __forceinline__ T ld_glb(const T* p, size_t i) { return ((const TDA_GLB T*)p)[i]; }
+
 // ---------------------------------------------------------------- staging
 // Copy nbytes (multiple of 4) global -> LDS with 16-B loads, 8 in flight per
 // lane before the first LDS store (a single wave otherwise serialises one

@@ -53,10 +53,16 @@ struct DimBufs {              // per reduction dim d (columns = d-simplices)
 // reads dm[I > J]), cast to f32 (:651), clamp (:429), diag 0 (:436), sqrt (:441).
 // The dot products and norms accumulate in increasing k with FMA, exact for
 // f32 inputs (products are exact in f64).
+// Row maxima for the enclosing radius (ripser.py rips_dm: thresh = min_i
+// max_j d(i,j)) are folded into the distance pass: per-tile row/column maxima,
+// then one atomicMax per row on the f32 bit pattern (non-negative floats order
+// like unsigned ints).  rowmax must be zeroed before the launch.
 template <typename T>
-__global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n, int D, float* __restrict__ dist) {
+__global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n, int D, float* __restrict__ dist,
+                                                  uint32_t* __restrict__ rowmax) {
     constexpr int TS = 16, KC = 32;
     __shared__ double xi[TS][KC + 1], xj[TS][KC + 1];
+    __shared__ uint32_t rmax_i[TS], rmax_j[TS];
     const int l = blockIdx.z;
     const int bi = blockIdx.y, bj = blockIdx.x;
     if (bj < bi) return;
@@ -82,24 +88,62 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
         }
         __syncthreads();
     }
-    if (i >= n || j >= n || j < i) return;
-    if (i == j) {
-        Dl[(size_t)i * n + i] = 0.0f;
-        return;
+    if (threadIdx.x < TS) {
+        rmax_i[threadIdx.x] = 0;
+        rmax_j[threadIdx.x] = 0;
     }
-    double d = (-2.0 * dot + ni) + nj;
-    float f;
-    if constexpr (sizeof(T) == 4) {
-        f = (float)d;
-        f = (f != f) ? f : fmaxf(f, 0.0f);
-        f = sqrt_rn_f32(f);
-    } else {
-        d = (d != d) ? d : fmax(d, 0.0);
-        f = (float)__dsqrt_rn(d);
+    __syncthreads();
+    if (i < n && j < n && j >= i) {
+        if (i == j) {
+            Dl[(size_t)i * n + i] = 0.0f;
+        } else {
+            double d = (-2.0 * dot + ni) + nj;
+            float f;
+            if constexpr (sizeof(T) == 4) {
+                f = (float)d;
+                f = (f != f) ? f : fmaxf(f, 0.0f);
+                f = sqrt_rn_f32(f);
+            } else {
+                d = (d != d) ? d : fmax(d, 0.0);
+                f = (float)__dsqrt_rn(d);
+            }
+            f = f + 0.0f;
+            Dl[(size_t)i * n + j] = f;
+            Dl[(size_t)j * n + i] = f;
+            atomicMax(&rmax_i[ty], __float_as_uint(f));
+            atomicMax(&rmax_j[tx], __float_as_uint(f));
+        }
     }
-    f = f + 0.0f;
-    Dl[(size_t)i * n + j] = f;
-    Dl[(size_t)j * n + i] = f;
+    __syncthreads();
+    uint32_t* rm = rowmax + (size_t)l * n;
+    if (threadIdx.x < TS && bi * TS + threadIdx.x < n && rmax_i[threadIdx.x]) atomicMax(&rm[bi * TS + threadIdx.x], rmax_i[threadIdx.x]);
+    if (threadIdx.x >= 64 && threadIdx.x < 64 + TS && bj * TS + threadIdx.x - 64 < n && rmax_j[threadIdx.x - 64])
+        atomicMax(&rm[bj * TS + threadIdx.x - 64], rmax_j[threadIdx.x - 64]);
+}
+
+// row maxima of a square distance matrix (distance-matrix inputs): one wave per row
+__global__ __launch_bounds__(256) void k_rowmax(const float* __restrict__ dist, int n, uint32_t* __restrict__ rowmax) {
+    const int l = blockIdx.y, w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, ln = threadIdx.x & 63;
+    if (w >= n) return;
+    const float* row = dist + ((size_t)l * n + w) * n;
+    float m = 0.0f;
+    for (int j = ln; j < n; j += 64) m = fmaxf(m, row[j]);
+    for (int k = 32; k >= 1; k >>= 1) m = fmaxf(m, __shfl_xor(m, k, 64));
+    if (ln == 0) rowmax[(size_t)l * n + w] = __float_as_uint(m);
+}
+
+// threshold of layer l: the user's, or the enclosing radius min_i rowmax[i]
+__device__ __forceinline__ float block_thresh(const uint32_t* __restrict__ rowmax, int n, float user_thresh, uint32_t* s_min) {
+    if (!(isinf(user_thresh) || user_thresh == 3.402823466e+38f)) return user_thresh;
+    if (threadIdx.x == 0) *s_min = 0xFFFFFFFFu;
+    __syncthreads();
+    uint32_t m = 0xFFFFFFFFu;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = min(m, rowmax[i]);
+    atomicMin(s_min, m);
+    __syncthreads();
+    const float r = __uint_as_float(*s_min);
+    __syncthreads();
+    return n == 1 ? 0.0f : r;
 }
 
 // distance-matrix input: ripser.py condenses dm[I > J] (upper triangle,
@@ -524,29 +568,29 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
 // an empty coboundary are essential (emitted here), the rest go to k_reduce.
 template <int DIM, bool DLDS>
 __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
-                                                  DimBufs b, Pair* __restrict__ pairs, uint64_t pcap) {
+                                                  DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.y;
     const float* Dl = dist + (size_t)l * n * n;
+    const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
     if (DLDS) {  // stage this layer's distance matrix in LDS (N <= 128: <= 64 KB)
-        float* sd = (float*)smem;
+        float* sd = (float*)(smem + 16);
         stage_to_lds(sd, Dl, sizeof(float) * n * n, threadIdx.x, blockDim.x);
         __syncthreads();
         Dl = sd;
     }
     LayerStats* st = stats + l;
-    const float r = st->thresh;
-    const uint32_t* cleared = b.cleared + (size_t)l * b.cleared_words;
+    const uint32_t* cleared = b.cleared ? b.cleared + (size_t)l * b.cleared_words : nullptr;
     uint32_t* piv = b.pivbits + (size_t)l * b.piv_words;
     uint64_t* resid = b.resid + (size_t)l * b.rcap;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t acc_cs = 0, acc_app = 0, acc_cols = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < b.ncand; base += stride) {
         const uint64_t s = base + threadIdx.x;
-        int kind = 0;  // 0 skip, 1 apparent, 2 residual, 3 essential
+        int kind = 0;  // 0 skip, 1 apparent, 2 residual (incl. empty coboundary)
         int vs[DIM + 1];
         float sd = 0.0f;
-        if (s < b.ncand && !((cleared[s >> 5] >> (s & 31)) & 1u)) {
+        if (s < b.ncand && !(cleared && ((cleared[s >> 5] >> (s & 31)) & 1u))) {
             decode<DIM>(s, n, vs);
             sd = simplex_diam<DIM>(Dl, n, vs);
             if (sd <= r) {
@@ -569,7 +613,7 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                     }
                 }
                 if (bv < 0) {
-                    kind = 3;
+                    kind = 2;  // empty coboundary: essential unless cleared -> decided by k_reduce_all
                 } else {
                     kind = 2;
                     if (bcd == sd) {
@@ -617,13 +661,6 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                     atomicOr(&st->err, ERR_RESID_CAP);
             }
         }
-        if (kind == 3) {
-            uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-            if (pos < pcap)
-                pairs[(size_t)l * pcap + pos] = Pair{sd, INFINITY, (int64_t)s, -1};
-            else
-                atomicOr(&st->err, ERR_PAIR_CAP);
-        }
     }
     acc_cs = wave_sum_u64(acc_cs);
     acc_app = wave_sum_u64(acc_app);
@@ -638,20 +675,26 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
 }
 
 // ------------------------------------------------------------------ sort residual
-__global__ __launch_bounds__(1024) void k_sort_resid(LayerStats* __restrict__ stats, int dim, uint64_t* __restrict__ resid,
-                                                     uint64_t rcap, uint64_t* __restrict__ tmp, uint64_t* __restrict__ rmap_keys,
-                                                     uint64_t rmap_stride, int sort_log2) {
+struct SortArgs {
+    uint64_t* resid[3];
+    uint64_t rcap[3];
+};
+__global__ __launch_bounds__(1024) void k_sort_resid(LayerStats* __restrict__ stats, SortArgs sa, uint64_t* __restrict__ tmp,
+                                                     uint64_t tmp_stride, uint64_t* __restrict__ rmap_keys, uint64_t rmap_stride,
+                                                     int sort_log2) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x;
+    const int l = blockIdx.x, dim = blockIdx.y + 1;
+    uint64_t* resid = sa.resid[dim];
+    const uint64_t rcap = sa.rcap[dim];
     uint64_t cnt = (uint64_t)stats[l].n_residual[dim];
     if (cnt > rcap) cnt = rcap;
-    block_sort<false>(resid + (size_t)l * rcap, nullptr, cnt, tmp + (size_t)l * rcap, nullptr, (uint64_t*)smem, nullptr,
-                      sort_log2);
+    block_sort<false>(resid + (size_t)l * rcap, nullptr, cnt, tmp + ((size_t)l * 2 + dim - 1) * tmp_stride, nullptr, (uint64_t*)smem,
+                      nullptr, sort_log2);
     // clear the residual pivot map region this layer will use
     uint64_t cap = 16;
     while (cap < 2 * cnt + 16) cap <<= 1;
     if (cap > rmap_stride) cap = rmap_stride;
-    uint64_t* rk = rmap_keys + (size_t)l * rmap_stride;
+    uint64_t* rk = rmap_keys + ((size_t)l * 2 + dim - 1) * rmap_stride;
     for (uint64_t e = threadIdx.x; e < cap; e += blockDim.x) rk[e] = kEmpty64;
 }
 

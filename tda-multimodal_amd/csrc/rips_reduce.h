@@ -90,64 +90,86 @@ struct RowLo {
 constexpr uint64_t kDead = 1ull << 63;
 struct KeySet {
     uint64_t* index;  // icap entries, 0 = free
+    uint32_t* fill;   // per-bucket fill count (icap / 8)
     uint64_t* log;    // cap keys (| kDead when cancelled)
     uint64_t* tmp;    // scratch >= 2 * cap keys (HBM)
     uint32_t imask;   // icap - 1
     uint32_t cnt;     // log length (wave-uniform register)
 
+    // index lookup of one key: 8-slot buckets (64 B, four 16-B reads in
+    // flight) with a per-bucket fill counter, so a probe is one LDS round trip
+    // and an insert takes its slot with one atomicAdd (no CAS retry loop when
+    // several lanes of the pass land in the same bucket).
     __device__ __forceinline__ void toggle_pass(uint64_t k, bool valid, int ln) {
         const uint32_t fp = (uint32_t)k;
-        uint32_t h = mix32(fp) & imask;
+        const uint32_t bmask = imask >> 3;
+        uint32_t bkt = mix32(fp) & bmask;
         uint32_t mine = 0;  // reserved log position + 1
         bool pending = valid;
         while (__ballot(pending)) {
             bool want = false;
+            uint32_t target = 0;
             if (pending) {
-                const uint64_t cur = index[h];
-                if (cur == 0) {
-                    want = true;
-                } else if ((uint32_t)(cur >> 32) == fp) {
-                    atomicXor((unsigned long long*)&log[(uint32_t)cur - 1], (unsigned long long)kDead);  // flip parity
+                const ulonglong2* bp = (const ulonglong2*)&index[(size_t)bkt * 8];
+                const ulonglong2 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
+                const uint64_t e[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+                uint64_t eh = 0;
+                bool full = true;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    if (e[u] != 0 && (uint32_t)(e[u] >> 32) == fp) eh = e[u];
+                    full &= e[u] != 0;
+                }
+                if (eh) {
+                    atomicXor((unsigned long long*)&log[(uint32_t)eh - 1], (unsigned long long)kDead);  // flip parity
                     pending = false;
+                } else if (!full) {
+                    const uint32_t slot = atomicAdd(&fill[bkt], 1u);
+                    if (slot < 8) {
+                        want = true;
+                        target = bkt * 8 + slot;
+                    } else {
+                        bkt = (bkt + 1) & bmask;  // filled up by other lanes of this pass
+                    }
                 } else {
-                    h = (h + 1) & imask;
+                    bkt = (bkt + 1) & bmask;  // bucket full: next one
                 }
             }
-            const uint64_t need = __ballot(want && !mine);
-            if (want && !mine) {
+            const uint64_t need = __ballot(want);
+            if (want) {
                 mine = cnt + lanes_below(need) + 1;
                 log[mine - 1] = k;  // new entry: live
+                index[target] = ((uint64_t)fp << 32) | mine;
+                pending = false;
             }
             cnt += (uint32_t)__popcll(need);
-            if (want) {
-                const unsigned long long nv = ((unsigned long long)fp << 32) | mine;
-                if (atomicCAS((unsigned long long*)&index[h], 0ull, nv) == 0ull)
-                    pending = false;
-                else
-                    h = (h + 1) & imask;  // lost the slot to another key
-            }
         }
     }
     // zero the index, cnt = 0 (whole wave)
     __device__ void reset(int ln) {
         const uint32_t c = cnt;
         if (c * 4 >= imask) {
+            for (uint32_t e = ln; e <= (imask >> 3); e += 64) fill[e] = 0;
             for (uint32_t e = ln; e <= imask; e += 64) index[e] = 0;
         } else {
             // probe each logged key's slot, then zero (two phases)
             uint32_t* slots = (uint32_t*)tmp;
+            const uint32_t bmask = imask >> 3;
             for (uint32_t e = ln; e < c; e += 64) {
                 const uint32_t fp = (uint32_t)log[e];
-                uint32_t h = mix32(fp) & imask;
+                uint32_t h = (mix32(fp) & bmask) * 8;
                 for (;;) {
                     const uint64_t cur = index[h];
                     if (cur == 0 || (uint32_t)(cur >> 32) == fp) break;
-                    h = (h + 1) & imask;
+                    h = (h + 1) & imask;  // buckets are filled in slot order
                 }
                 slots[e] = h;
             }
             __syncthreads();
-            for (uint32_t e = ln; e < c; e += 64) index[slots[e]] = 0;
+            for (uint32_t e = ln; e < c; e += 64) {
+                index[slots[e]] = 0;
+                fill[slots[e] >> 3] = 0;
+            }
         }
         cnt = 0;
         __syncthreads();
@@ -210,7 +232,7 @@ struct KeySet {
 };
 
 struct Reduce2Bufs {
-    uint64_t* rmap_keys;  // [L][rmap_stride] (when the map does not fit LDS)
+    uint64_t* rmap_keys;  // [L][2][rmap_stride] per-dim maps that do not fit LDS
     uint32_t* rmap_vals;
     uint64_t rmap_stride;
     uint64_t* roff;       // [L][rcap] offset of R_j in rpool
@@ -221,97 +243,146 @@ struct Reduce2Bufs {
     uint64_t wtmp_stride;
     // global working tables (global mode)
     uint64_t* windex;  // [L][2 wcap]
+    uint32_t* wfill;   // [L][2 wcap / 8]
     uint64_t* wlog;    // [L][wcap]
     uint64_t wcap;
+    const uint32_t* mst;  // [L][mst_words] H0 forest edges (dim-1 columns to skip)
+    uint64_t mst_words;
 };
 
-struct Reduce2Cfg {  // LDS carve, decided on the host
+struct Reduce2Cfg {  // per-dim LDS carve, decided on the host
     uint32_t wcap, rmap_lds_cap;  // rmap_lds_cap = 0 -> global map
-    int dist_lds, piv_lds;
-    uint32_t bytes;
+    int piv_lds;
+};
+struct ReduceAllCfg {
+    Reduce2Cfg dim[3];
+    int dist_lds;
+    uint32_t bytes;  // dynamic LDS of the launch
 };
 
 enum : int32_t { ERR_LDS_SPILL = 32 };
 
-template <int DIM, bool LDSW, bool PACKED>
-__global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats, DimBufs b,
-                                                Reduce2Bufs rb, Reduce2Cfg cfg, Pair* __restrict__ pairs, uint64_t pcap) {
+// residual pivot map of one dim: open addressing, key = row payload lo32
+struct PivMap {
+    uint64_t* k;
+    uint32_t* v;
+    uint64_t mask;
+    __device__ int64_t find(uint32_t lo, int ln) const {  // wave-parallel probe
+        for (uint64_t h0 = mix32(lo);; h0 += 64) {
+            const uint64_t kk = k[(h0 + ln) & mask];
+            const uint64_t mhit = __ballot(kk == lo), mend = __ballot(kk == kEmpty64);
+            const uint64_t below_end = mend ? ((mend & (~mend + 1)) - 1) : ~0ull;
+            if (mhit & below_end) return (int64_t)v[(h0 + __builtin_ctzll(mhit & below_end)) & mask];
+            if (mend) return -1;
+        }
+    }
+    __device__ void insert(uint32_t lo, uint32_t val) const {  // one lane
+        uint64_t h = mix32(lo) & mask;
+        while (k[h] != kEmpty64) h = (h + 1) & mask;
+        k[h] = lo;
+        v[h] = val;
+    }
+};
+
+struct ReduceCtx {
+    const float* D;  // distance matrix (LDS or HBM)
+    int n;
+    float r;
+    LayerStats* st;
+    unsigned char* lds;  // start of the per-dim LDS region
+    int l, ln;
+};
+
+// payload (lo32) of a d-simplex with descending vertices, as the dim-(d-1)
+// reduction keyed its rows
+template <int NVTX, bool PACKED>
+__device__ __forceinline__ uint32_t row_payload(const int (&t)[NVTX]) {
+    if (PACKED) return RowLo<NVTX>::pack(t);
+    return (uint32_t)encode<NVTX - 1>(t);
+}
+
+// Reduce the residual columns of dimension DIM of one layer (one wave).
+// prev: residual pivot map of DIM-1 (DIM == 2), used to skip columns that are
+// H_{DIM-1} deaths found by the serial reduction (clearing; k_apparent only
+// knew the apparent ones).  Returns this dim's map (valid until the kernel ends
+// if it lives in a persistent region).
+template <int DIM, bool LDSW, bool PACKED, bool PREV_PACKED>
+__device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bufs& rb, const Reduce2Cfg& cfg, PivMap& map,
+                           const PivMap* prev, unsigned char* map_lds, Pair* __restrict__ pairs, uint64_t pcap) {
     constexpr int NV = DIM + 2;  // vertices of a row simplex
     using Lo = RowLo<NV>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, ln = threadIdx.x;
-    LayerStats* st = stats + l;
-    const float r = st->thresh;
+    const int l = c.l, ln = c.ln, n = c.n;
+    const float r = c.r;
+    const float* D = c.D;
+    // distance matrix: LDS in LDS mode, HBM otherwise (typed loads, no FLAT)
+    auto dist_at = [&](size_t i) -> float { return LDSW ? ld_lds(D, i) : ld_glb(D, i); };
+    LayerStats* st = c.st;
     uint64_t nres = (uint64_t)st->n_residual[DIM];
     if (nres > b.rcap) nres = b.rcap;
-    if (nres == 0) return;
     const uint64_t* resid = b.resid + (size_t)l * b.rcap;
     uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
 
-    // ---- LDS carve (16-B aligned pieces)
-    unsigned char* p = smem + 16;
-    KeySet W;
+    // ---- residual pivot map of this dim (LDS when it fits)
+    uint64_t rcap2 = 16;
+    while (rcap2 < 2 * nres + 16) rcap2 <<= 1;
+    if (cfg.rmap_lds_cap && rcap2 <= cfg.rmap_lds_cap) {
+        rcap2 = cfg.rmap_lds_cap;
+        map.k = (uint64_t*)map_lds;
+        map.v = (uint32_t*)(map_lds + 8ull * rcap2);
+        for (uint64_t e = ln; e < rcap2; e += 64) map.k[e] = kEmpty64;
+    } else {
+        if (rcap2 > rb.rmap_stride) rcap2 = rb.rmap_stride;
+        map.k = rb.rmap_keys + ((size_t)l * 2 + (DIM - 1)) * rb.rmap_stride;  // cleared by k_sort_resid
+        map.v = rb.rmap_vals + ((size_t)l * 2 + (DIM - 1)) * rb.rmap_stride;
+    }
+    map.mask = rcap2 - 1;
+    if (nres == 0) {
+        __syncthreads();
+        return;
+    }
+
+    // ---- LDS carve of the per-dim region (16-B aligned pieces)
+    unsigned char* p = c.lds;
     auto take = [&](size_t bytes) {
         unsigned char* q = p;
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
+    KeySet W;
     uint32_t wcap;
     if (LDSW) {
         wcap = cfg.wcap;
         W.log = (uint64_t*)take(8ull * wcap);
         W.index = (uint64_t*)take(16ull * wcap);
+        W.fill = (uint32_t*)take(4ull * (2 * wcap / 8));
     } else {
         wcap = (uint32_t)rb.wcap;
         W.log = rb.wlog + (size_t)l * wcap;
         W.index = rb.windex + (size_t)l * 2 * wcap;
+        W.fill = rb.wfill + (size_t)l * (2 * wcap / 8);
     }
     W.tmp = rb.wtmp + (size_t)l * rb.wtmp_stride;
     W.imask = 2 * wcap - 1;
     W.cnt = 0;
-    // residual pivot map (keyed by the row payload lo32)
-    uint64_t rcap2 = 16;
-    while (rcap2 < 2 * nres + 16) rcap2 <<= 1;
-    uint64_t* rk;
-    uint32_t* rv;
-    if (cfg.rmap_lds_cap && rcap2 <= cfg.rmap_lds_cap) {
-        rcap2 = cfg.rmap_lds_cap;
-        rk = (uint64_t*)take(8ull * rcap2);
-        rv = (uint32_t*)take(4ull * rcap2);
-        for (uint64_t e = ln; e < rcap2; e += 64) rk[e] = kEmpty64;
-    } else {
-        if (cfg.rmap_lds_cap) {
-            take(8ull * cfg.rmap_lds_cap);
-            take(4ull * cfg.rmap_lds_cap);
-        }
-        if (rcap2 > rb.rmap_stride) rcap2 = rb.rmap_stride;
-        rk = rb.rmap_keys + (size_t)l * rb.rmap_stride;  // cleared by k_sort_resid
-        rv = rb.rmap_vals + (size_t)l * rb.rmap_stride;
-    }
-    const uint64_t rmask = rcap2 - 1;
-    const float* D = dist + (size_t)l * n * n;
-    if (cfg.dist_lds) {
-        float* dl = (float*)take(4ull * n * n);
-        stage_to_lds(dl, D, 4ull * n * n, ln, 64);
-        D = dl;
-    }
     uint32_t* piv = pivg;
     if (cfg.piv_lds) {
         uint32_t* pl = (uint32_t*)take(4ull * b.piv_words);
         stage_to_lds(pl, pivg, 4ull * b.piv_words, ln, 64);
         piv = pl;
     }
-    if (LDSW) {  // global-mode tables are zeroed by the host (hipMemsetAsync)
+    if (LDSW) {  // global-mode index: zeroed by the host, left clean by reset()
         for (uint32_t e = ln; e <= W.imask; e += 64) W.index[e] = 0;
+        for (uint32_t e = ln; e <= (W.imask >> 3); e += 64) W.fill[e] = 0;
     }
     __syncthreads();
+    const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
 
     uint64_t* roff = rb.roff + (size_t)l * b.rcap;
     uint32_t* rlen = rb.rlen + (size_t)l * b.rcap;
     uint64_t* rpool = rb.rpool + (size_t)l * rb.rpool_cap;
     uint64_t rused = 0;
     Pair* P = pairs + (size_t)l * pcap;
-    uint64_t cs = 0, npairs = 0, nadds = 0;
+    uint64_t cs = 0, npairs = 0, nadds = 0, nskip = 0;
     int err = 0;  // wave-uniform
 #ifdef TDA_PROFILE
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // scan, lookup, facet, cob-app, cob-res, reset, compact, total
@@ -338,7 +409,7 @@ __global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, 
             uint64_t key = 0;
             if (ok) {
 #pragma unroll
-                for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, D[(size_t)vs[i] * n + v]);  // D symmetric: column read
+                for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, dist_at((size_t)vs[i] * n + v));  // D symmetric: column read
                 ok = cd <= r;
                 uint32_t lo;
                 if (PACKED) {
@@ -360,16 +431,30 @@ __global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, 
                 }
                 key = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | (0xFFFFFFFFu - lo);
             }
+            TDA_STAMP(tq);
             W.toggle_pass(key, ok, ln);
+            TDA_ACC(4, tq);
         }
     };
 
     for (uint64_t j = 0; j < nres && !err; ++j) {
-        const uint64_t key = resid[j];
+        const uint64_t key = ld_glb(resid, j);
         const uint64_t sidx = key_idx(key);
         const float sdm = key_diam(key);
         int vs[DIM + 1];
         decode_wave<DIM>(sidx, n, vs, ln);
+        // clearing: skip columns that are H_{DIM-1} deaths
+        bool cleared;
+        if (DIM == 1) {
+            cleared = (ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u;
+        } else {
+            cleared = prev->find(row_payload<DIM + 1, PREV_PACKED>(vs), ln) >= 0;
+        }
+        if (cleared) {
+            ++nskip;
+            if (ln == 0) rlen[j] = 0;
+            continue;
+        }
         if (!room((uint32_t)n)) break;
         cob(vs, sdm);
         __syncthreads();
@@ -408,32 +493,22 @@ __global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, 
                 pidx = plo;
                 decode_wave<DIM + 1>(pidx, n, t, ln);
             }
-            // owner lookup: 64 consecutive probe slots per round, ballot
-            const bool app = (piv[pidx >> 5] >> (pidx & 31)) & 1u;
-            int64_t owner = -1;
-            for (uint64_t h0 = mix32(plo);; h0 += 64) {
-                const uint64_t kk = rk[(h0 + ln) & rmask];
-                const uint64_t mhit = __ballot(kk == plo), mend = __ballot(kk == kEmpty64);
-                const uint64_t below_end = mend ? ((mend & (~mend + 1)) - 1) : ~0ull;
-                if (mhit & below_end) {
-                    owner = (int64_t)rv[(h0 + __builtin_ctzll(mhit & below_end)) & rmask];
-                    break;
-                }
-                if (mend) break;
-            }
+            const uint32_t pw = cfg.piv_lds ? ld_lds(piv, pidx >> 5) : ld_glb((const uint32_t*)pivg, pidx >> 5);
+            const bool app = (pw >> (pidx & 31)) & 1u;
+            const int64_t owner = map.find(plo, ln);
             TDA_ACC(1, t1);
             TDA_STAMP(t2);
             if (owner >= 0) {
                 // add the stored reduced column R_owner
-                const uint64_t o0 = roff[owner];
-                const uint32_t ol = rlen[owner];
+                const uint64_t o0 = ld_glb((const uint64_t*)roff, owner);
+                const uint32_t ol = ld_glb((const uint32_t*)rlen, owner);
                 if (!room(ol)) break;
                 for (uint32_t e0 = 0; e0 < ol; e0 += 8 * 64) {
                     uint64_t rk8[8];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const uint32_t e = e0 + u * 64 + ln;
-                        rk8[u] = e < ol ? rpool[o0 + e] : 0;
+                        rk8[u] = e < ol ? ld_glb((const uint64_t*)rpool, o0 + e) : 0;
                     }
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
@@ -451,7 +526,7 @@ __global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, 
 #pragma unroll
                 for (int i = 0; i < NV; ++i)
 #pragma unroll
-                    for (int k = i + 1; k < NV; ++k) dd[i][k] = D[(size_t)t[i] * n + t[k]];
+                    for (int k = i + 1; k < NV; ++k) dd[i][k] = dist_at((size_t)t[i] * n + t[k]);
                 float fd = -1.0f;
                 int fu = 0;
 #pragma unroll
@@ -491,10 +566,7 @@ __global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, 
                         else
                             atomicOr(&st->err, ERR_PAIR_CAP);
                     }
-                    uint64_t h = mix32(plo) & rmask;
-                    while (rk[h] != kEmpty64) h = (h + 1) & rmask;
-                    rk[h] = plo;
-                    rv[h] = (uint32_t)j;
+                    map.insert(plo, (uint32_t)j);
                     atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
                     if (piv != pivg) atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
                 }
@@ -525,10 +597,52 @@ __global__ __launch_bounds__(64) void k_reduce2(const float* __restrict__ dist, 
         atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)cs);
         atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)npairs);
         atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)nadds);
+        // cleared columns were counted as columns by k_apparent
+        atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)(0ull - nskip));
+        atomicAdd((unsigned long long*)&st->n_residual[DIM], (unsigned long long)(0ull - nskip));
 #ifdef TDA_PROFILE
         prof[7] = clock64() - t_all;
         for (int i = 0; i < 8; ++i) st->prof[DIM][i] = prof[i];
 #endif
+    }
+    __syncthreads();
+}
+
+// All serial reductions of one layer in ONE launch (one wave per layer):
+// H1 then H2, so a layer's H2 chain starts as soon as its own H1 chain ends
+// (the batch time is the max over layers of the sum, not the sum of maxes).
+// LDS: [16 B][distance matrix][H1 residual-pivot map][per-dim region].
+template <bool LDSW, bool P1, bool P2>
+__global__ __launch_bounds__(64) void k_reduce_all(const float* __restrict__ dist, int n, int maxdim, LayerStats* __restrict__ stats,
+                                                   DimBufs b1, DimBufs b2, Reduce2Bufs rb, ReduceAllCfg cfg, Pair* __restrict__ pairs1,
+                                                   Pair* __restrict__ pairs2, uint64_t pcap1, uint64_t pcap2) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, ln = threadIdx.x;
+    LayerStats* st = stats + l;
+    unsigned char* p = smem + 16;
+    ReduceCtx c;
+    c.n = n;
+    c.l = l;
+    c.ln = ln;
+    c.st = st;
+    c.r = st->thresh;
+    c.D = dist + (size_t)l * n * n;
+    if (LDSW) {  // LDS mode (N <= 64): the matrix always fits
+        float* dl = (float*)p;
+        stage_to_lds(dl, c.D, 4ull * n * n, ln, 64);
+        p += (4ull * n * n + 15) & ~15ull;
+        c.D = dl;
+    }
+    unsigned char* map1_lds = p;
+    p += 12ull * cfg.dim[1].rmap_lds_cap;
+    __syncthreads();
+    PivMap m1, m2;
+    c.lds = p;
+    reduce_dim<1, LDSW, P1, P1>(c, b1, rb, cfg.dim[1], m1, nullptr, map1_lds, pairs1, pcap1);
+    if (maxdim >= 2) {
+        unsigned char* map2_lds = p;
+        c.lds = p + 12ull * cfg.dim[2].rmap_lds_cap;
+        reduce_dim<2, LDSW, P2, P1>(c, b2, rb, cfg.dim[2], m2, &m1, map2_lds, pairs2, pcap2);
     }
 }
 
