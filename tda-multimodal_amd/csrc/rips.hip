@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -17,7 +18,7 @@
 
 #include "../../include/tda_rips.h"
 #include "rips_kernels.h"
-#include "rips_reduce.h"
+#include "rips_reduce_big.h"
 
 using namespace tda;
 
@@ -52,7 +53,8 @@ constexpr uint64_t kRCapMax = 1ull << 22;    // residual columns per layer and d
 constexpr uint64_t kPCapMax = 1ull << 16;    // emitted pairs per layer and dim (H>=1)
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kSmallN = 64;                  // one-wave H0 + LDS-resident reduction up to here
-constexpr int kAppLdsMaxN = 128;             // k_apparent stages the distance matrix in LDS up to here
+constexpr int kAppLdsMaxN = 128;
+constexpr int kBigMinN = 256;                // k_reduce_big above this N (global mode)             // k_apparent stages the distance matrix in LDS up to here
 
 // ------------------------------------------------------------------ plan
 struct Plan {
@@ -61,10 +63,11 @@ struct Plan {
     uint64_t ncand[4] = {0}, piv_words[4] = {0}, rcap[4] = {0}, pcap[4] = {0};
     uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, vcap_g = 0, sstride = 0;
     bool lds_mode = false;
+    bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -118,6 +121,13 @@ int make_plan(Plan& p, bool force_global, int scale) {
     p.lds_mode = p.N <= kSmallN && !force_global;
     p.rcfg = reduce_cfg((int)N, p.maxdim, p.piv_words, p.lds_mode);
     p.wcap_g = (N <= 256 ? 1ull << 17 : (N <= 640 ? 1ull << 21 : 1ull << 23)) << (2 * scale);
+    {
+        const char* m = getenv("TDA_REDUCE");
+        // measured (r01): one wave per layer wins up to N = 256 (grid144 md2
+        // 20.6 vs 26.8 ms, torus256 md2 64 vs 91 ms); the radix heap above
+        const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big");
+        p.big = !p.lds_mode && (want_big || (!want_wave && p.N > kBigMinN));
+    }
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
     p.sstride = 3 * maxp;
@@ -146,12 +156,13 @@ int make_plan(Plan& p, bool force_global, int scale) {
         p.o_vpool = take(L * p.vpool_cap * 8);
         p.o_voff = take(L * p.max_rcap * 8);
         uint64_t wmax = p.lds_mode ? 8192 : p.wcap_g;
-        p.o_wt = take(L * wmax * 8 * 2);  // slot scratch + compaction keys
+        if (!p.big) p.o_wt = take(L * wmax * 8 * 2);  // slot scratch + compaction keys
         if (!p.lds_mode) {
             p.o_wk = take(L * p.wcap_g * 8);       // key log
             p.o_wl = take(L * p.wcap_g * 2 * 8);   // u64 index, 2 * wcap slots
             p.o_wp = take(L * p.wcap_g / 4 * 4);   // bucket fill counters
         }
+        if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
     }
     for (int d = 0; d <= p.maxdim; ++d) p.o_pairs[d] = take(L * p.pcap[d] * sizeof(Pair));
     p.o_h0s = take(L * 2 * N * 8 + 64);
@@ -313,6 +324,7 @@ std::string err_flags(int e) {
     if (e & ERR_WORK_CAP) s += " working-column-capacity";
     if (e & ERR_VPOOL_CAP) s += " reduction-pool-capacity";
     if (e & ERR_OUT_CAP) s += " output-capacity";
+    if (e & ERR_STEP_LIMIT) s += " reduction-step-limit";
     return s;
 }
 
@@ -480,14 +492,26 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 #define TDA_LAUNCH_RED(LW, P1, P2)                                                                                        \
     hipLaunchKernelGGL((k_reduce_all<LW, P1, P2>), dim3(L), dim3(64), rc.bytes, s, dist, n, p.maxdim, stats, db[1], db[2], rb, rc, \
                        pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
-        if (p.lds_mode) {
+        if (p.big) {
+            BigBufs gb;
+            gb.log = rb.wlog;
+            gb.index = rb.windex;
+            gb.fill = rb.wfill;
+            gb.bref = (uint32_t*)(B + p.o_bref);
+            gb.cap = p.wcap_g;
+            gb.bcap = p.wcap_g;
+            const char* sl = getenv("TDA_STEP_LIMIT");
+            gb.step_limit = sl ? strtoull(sl, nullptr, 10) : (1ull << 26);
+            hipLaunchKernelGGL(k_reduce_big, dim3(L), dim3(kBigT), 0, s, dist, n, p.maxdim, stats, db[1], db[2], rb, gb, pairs1,
+                               pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0);
+        } else if (p.lds_mode) {
             if (p2) TDA_LAUNCH_RED(true, true, true); else if (p1) TDA_LAUNCH_RED(true, true, false); else TDA_LAUNCH_RED(true, false, false);
         } else {
             if (p2) TDA_LAUNCH_RED(false, true, true); else if (p1) TDA_LAUNCH_RED(false, true, false); else TDA_LAUNCH_RED(false, false, false);
         }
 #undef TDA_LAUNCH_RED
         HIPC(hipGetLastError());
-        MARK("k_reduce_all");
+        MARK(p.big ? "k_reduce_big" : "k_reduce_all");
     } else {
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
@@ -537,6 +561,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         errs = 0;
         for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
     }
+    if (errs && getenv("TDA_DEBUG"))
+        fprintf(stderr, "[tda] N=%d L=%d errs=%s force_global=%d scale=%d\n", n, L, err_flags(errs).c_str(), (int)force_global, scale);
     if ((errs & ERR_LDS_SPILL) && !force_global) {
         // a working column outgrew LDS: redo the batch with global-memory tables
         return run_pipeline(a, input_kind, host_or_dev, out, true, scale);

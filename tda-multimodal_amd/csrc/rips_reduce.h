@@ -495,7 +495,9 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
             }
             const uint32_t pw = cfg.piv_lds ? ld_lds(piv, pidx >> 5) : ld_glb((const uint32_t*)pivg, pidx >> 5);
             const bool app = (pw >> (pidx & 31)) & 1u;
-            const int64_t owner = map.find(plo, ln);
+            // the pivot bitmap marks apparent AND residual pivots: a clear bit
+            // is a new pair without probing the residual map
+            const int64_t owner = app ? map.find(plo, ln) : -1;
             TDA_ACC(1, t1);
             TDA_STAMP(t2);
             if (owner >= 0) {

@@ -88,11 +88,25 @@ def test_sweep48_maxdim2_vs_oracle(gpu, oracle):
         assert_same(res[l], orc[l], 2, f"layer{l}")
 
 
-def test_grid144_maxdim2_vs_oracle(gpu, oracle):
+@pytest.mark.parametrize("reduce_kernel", ["auto", "wave", "big"])
+def test_grid144_maxdim2_vs_oracle(gpu, oracle, monkeypatch, reduce_kernel):
+    """C5 layers; both serial-reduction kernels (one wave per layer with
+    compacted scans, and the 1024-thread radix-heap kernel) are forced via
+    TDA_REDUCE and must agree bit-for-bit with the oracle."""
+    monkeypatch.setenv("TDA_REDUCE", reduce_kernel)
     X = gpu.synthetic.sweep144(3)
     res = gpu.ripser_batch(X, maxdim=2)
+    orc = oracle.rips_batch_f32(X, 2)
     for l in range(3):
-        assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, f"grid{l}")
+        assert_same(res[l], orc[l], 2, f"grid{l}")
+
+
+@pytest.mark.parametrize("reduce_kernel", ["wave", "big"])
+def test_torus256_maxdim2_vs_oracle(gpu, oracle, monkeypatch, reduce_kernel):
+    monkeypatch.setenv("TDA_REDUCE", reduce_kernel)
+    X = gpu.synthetic.torus(256, seed=1)
+    res = gpu.ripser_batch(X[None], maxdim=2)[0]
+    assert_same(res, oracle.rips(X, maxdim=2), 2, "torus256")
 
 
 def test_torus512_maxdim1_vs_oracle(gpu, oracle):
