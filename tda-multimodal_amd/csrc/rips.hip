@@ -19,6 +19,7 @@
 #include "../../include/tda_rips.h"
 #include "rips_kernels.h"
 #include "rips_reduce_big.h"
+#include "rips_reduce_small.h"
 
 using namespace tda;
 
@@ -64,14 +65,29 @@ struct Plan {
     uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, vcap_g = 0, sstride = 0;
     bool lds_mode = false;
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
+    bool dense = false;  // N <= 64: dense-bitmap H1 chain + column-parallel H2 phase 1 (rips_reduce_small.h)
+    int E2 = 0;          // edge count rounded up to a power of two (k_edge_class)
+    uint32_t small_lds = 0;  // dynamic LDS of k_reduce_small
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_cls = 0, o_srt = 0, o_p1k = 0, o_p1i = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
 };
+
+bool getenv_is(const char* name, const char* val) {
+    const char* m = getenv(name);
+    return m && !strcmp(m, val);
+}
+
+// pivots per column before a reduction kernel gives up (ERR_STEP_LIMIT): an
+// exit guarantee, far above any real column (torus1024: < 2^15)
+uint64_t step_limit() {
+    const char* sl = getenv("TDA_STEP_LIMIT");
+    return sl ? strtoull(sl, nullptr, 10) : (1ull << 26);
+}
 
 // LDS carve of k_reduce_all (mirrors the kernel): [16][dist][map H1][per-dim:
 // map H2 (dim 2 only) + W (log 8 B + index 16 B per entry) + pivot bitmap]
@@ -101,10 +117,11 @@ ReduceAllCfg reduce_cfg(int n, int maxdim, const uint64_t* piv_words, bool lds_m
         need = std::max<uint64_t>(need, bytes());
     }
     c.bytes = (uint32_t)need;
+    c.step_limit = step_limit();
     return c;
 }
 
-int make_plan(Plan& p, bool force_global, int scale) {
+int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
     const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
     p.mst_words = (binom(N, 2) + 31) / 32 + 1;
     for (int d = 1; d <= p.maxdim; ++d) {
@@ -126,7 +143,24 @@ int make_plan(Plan& p, bool force_global, int scale) {
         // measured (r01): one wave per layer wins up to N = 256 (grid144 md2
         // 20.6 vs 26.8 ms, torus256 md2 64 vs 91 ms); the radix heap above
         const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big");
-        p.big = !p.lds_mode && (want_big || (!want_wave && p.N > kBigMinN));
+        p.big = !p.lds_mode && (force_big || want_big || (!want_wave && p.N > kBigMinN));
+        p.dense = p.lds_mode && p.maxdim >= 1 && p.N <= kDenseMaxN && p.N >= 3 && !want_wave;
+    }
+    if (p.dense) {
+        const uint64_t E = binom(N, 2);
+        p.E2 = 1;
+        while ((uint64_t)p.E2 < E) p.E2 <<= 1;
+        auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
+        const uint64_t pre = 16 + al(4 * N * N);
+        const uint64_t h1 = al(4 * ((binom(N, 3) + 31) / 32)) + al(4 * E) + al(256) + 2 * al(2 * E) + al(4 * p.piv_words[1]) +
+                            al(8 * 1024) + al(4 * 1024);  // LDS residual-pivot map (kernel: when it fits 1024)
+        uint64_t h2 = 0;
+        if (p.maxdim >= 2) {
+            const uint64_t w = 1024;
+            h2 = al(8 * w) + al(16 * w) + al(4 * (2 * w / 8)) + al(16 * w) + (4 * p.piv_words[2] <= 32768 ? al(4 * p.piv_words[2]) : 0);
+        }
+        p.small_lds = (uint32_t)(pre + std::max(h1, h2));
+        if (p.small_lds > (uint32_t)kLdsMax) p.dense = false;
     }
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
@@ -146,6 +180,7 @@ int make_plan(Plan& p, bool force_global, int scale) {
     p.o_mst = take(L * p.mst_words * 4);
     for (int d = 1; d <= p.maxdim; ++d) p.o_piv[d] = take(L * p.piv_words[d] * 4);
     p.o_rowmax = take(L * N * 4);
+    p.o_p1used = take(L * 8);
     p.memset_hi = o;
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
     p.o_tmp = take(L * 2 * p.max_rcap * 8);
@@ -163,6 +198,17 @@ int make_plan(Plan& p, bool force_global, int scale) {
             p.o_wp = take(L * p.wcap_g / 4 * 4);   // bucket fill counters
         }
         if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
+        if (p.dense) {
+            p.o_cls = take(L * p.E2 * 2);
+            p.o_srt = take(L * p.E2 * 2);
+            if (p.maxdim >= 2) {
+                p.o_p1k = take(L * p.rcap[2] * 8);
+                p.o_p1i = take(L * p.rcap[2] * 4);
+                p.o_roff2 = take(L * p.rcap[2] * 8);
+                p.o_rlen2 = take(L * p.rcap[2] * 4);
+                p.o_rpool2 = take(L * p.vpool_cap * 8);
+            }
+        }
     }
     for (int d = 0; d <= p.maxdim; ++d) p.o_pairs[d] = take(L * p.pcap[d] * sizeof(Pair));
     p.o_h0s = take(L * 2 * N * 8 + 64);
@@ -300,6 +346,8 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, true, false);
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_small<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -331,7 +379,7 @@ std::string err_flags(int e) {
 // ------------------------------------------------------------------ pipeline
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
-                 bool force_global = false, int scale = 0) {
+                 bool force_global = false, int scale = 0, bool force_big = false) {
     Plan p;
     p.L = a.L;
     p.N = a.N;
@@ -339,11 +387,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     p.maxdim = a.maxdim;
     p.dtype = a.dtype;
     p.is_dist = input_kind != 0;
-    make_plan(p, force_global, scale);
+    make_plan(p, force_global, scale, force_big);
     const int dev = a.device;
     HIPC(hipSetDevice(dev));
     Workspace& w = *get_ws(dev);
-    std::lock_guard<std::mutex> guard(w.mu);
+    std::unique_lock<std::mutex> guard(w.mu);  // released before any retry (which re-enters)
     if (int rc = ws_prepare(w, p)) return rc;
     if (int rc = set_lds_attrs(dev)) return rc;
     hipStream_t s = a.stream ? (hipStream_t)a.stream : w.stream;
@@ -424,6 +472,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     HIPC(hipGetLastError());
     if (int rc = tm2.mark("k_h0")) return rc;
+    if (p.dense) {  // edge length classes for the dense H1 chain, still off the critical path
+        hipLaunchKernelGGL(k_edge_class, dim3(L), dim3(256), (size_t)p.E2 * 8, s2, dist, n, (uint16_t*)(B + p.o_cls),
+                           (uint16_t*)(B + p.o_srt), p.E2);
+        HIPC(hipGetLastError());
+        if (int rc = tm2.mark("k_edge_class")) return rc;
+    }
     HIPC(hipEventRecord(w.evj, s2));
 
     // ---- H1 .. Hmaxdim: apparent pairs (parallel), residual sort, serial reduction
@@ -492,7 +546,32 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 #define TDA_LAUNCH_RED(LW, P1, P2)                                                                                        \
     hipLaunchKernelGGL((k_reduce_all<LW, P1, P2>), dim3(L), dim3(64), rc.bytes, s, dist, n, p.maxdim, stats, db[1], db[2], rb, rc, \
                        pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
-        if (p.big) {
+        if (p.dense) {
+            SmallBufs sb = {};
+            sb.cls = (const uint16_t*)(B + p.o_cls);
+            sb.srt = (const uint16_t*)(B + p.o_srt);
+            sb.E2 = p.E2;
+            sb.p1_key = (uint64_t*)(B + p.o_p1k);
+            sb.p1_info = (uint32_t*)(B + p.o_p1i);
+            sb.roff2 = (uint64_t*)(B + p.o_roff2);
+            sb.rlen2 = (uint32_t*)(B + p.o_rlen2);
+            sb.rpool2 = (uint64_t*)(B + p.o_rpool2);
+            sb.rpool2_cap = p.vpool_cap;
+            sb.p1_used = (unsigned long long*)(B + p.o_p1used);
+            sb.p1_wcap = 1024;
+            sb.p1_piv_lds = p.maxdim >= 2 && 4 * p.piv_words[2] <= 32768;
+            const int roles = 1 + (p.maxdim >= 2 ? kP1Waves : 0);
+            hipLaunchKernelGGL(k_reduce_small<true>, dim3(L, roles), dim3(64), p.small_lds, s, dist, n, p.maxdim, stats, db[1], db[2],
+                               rb, sb, step_limit(), pairs1, p.pcap[1]);
+            HIPC(hipGetLastError());
+            MARK("k_reduce_small");
+            if (p.maxdim >= 2) {
+                hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[2], rb, rc, sb, pairs2,
+                                   p.pcap[2]);
+                HIPC(hipGetLastError());
+                MARK("k_reduce_h2_finish");
+            }
+        } else if (p.big) {
             BigBufs gb;
             gb.log = rb.wlog;
             gb.index = rb.windex;
@@ -500,8 +579,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             gb.bref = (uint32_t*)(B + p.o_bref);
             gb.cap = p.wcap_g;
             gb.bcap = p.wcap_g;
-            const char* sl = getenv("TDA_STEP_LIMIT");
-            gb.step_limit = sl ? strtoull(sl, nullptr, 10) : (1ull << 26);
+            gb.step_limit = step_limit();
             hipLaunchKernelGGL(k_reduce_big, dim3(L), dim3(kBigT), 0, s, dist, n, p.maxdim, stats, db[1], db[2], rb, gb, pairs1,
                                pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0);
         } else if (p.lds_mode) {
@@ -511,7 +589,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         }
 #undef TDA_LAUNCH_RED
         HIPC(hipGetLastError());
-        MARK(p.big ? "k_reduce_big" : "k_reduce_all");
+        if (!p.dense) MARK(p.big ? "k_reduce_big" : "k_reduce_all");
     } else {
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
@@ -565,11 +643,19 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         fprintf(stderr, "[tda] N=%d L=%d errs=%s force_global=%d scale=%d\n", n, L, err_flags(errs).c_str(), (int)force_global, scale);
     if ((errs & ERR_LDS_SPILL) && !force_global) {
         // a working column outgrew LDS: redo the batch with global-memory tables
+        guard.unlock();
         return run_pipeline(a, input_kind, host_or_dev, out, true, scale);
+    }
+    if ((errs & ERR_WORK_CAP) && !p.big && !getenv_is("TDA_REDUCE", "wave")) {
+        // a working column outgrew the one-wave HBM tables: full scans of a
+        // large column are the slow case, so switch to the radix-heap kernel
+        guard.unlock();
+        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true);
     }
     if ((errs & ~(ERR_LDS_SPILL)) == (errs & (ERR_WORK_CAP | ERR_VPOOL_CAP)) && errs && scale < 2) {
         // working column / reduced-column pool too small: retry with larger buffers
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1);
+        guard.unlock();
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big);
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
 #ifdef TDA_PROFILE
@@ -611,7 +697,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             R->checksum[l * nd + d] = st.checksum[d];
             R->n_all[l * nd + d] = st.all_pairs[d];
             R->n_cols[l * nd + d] = st.n_columns[d];
-            R->n_res[l * nd + d] = st.n_residual[d];
+            R->n_res[l * nd + d] = st.n_residual[d] - st.nskip[d];
             R->n_add[l * nd + d] = st.n_adds[d];
             total += (size_t)c;
         }
@@ -657,13 +743,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         R->stage_ms.push_back(t);
         R->stage_name.push_back(tm.names[i]);
     }
-    if (tm.on) {  // side stream: H0
+    for (size_t i = 0; i < tm2.names.size(); ++i) {  // side stream: H0, edge classes
         float t = 0.0f;
-        (void)hipEventElapsedTime(&t, w.stage_ev2[0], w.stage_ev2[1]);
+        (void)hipEventElapsedTime(&t, w.stage_ev2[i], w.stage_ev2[i + 1]);
         R->stage_ms.push_back(t);
-        R->stage_name.push_back("k_h0");
+        R->stage_name.push_back(tm2.names[i]);
     }
-    o.n_stages = (int32_t)tm.names.size();
+    o.n_stages = (int32_t)R->stage_name.size();
     o.stage_name = R->stage_name.data();
     o.stage_ms = R->stage_ms.data();
     *out = &R->pub;

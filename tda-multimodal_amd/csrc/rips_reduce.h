@@ -250,17 +250,35 @@ struct Reduce2Bufs {
     uint64_t mst_words;
 };
 
+// H2 phase 1 -> phase 2 hand-off (rips_reduce_small.h)
+struct SmallBufs {
+    const uint16_t* cls;  // [L][E2] class of each edge
+    const uint16_t* srt;  // [L][E2] edges sorted by length
+    int E2;
+    uint64_t* p1_key;     // [L][rcap2] pivot key after phase 1 (kEmpty64: zero column)
+    uint32_t* p1_info;    // [L][rcap2] additions | kP1Overflow
+    uint64_t* roff2;      // [L][rcap2] phase-1 working column, then R_j, in rpool2
+    uint32_t* rlen2;
+    uint64_t* rpool2;     // [L][rpool2_cap]
+    uint64_t rpool2_cap;
+    unsigned long long* p1_used;  // [L] rpool2 entries taken by phase 1 (zeroed per call)
+    uint32_t p1_wcap;     // phase-1 LDS toggle-set capacity
+    int p1_piv_lds;       // H2 pivot bitmap staged in LDS by phase-1 waves
+};
+constexpr uint32_t kP1Overflow = 1u << 31;  // phase-1 column outgrew its LDS table
+
 struct Reduce2Cfg {  // per-dim LDS carve, decided on the host
     uint32_t wcap, rmap_lds_cap;  // rmap_lds_cap = 0 -> global map
     int piv_lds;
 };
 struct ReduceAllCfg {
     Reduce2Cfg dim[3];
+    uint64_t step_limit;  // pivots per column before giving up (exit guarantee)
     int dist_lds;
     uint32_t bytes;  // dynamic LDS of the launch
 };
 
-enum : int32_t { ERR_LDS_SPILL = 32 };
+enum : int32_t { ERR_LDS_SPILL = 32, ERR_STEP_LIMIT = 64 };  // STEP_LIMIT: a column exceeded the pivot budget
 
 // residual pivot map of one dim: open addressing, key = row payload lo32
 struct PivMap {
@@ -291,6 +309,7 @@ struct ReduceCtx {
     LayerStats* st;
     unsigned char* lds;  // start of the per-dim LDS region
     int l, ln;
+    uint64_t step_limit;
 };
 
 // payload (lo32) of a d-simplex with descending vertices, as the dim-(d-1)
@@ -306,9 +325,12 @@ __device__ __forceinline__ uint32_t row_payload(const int (&t)[NVTX]) {
 // H_{DIM-1} deaths found by the serial reduction (clearing; k_apparent only
 // knew the apparent ones).  Returns this dim's map (valid until the kernel ends
 // if it lives in a persistent region).
-template <int DIM, bool LDSW, bool PACKED, bool PREV_PACKED>
+// PH2: phase 2 of the split H2 reduction (rips_reduce_small.h): every column
+// starts from its phase-1 result in `sb` instead of its coboundary.
+template <int DIM, bool LDSW, bool PACKED, bool PREV_PACKED, bool PH2 = false>
 __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bufs& rb, const Reduce2Cfg& cfg, PivMap& map,
-                           const PivMap* prev, unsigned char* map_lds, Pair* __restrict__ pairs, uint64_t pcap) {
+                           const PivMap* prev, unsigned char* map_lds, Pair* __restrict__ pairs, uint64_t pcap,
+                           const SmallBufs* sb = nullptr) {
     constexpr int NV = DIM + 2;  // vertices of a row simplex
     using Lo = RowLo<NV>;
     const int l = c.l, ln = c.ln, n = c.n;
@@ -377,10 +399,15 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
     __syncthreads();
     const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
 
-    uint64_t* roff = rb.roff + (size_t)l * b.rcap;
-    uint32_t* rlen = rb.rlen + (size_t)l * b.rcap;
-    uint64_t* rpool = rb.rpool + (size_t)l * rb.rpool_cap;
+    uint64_t* roff = PH2 ? sb->roff2 + (size_t)l * b.rcap : rb.roff + (size_t)l * b.rcap;
+    uint32_t* rlen = PH2 ? sb->rlen2 + (size_t)l * b.rcap : rb.rlen + (size_t)l * b.rcap;
+    const uint64_t pool_cap = PH2 ? sb->rpool2_cap : rb.rpool_cap;
+    uint64_t* rpool = PH2 ? sb->rpool2 + (size_t)l * sb->rpool2_cap : rb.rpool + (size_t)l * rb.rpool_cap;
     uint64_t rused = 0;
+    if (PH2) {
+        rused = (uint64_t)sb->p1_used[l];
+        if (rused > pool_cap) rused = pool_cap;
+    }
     Pair* P = pairs + (size_t)l * pcap;
     uint64_t cs = 0, npairs = 0, nadds = 0, nskip = 0;
     int err = 0;  // wave-uniform
@@ -437,6 +464,33 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
         }
     };
 
+    auto emit_essential = [&](uint64_t j, float sdm, uint64_t sidx) {
+        if (ln == 0) {
+            uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
+            if (pos < pcap)
+                P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
+            else
+                atomicOr(&st->err, ERR_PAIR_CAP);
+            rlen[j] = 0;
+        }
+    };
+    auto emit_pair = [&](uint64_t j, float sdm, uint64_t sidx, float pd, uint64_t pidx, uint32_t plo) {
+        if (ln == 0) {
+            if (pd > sdm) {
+                uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
+                if (pos < pcap)
+                    P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
+                else
+                    atomicOr(&st->err, ERR_PAIR_CAP);
+            }
+            map.insert(plo, (uint32_t)j);
+            atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
+            if (piv != pivg) atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
+        }
+        cs += pair_hash(sidx, pidx);
+        npairs += 1;
+    };
+
     for (uint64_t j = 0; j < nres && !err; ++j) {
         const uint64_t key = ld_glb(resid, j);
         const uint64_t sidx = key_idx(key);
@@ -455,30 +509,63 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
             if (ln == 0) rlen[j] = 0;
             continue;
         }
-        if (!room((uint32_t)n)) break;
-        cob(vs, sdm);
+        if (PH2 && !(ld_glb(sb->p1_info + (size_t)l * b.rcap, j) & kP1Overflow)) {
+            const uint32_t info = ld_glb(sb->p1_info + (size_t)l * b.rcap, j);
+            const uint64_t pk1 = ld_glb(sb->p1_key + (size_t)l * b.rcap, j);
+            nadds += info;
+            if (pk1 == kEmpty64) {
+                emit_essential(j, sdm, sidx);
+                continue;
+            }
+            const uint32_t plo1 = 0xFFFFFFFFu - (uint32_t)pk1;
+            uint64_t pidx1;
+            if (PACKED) {
+                int t1[NV];
+                Lo::unpack(plo1, t1);
+                pidx1 = encode<DIM + 1>(t1);
+            } else {
+                pidx1 = plo1;
+            }
+            // not apparent (phase 1 stopped there): a set bit is an earlier residual pivot
+            const uint32_t pw1 = cfg.piv_lds ? ld_lds(piv, pidx1 >> 5) : ld_glb((const uint32_t*)pivg, pidx1 >> 5);
+            const int64_t own1 = ((pw1 >> (pidx1 & 31)) & 1u) ? map.find(plo1, ln) : -1;
+            if (own1 < 0) {  // new pair; R_j is the stored phase-1 column
+                emit_pair(j, sdm, sidx, __uint_as_float((uint32_t)(pk1 >> 32)), pidx1, plo1);
+                continue;
+            }
+            // continue Ripser's loop from the stored working column
+            const uint64_t o0 = roff[j];
+            const uint32_t ol = rlen[j];
+            if (!room(ol)) break;
+            for (uint32_t e0 = 0; e0 < ol; e0 += 64) {
+                const uint32_t e = e0 + ln;
+                W.toggle_pass(e < ol ? ld_glb((const uint64_t*)rpool, o0 + e) : 0, e < ol, ln);
+            }
+        } else {
+            if (!room((uint32_t)n)) break;
+            cob(vs, sdm);
+        }
         __syncthreads();
-        for (;;) {
+        for (uint64_t step = 0;; ++step) {
             uint64_t pk;
             uint32_t nlive;
             TDA_STAMP(t0);
             W.scan(ln, pk, nlive);
             TDA_ACC(0, t0);
+            if (step >= c.step_limit) {
+                if (ln == 0)
+                    printf("k_reduce_all: layer %d dim %d column %llu (idx %llu) step limit: pivot %016llx cnt %u live %u\n", l,
+                           DIM, (unsigned long long)j, (unsigned long long)sidx, (unsigned long long)pk, W.cnt, nlive);
+                err = 3;
+                break;
+            }
             if (W.cnt > 2 * nlive + 256) {
                 TDA_STAMP(t6);
                 W.compact(ln);
                 TDA_ACC(6, t6);
             }
             if (pk == kEmpty64) {
-                // zero column: essential class (birth = diam sigma_j)
-                if (ln == 0) {
-                    uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-                    if (pos < pcap)
-                        P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
-                    else
-                        atomicOr(&st->err, ERR_PAIR_CAP);
-                    rlen[j] = 0;
-                }
+                emit_essential(j, sdm, sidx);  // zero column: essential class (birth = diam sigma_j)
                 break;
             }
             TDA_STAMP(t1);
@@ -560,21 +647,8 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
                 TDA_ACC(3, t3);
             } else {
                 // new persistence pair (sigma_j, pivot); R_j = live keys of W
-                if (ln == 0) {
-                    if (pd > sdm) {
-                        uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-                        if (pos < pcap)
-                            P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
-                        else
-                            atomicOr(&st->err, ERR_PAIR_CAP);
-                    }
-                    map.insert(plo, (uint32_t)j);
-                    atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
-                    if (piv != pivg) atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
-                }
-                cs += pair_hash(sidx, pidx);
-                npairs += 1;
-                if (rused + nlive > rb.rpool_cap) {
+                emit_pair(j, sdm, sidx, pd, pidx, plo);
+                if (rused + nlive > pool_cap) {
                     err = 2;
                     break;
                 }
@@ -596,12 +670,13 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
     if (ln == 0) {
         if (err == 1) atomicOr(&st->err, LDSW ? (int32_t)ERR_LDS_SPILL : (int32_t)ERR_WORK_CAP);
         if (err == 2) atomicOr(&st->err, ERR_VPOOL_CAP);
+        if (err == 3) atomicOr(&st->err, ERR_STEP_LIMIT);
         atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)cs);
         atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)npairs);
         atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)nadds);
         // cleared columns were counted as columns by k_apparent
         atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)(0ull - nskip));
-        atomicAdd((unsigned long long*)&st->n_residual[DIM], (unsigned long long)(0ull - nskip));
+        st->nskip[DIM] = nskip;
 #ifdef TDA_PROFILE
         prof[7] = clock64() - t_all;
         for (int i = 0; i < 8; ++i) st->prof[DIM][i] = prof[i];
@@ -628,6 +703,7 @@ __global__ __launch_bounds__(64) void k_reduce_all(const float* __restrict__ dis
     c.ln = ln;
     c.st = st;
     c.r = st->thresh;
+    c.step_limit = cfg.step_limit;
     c.D = dist + (size_t)l * n * n;
     if (LDSW) {  // LDS mode (N <= 64): the matrix always fits
         float* dl = (float*)p;
@@ -646,6 +722,51 @@ __global__ __launch_bounds__(64) void k_reduce_all(const float* __restrict__ dis
         c.lds = p + 12ull * cfg.dim[2].rmap_lds_cap;
         reduce_dim<2, LDSW, P2, P1>(c, b2, rb, cfg.dim[2], m2, &m1, map2_lds, pairs2, pcap2);
     }
+}
+
+// Phase 2 of the split H2 reduction (N <= 64): one wave per layer walks the
+// H2 columns in order on top of k_reduce_small's phase-1 results.  LDS:
+// [16 B][distance matrix][H1 residual-pivot map][H2 map + W + pivot bitmap],
+// the k_reduce_all carve.
+__global__ __launch_bounds__(64) void k_reduce_h2_finish(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                         DimBufs b2, Reduce2Bufs rb, ReduceAllCfg cfg, SmallBufs sb,
+                                                         Pair* __restrict__ pairs2, uint64_t pcap2) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, ln = threadIdx.x;
+    LayerStats* st = stats + l;
+    unsigned char* p = smem + 16;
+    ReduceCtx c;
+    c.n = n;
+    c.l = l;
+    c.ln = ln;
+    c.st = st;
+    c.r = st->thresh;
+    c.step_limit = cfg.step_limit;
+    float* dl = (float*)p;
+    stage_to_lds(dl, dist + (size_t)l * n * n, 4ull * n * n, ln, 64);
+    p += (4ull * n * n + 15) & ~15ull;
+    c.D = dl;
+    // H1 residual pivot map: HBM mirror written by the H1 chain, staged to LDS
+    PivMap m1;
+    m1.k = rb.rmap_keys + ((size_t)l * 2) * rb.rmap_stride;
+    m1.v = rb.rmap_vals + ((size_t)l * 2) * rb.rmap_stride;
+    m1.mask = st->rmask[1];
+    const uint64_t cap1 = m1.mask + 1;
+    if (cap1 <= cfg.dim[1].rmap_lds_cap) {
+        uint64_t* k1 = (uint64_t*)p;
+        uint32_t* v1 = (uint32_t*)(p + 8ull * cap1);
+        for (uint64_t e = ln; e < cap1; e += 64) {
+            k1[e] = m1.k[e];
+            v1[e] = m1.v[e];
+        }
+        m1.k = k1;
+        m1.v = v1;
+    }
+    p += 12ull * cfg.dim[1].rmap_lds_cap;
+    __syncthreads();
+    PivMap m2;
+    c.lds = p + 12ull * cfg.dim[2].rmap_lds_cap;
+    reduce_dim<2, true, true, true, true>(c, b2, rb, cfg.dim[2], m2, &m1, p, pairs2, pcap2, &sb);
 }
 
 }  // namespace tda

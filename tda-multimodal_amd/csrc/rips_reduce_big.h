@@ -19,7 +19,6 @@ namespace tda {
 constexpr int kBigT = 1024;    // threads per layer
 constexpr int kBigW = kBigT / 64;
 constexpr int kNB = 33;        // radix buckets (f32 diameter bits)
-enum : int32_t { ERR_STEP_LIMIT = 64 };  // a column exceeded BigBufs::step_limit pivots (never expected)
 
 struct BigBufs {
     uint64_t* log;       // [L][cap] keys (| kDead)
@@ -506,7 +505,7 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
         atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)npairs);
         atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)nadds);
         atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)(0ull - nskip));
-        atomicAdd((unsigned long long*)&st->n_residual[DIM], (unsigned long long)(0ull - nskip));
+        st->nskip[DIM] = nskip;
     }
     __syncthreads();
 }

@@ -41,46 +41,44 @@ class LayerResult:
     dist: np.ndarray | None = None
 
 
+def _arr(ptr, n, dtype):
+    """Copy n elements of a library-owned C array (one memcpy, no per-element work)."""
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.frombuffer(ctypes.string_at(ptr, n * np.dtype(dtype).itemsize), dtype=dtype)
+
+
 def _unpack(res_p, want_dist: bool) -> tuple[list, float]:
     r = res_p.contents
     L, md, N = int(r.L), int(r.maxdim), int(r.N)
     nd = md + 1
-    cnt = np.ctypeslib.as_array(r.count, shape=(L * nd,)).copy()
-    off = np.ctypeslib.as_array(r.offset, shape=(L * nd,)).copy()
+    cnt = _arr(r.count, L * nd, np.int64)
+    off = _arr(r.offset, L * nd, np.int64)
     total = int(cnt.sum())
-    if total:
-        birth = np.ctypeslib.as_array(r.birth, shape=(total,)).astype(np.float64)
-        death = np.ctypeslib.as_array(r.death, shape=(total,)).astype(np.float64)
-        bidx = np.ctypeslib.as_array(r.birth_idx, shape=(total,)).copy()
-        didx = np.ctypeslib.as_array(r.death_idx, shape=(total,)).copy()
-    else:
-        birth = death = np.zeros(0)
-        bidx = didx = np.zeros(0, dtype=np.int64)
-    thr = np.ctypeslib.as_array(r.thresh, shape=(L,)).copy()
-    ne = np.ctypeslib.as_array(r.num_edges, shape=(L,)).copy()
-    cs = np.ctypeslib.as_array(r.checksum, shape=(L * nd,)).copy()
-    na = np.ctypeslib.as_array(r.n_all_pairs, shape=(L * nd,)).copy()
-    nc = np.ctypeslib.as_array(r.n_columns, shape=(L * nd,)).copy()
-    nr = np.ctypeslib.as_array(r.n_residual, shape=(L * nd,)).copy()
-    na2 = np.ctypeslib.as_array(r.n_adds, shape=(L * nd,)).copy()
+    # one (total, 2) float64 block; every diagram is a view into it
+    pairs = np.empty((total, 2), dtype=np.float64)
+    pairs[:, 0] = _arr(r.birth, total, np.float32)
+    pairs[:, 1] = _arr(r.death, total, np.float32)
+    bidx = _arr(r.birth_idx, total, np.int64)
+    didx = _arr(r.death_idx, total, np.int64)
+    thr = _arr(r.thresh, L, np.float32).tolist()
+    ne = _arr(r.num_edges, L, np.int64).tolist()
+    cs = _arr(r.checksum, L * nd, np.uint64).reshape(L, nd).tolist()
+    na = _arr(r.n_all_pairs, L * nd, np.int64).reshape(L, nd).tolist()
+    nc = _arr(r.n_columns, L * nd, np.int64).reshape(L, nd).tolist()
+    nr = _arr(r.n_residual, L * nd, np.int64).reshape(L, nd).tolist()
+    na2 = _arr(r.n_adds, L * nd, np.int64).reshape(L, nd).tolist()
     dist = None
     if want_dist and bool(r.dist):
-        dist = np.ctypeslib.as_array(r.dist, shape=(L, N, N)).copy()
+        dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N)
+    bounds = np.stack([off, off + cnt], axis=1).reshape(L, nd, 2).tolist()
     out = []
     for l in range(L):
-        dg, bi, di = [], [], []
-        for d in range(nd):
-            c, o = int(cnt[l * nd + d]), int(off[l * nd + d])
-            dg.append(np.stack([birth[o:o + c], death[o:o + c]], axis=1) if c else np.zeros((0, 2)))
-            bi.append(bidx[o:o + c])
-            di.append(didx[o:o + c])
+        bl = bounds[l]
         out.append(LayerResult(
-            dgms=dg, birth_idx=bi, death_idx=di, num_edges=int(ne[l]), thresh=float(thr[l]),
-            checksum=[int(x) for x in cs[l * nd:(l + 1) * nd]],
-            n_all_pairs=[int(x) for x in na[l * nd:(l + 1) * nd]],
-            n_columns=[int(x) for x in nc[l * nd:(l + 1) * nd]],
-            n_residual=[int(x) for x in nr[l * nd:(l + 1) * nd]],
-            n_adds=[int(x) for x in na2[l * nd:(l + 1) * nd]],
+            dgms=[pairs[a:b] for a, b in bl], birth_idx=[bidx[a:b] for a, b in bl],
+            death_idx=[didx[a:b] for a, b in bl], num_edges=ne[l], thresh=thr[l], checksum=cs[l],
+            n_all_pairs=na[l], n_columns=nc[l], n_residual=nr[l], n_adds=na2[l],
             dist=None if dist is None else dist[l],
         ))
     stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(int(r.n_stages))]

@@ -101,10 +101,12 @@ def test_grid144_maxdim2_vs_oracle(gpu, oracle, monkeypatch, reduce_kernel):
         assert_same(res[l], orc[l], 2, f"grid{l}")
 
 
-@pytest.mark.parametrize("reduce_kernel", ["wave", "big"])
-def test_torus256_maxdim2_vs_oracle(gpu, oracle, monkeypatch, reduce_kernel):
+@pytest.mark.parametrize("reduce_kernel,seed", [("auto", 1), ("big", 1), ("wave", 0)])
+def test_torus256_maxdim2_vs_oracle(gpu, oracle, monkeypatch, reduce_kernel, seed):
+    """seed 1 overflows the one-wave kernel's working column at scale 0; the
+    auto policy must then finish on the radix-heap kernel."""
     monkeypatch.setenv("TDA_REDUCE", reduce_kernel)
-    X = gpu.synthetic.torus(256, seed=1)
+    X = gpu.synthetic.torus(256, seed=seed)
     res = gpu.ripser_batch(X[None], maxdim=2)[0]
     assert_same(res, oracle.rips(X, maxdim=2), 2, "torus256")
 
