@@ -1,0 +1,72 @@
+"""rocprofv3 --pmc CSVs -> profiles/pmc_<workload>.json (HBM bytes per launch).
+
+Per MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are the
+L2 memory-side (fabric) request counters in KiB; on gfx950 FETCH_SIZE reports
+half the bytes of a wide coalesced read, so it is doubled here; WRITE_SIZE is
+taken as is.  Infinity-Cache hits are counted (not excluded), so at small N
+this is an upper bound on DRAM bytes.  Per kernel: mean over its dispatches.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short_name(name: str) -> str:
+    """'void tda::k_apparent<1, true>(...)' -> 'k_apparent<1>' (bench.py stage names)."""
+    name = re.sub(r"^void ", "", name).split("(")[0].replace("tda::", "").strip()
+    if "<" in name:
+        base, targs = name.split("<", 1)
+        args = [a.strip() for a in targs.rstrip(">").split(",")]
+        return f"{base}<{args[0]}>" if base == "k_apparent" else base
+    return name
+
+
+def load(d: str, counter: str) -> dict:
+    per = collections.defaultdict(dict)  # kernel -> dispatch -> value
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                k = short_name(row["Kernel_Name"])
+                disp = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                per[k][disp] = per[k].get(disp, 0.0) + float(row["Counter_Value"])
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="sweep48")
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    a = ap.parse_args()
+    fetch = load(a.fetch_dir, "FETCH_SIZE")
+    write = load(a.write_dir, "WRITE_SIZE")
+    out = {"workload": a.workload,
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; KiB -> bytes; FETCH_SIZE x2 "
+                     "(gfx950 correction, MI355X_MICROARCH.md HBM section); mean over dispatches",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f = list(fetch.get(k, {}).values())
+        w = list(write.get(k, {}).values())
+        fb = 2.0 * 1024.0 * sum(f) / len(f) if f else 0.0
+        wb = 1024.0 * sum(w) / len(w) if w else 0.0
+        out["kernels"][k] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                             "hbm_bytes_per_launch": fb + wb, "dispatches": max(len(f), len(w))}
+    path = os.path.join(ROOT, "profiles", f"pmc_{a.workload}.json")
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out["kernels"], indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,11 +1,17 @@
 #!/bin/bash
-# rocprofv3 kernel trace + stats of the default bench (round artifacts -> gpurun_out/prof_*)
+# rocprofv3 kernel trace + stats of the default bench -> gpurun_out/prof_trace
+#   usage: bash tools/profile_bench.sh [workload] [extra bench args]
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+WL=${1:-sweep48}
+shift
+ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd /tmp && export TMPDIR=/tmp && cd "$ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace -o run -- \
-    python3 bench.py --steps 20 --warmup 3 --no-cpu > gpurun_out/prof_bench.log 2>&1
+rm -rf gpurun_out/prof_$WL
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$WL -o run -- \
+    python3 bench.py --workload $WL --steps 20 --warmup 3 --no-cpu "$@" > gpurun_out/prof_$WL.txt 2>&1
 rc=$?
 echo "rocprof rc=$rc"
-find gpurun_out/prof_trace -name "*.csv" | head -20
+tail -1 gpurun_out/prof_$WL.txt
+find gpurun_out/prof_$WL -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats_$WL.csv \;
 exit $rc
