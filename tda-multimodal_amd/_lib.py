@@ -79,9 +79,13 @@ EXPORTS = ("tda_rips_batch", "tda_rips_dm", "tda_rips_free", "tda_last_error", "
 _lib = None
 
 
-def build(verbose: bool = False) -> str:
-    """Compile csrc/rips.hip for gfx950 into _build/libtda_rips.so (in-tree)."""
-    os.makedirs(BUILD_DIR, exist_ok=True)
+def build(verbose: bool = False, out: str | None = None, extra_flags: tuple = ()) -> str:
+    """Compile csrc/rips.hip for gfx950 into _build/libtda_rips.so (in-tree).
+
+    ``out``/``extra_flags`` build variants (e.g. ``-DTDA_PROFILE`` into another
+    path, selected at load time with TDA_RIPS_LIB)."""
+    out = out or LIB_PATH
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     src = os.path.join(CSRC, "rips.hip")
     cmd = [
         os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"),
@@ -91,8 +95,9 @@ def build(verbose: bool = False) -> str:
         "-shared",
         "-fPIC",
         "-I" + INCLUDE,
+        *extra_flags,
         "-o",
-        LIB_PATH + ".tmp",
+        out + ".tmp",
         src,
     ]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -100,8 +105,8 @@ def build(verbose: bool = False) -> str:
         raise RuntimeError("hipcc failed:\n" + r.stderr[-4000:])
     if verbose and r.stderr:
         print(r.stderr, file=sys.stderr)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def lib():

@@ -66,12 +66,15 @@ struct Plan {
     bool lds_mode = false;
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
     bool dense = false;  // N <= 64: dense-bitmap H1 chain + column-parallel H2 phase 1 (rips_reduce_small.h)
-    int E2 = 0;          // edge count rounded up to a power of two (k_edge_class)
-    uint32_t small_lds = 0;  // dynamic LDS of k_reduce_small
+    int E2 = 0;          // edge count rounded up to a power of two (k_h1_prep sort)
+    int dK = 0;          // dense H1 bitmap words per lane
+    uint32_t inv_stride = 0;  // rank -> edge table stride (C(N,3) rounded up)
+    uint32_t small_lds = 0;   // dynamic LDS of k_reduce_small
+    uint32_t prep_lds = 0;    // dynamic LDS of k_h1_prep
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_cls = 0, o_srt = 0, o_p1k = 0, o_p1i = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -146,21 +149,25 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         p.big = !p.lds_mode && (force_big || want_big || (!want_wave && p.N > kBigMinN));
         p.dense = p.lds_mode && p.maxdim >= 1 && p.N <= kDenseMaxN && p.N >= 3 && !want_wave;
     }
-    if (p.dense) {
-        const uint64_t E = binom(N, 2);
+    if (p.dense) {  // carve of rips_reduce_small.h (h1_chain / h2_phase1), mirrored here
+        const uint64_t E = binom(N, 2), T3 = binom(N, 3);
         p.E2 = 1;
         while ((uint64_t)p.E2 < E) p.E2 <<= 1;
+        p.dK = (int)std::max<uint64_t>(1, (((T3 + 31) / 32) + 63) / 64);
+        p.inv_stride = (uint32_t)align_up(T3, 8);
         auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
         const uint64_t pre = 16 + al(4 * N * N);
-        const uint64_t h1 = al(4 * ((binom(N, 3) + 31) / 32)) + al(4 * E) + al(256) + 2 * al(2 * E) + al(4 * p.piv_words[1]) +
-                            al(8 * 1024) + al(4 * 1024);  // LDS residual-pivot map (kernel: when it fits 1024)
+        const uint64_t WP = 64ull * p.dK;
+        const uint64_t h1 = al(16 * E) + al(2ull * p.inv_stride) + 2 * al(4 * WP) + al(4 * p.piv_words[1]) +
+                            al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols);
         uint64_t h2 = 0;
         if (p.maxdim >= 2) {
-            const uint64_t w = 1024;
-            h2 = al(8 * w) + al(16 * w) + al(4 * (2 * w / 8)) + al(16 * w) + (4 * p.piv_words[2] <= 32768 ? al(4 * p.piv_words[2]) : 0);
+            const uint64_t w = kP1WCap;
+            h2 = (uint64_t)kSmallW * (8 * w + 16 * w + al(4 * (2 * w / 8)) + 16 * w);
         }
         p.small_lds = (uint32_t)(pre + std::max(h1, h2));
-        if (p.small_lds > (uint32_t)kLdsMax) p.dense = false;
+        p.prep_lds = (uint32_t)(pre + (uint64_t)p.E2 * 20);
+        if (p.small_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.dK > kMaxK) p.dense = false;
     }
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
@@ -181,6 +188,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
     for (int d = 1; d <= p.maxdim; ++d) p.o_piv[d] = take(L * p.piv_words[d] * 4);
     p.o_rowmax = take(L * N * 4);
     p.o_p1used = take(L * 8);
+    p.o_p1next = take(L * 4);
     p.memset_hi = o;
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
     p.o_tmp = take(L * 2 * p.max_rcap * 8);
@@ -199,8 +207,8 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         }
         if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
         if (p.dense) {
-            p.o_cls = take(L * p.E2 * 2);
-            p.o_srt = take(L * p.E2 * 2);
+            p.o_recs = take(L * binom(N, 2) * 16);
+            p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
             if (p.maxdim >= 2) {
                 p.o_p1k = take(L * p.rcap[2] * 8);
                 p.o_p1i = take(L * p.rcap[2] * 4);
@@ -346,7 +354,8 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, true, false);
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
-    HIPC(hipFuncSetAttribute((const void*)k_reduce_small<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_small, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_h1_prep, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -472,11 +481,16 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     HIPC(hipGetLastError());
     if (int rc = tm2.mark("k_h0")) return rc;
-    if (p.dense) {  // edge length classes for the dense H1 chain, still off the critical path
-        hipLaunchKernelGGL(k_edge_class, dim3(L), dim3(256), (size_t)p.E2 * 8, s2, dist, n, (uint16_t*)(B + p.o_cls),
-                           (uint16_t*)(B + p.o_srt), p.E2);
+    DenseBufs dnb = {};
+    if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
+        dnb.recs = (EdgeRec*)(B + p.o_recs);
+        dnb.inv = (uint16_t*)(B + p.o_inv);
+        dnb.E = (uint32_t)binom((uint64_t)n, 2);
+        dnb.inv_stride = p.inv_stride;
+        dnb.K = p.dK;
+        hipLaunchKernelGGL(k_h1_prep, dim3(L), dim3(1024), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.E2, stats);
         HIPC(hipGetLastError());
-        if (int rc = tm2.mark("k_edge_class")) return rc;
+        if (int rc = tm2.mark("k_h1_prep")) return rc;
     }
     HIPC(hipEventRecord(w.evj, s2));
 
@@ -548,9 +562,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                        pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
         if (p.dense) {
             SmallBufs sb = {};
-            sb.cls = (const uint16_t*)(B + p.o_cls);
-            sb.srt = (const uint16_t*)(B + p.o_srt);
-            sb.E2 = p.E2;
+            sb.p1_next = (uint32_t*)(B + p.o_p1next);
             sb.p1_key = (uint64_t*)(B + p.o_p1k);
             sb.p1_info = (uint32_t*)(B + p.o_p1i);
             sb.roff2 = (uint64_t*)(B + p.o_roff2);
@@ -558,16 +570,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             sb.rpool2 = (uint64_t*)(B + p.o_rpool2);
             sb.rpool2_cap = p.vpool_cap;
             sb.p1_used = (unsigned long long*)(B + p.o_p1used);
-            sb.p1_wcap = 1024;
-            sb.p1_piv_lds = p.maxdim >= 2 && 4 * p.piv_words[2] <= 32768;
-            const int roles = 1 + (p.maxdim >= 2 ? kP1Waves : 0);
-            hipLaunchKernelGGL(k_reduce_small<true>, dim3(L, roles), dim3(64), p.small_lds, s, dist, n, p.maxdim, stats, db[1], db[2],
-                               rb, sb, step_limit(), pairs1, p.pcap[1]);
+            sb.p1_wcap = kP1WCap;
+            const int roles = 1 + (p.maxdim >= 2 ? kP1Blocks : 0);
+            hipLaunchKernelGGL(k_reduce_small, dim3(L, roles), dim3(kSmallT), p.small_lds, s, dist, n, p.maxdim, stats, db[1], db[2],
+                               rb, sb, dnb, step_limit(), pairs1, p.pcap[1]);
             HIPC(hipGetLastError());
             MARK("k_reduce_small");
             if (p.maxdim >= 2) {
-                hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[2], rb, rc, sb, pairs2,
-                                   p.pcap[2]);
+                hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[1], db[2], rb, rc, sb,
+                                   pairs2, p.pcap[2]);
                 HIPC(hipGetLastError());
                 MARK("k_reduce_h2_finish");
             }
@@ -659,6 +670,19 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
 #ifdef TDA_PROFILE
+    if (p.dense) {
+        int arg = 0;
+        uint64_t p1max = 0;
+        for (int l = 0; l < L; ++l) {
+            if (w.hstats[l].prof[0][0] > w.hstats[arg].prof[0][0]) arg = l;
+            p1max = std::max<uint64_t>(p1max, w.hstats[l].prof[1][0]);
+        }
+        const uint64_t* q = w.hstats[arg].prof[0];
+        fprintf(stderr, "[tda-prof] dense H1 slowest layer %d adds %lld: total %llu pivot %llu (calls %llu ties %llu) cob_app %llu add_owner %llu new_pair %llu cycles; H2 phase-1 slowest wave %llu cycles\n",
+                arg, (long long)w.hstats[arg].n_adds[1], (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[7],
+                (unsigned long long)q[2], (unsigned long long)q[3], (unsigned long long)q[4], (unsigned long long)q[5],
+                (unsigned long long)p1max);
+    }
     for (int d = 1; d <= p.maxdim; ++d) {
         uint64_t mx[8] = {0};
         int arg = 0;

@@ -198,6 +198,13 @@ __host__ __device__ __forceinline__ uint64_t filt_key(float diam, uint64_t idx) 
 }
 
 // ---------------------------------------------------------------- wave ops
+// Synchronisation of ONE wave's lanes through memory (LDS and global): waits
+// for the wave's outstanding memory operations and fences the compiler, but
+// issues no s_barrier, so waves of one workgroup can run independent loops.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));

@@ -165,14 +165,14 @@ struct KeySet {
                 }
                 slots[e] = h;
             }
-            __syncthreads();
+            wave_sync();
             for (uint32_t e = ln; e < c; e += 64) {
                 index[slots[e]] = 0;
                 fill[slots[e] >> 3] = 0;
             }
         }
         cnt = 0;
-        __syncthreads();
+        wave_sync();
     }
     // min live key + live count (wave-uniform)
     __device__ void scan(int ln, uint64_t& best, uint32_t& nlive) const {
@@ -221,13 +221,13 @@ struct KeySet {
     __device__ void compact(int ln) {
         uint64_t* kept = tmp + (imask + 1) / 2;  // after the slot scratch
         const uint32_t pos = gather_live(ln, kept);
-        __syncthreads();
+        wave_sync();
         reset(ln);
         for (uint32_t e0 = 0; e0 < pos; e0 += 64) {
             const uint32_t e = e0 + ln;
             toggle_pass(e < pos ? kept[e] : 0, e < pos, ln);
         }
-        __syncthreads();
+        wave_sync();
     }
 };
 
@@ -252,9 +252,7 @@ struct Reduce2Bufs {
 
 // H2 phase 1 -> phase 2 hand-off (rips_reduce_small.h)
 struct SmallBufs {
-    const uint16_t* cls;  // [L][E2] class of each edge
-    const uint16_t* srt;  // [L][E2] edges sorted by length
-    int E2;
+    uint32_t* p1_next;    // [L] next H2 column for a phase-1 wave (zeroed per call)
     uint64_t* p1_key;     // [L][rcap2] pivot key after phase 1 (kEmpty64: zero column)
     uint32_t* p1_info;    // [L][rcap2] additions | kP1Overflow
     uint64_t* roff2;      // [L][rcap2] phase-1 working column, then R_j, in rpool2
@@ -262,10 +260,10 @@ struct SmallBufs {
     uint64_t* rpool2;     // [L][rpool2_cap]
     uint64_t rpool2_cap;
     unsigned long long* p1_used;  // [L] rpool2 entries taken by phase 1 (zeroed per call)
-    uint32_t p1_wcap;     // phase-1 LDS toggle-set capacity
-    int p1_piv_lds;       // H2 pivot bitmap staged in LDS by phase-1 waves
+    uint32_t p1_wcap;     // phase-1 LDS toggle-set capacity per wave
 };
 constexpr uint32_t kP1Overflow = 1u << 31;  // phase-1 column outgrew its LDS table
+constexpr uint32_t kP1Cleared = 1u << 30;   // phase 2: the column is an H1 death (prefetched flag)
 
 struct Reduce2Cfg {  // per-dim LDS carve, decided on the host
     uint32_t wcap, rmap_lds_cap;  // rmap_lds_cap = 0 -> global map
@@ -330,7 +328,8 @@ __device__ __forceinline__ uint32_t row_payload(const int (&t)[NVTX]) {
 template <int DIM, bool LDSW, bool PACKED, bool PREV_PACKED, bool PH2 = false>
 __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bufs& rb, const Reduce2Cfg& cfg, PivMap& map,
                            const PivMap* prev, unsigned char* map_lds, Pair* __restrict__ pairs, uint64_t pcap,
-                           const SmallBufs* sb = nullptr) {
+                           const SmallBufs* sb = nullptr, const uint32_t* clr = nullptr, unsigned char* pre_lds = nullptr,
+                           uint32_t pre_cap = 0) {
     constexpr int NV = DIM + 2;  // vertices of a row simplex
     using Lo = RowLo<NV>;
     const int l = c.l, ln = c.ln, n = c.n;
@@ -410,7 +409,35 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
     }
     Pair* P = pairs + (size_t)l * pcap;
     uint64_t cs = 0, npairs = 0, nadds = 0, nskip = 0;
+    uint64_t ecnt = (uint64_t)st->count[DIM];  // emitted pairs: one wave owns this dim's count
     int err = 0;  // wave-uniform
+    // PH2: per-column inputs prefetched into LDS in parallel (key, phase-1
+    // pivot, phase-1 info | kP1Cleared), so the serial walk issues no
+    // dependent HBM loads on its common path
+    uint64_t* pre_k = (uint64_t*)pre_lds;
+    uint64_t* pre_p = pre_k + pre_cap;
+    uint32_t* pre_i = (uint32_t*)(pre_p + pre_cap);
+    const uint64_t npre = PH2 ? (nres < pre_cap ? nres : pre_cap) : 0;
+    const uint64_t* p1k_g = PH2 ? sb->p1_key + (size_t)l * b.rcap : nullptr;
+    const uint32_t* p1i_g = PH2 ? sb->p1_info + (size_t)l * b.rcap : nullptr;
+    const uint32_t* clr_l = PH2 ? clr + (size_t)l * b.cleared_words : nullptr;
+    auto ph2_load = [&](uint64_t j, uint64_t& key, uint64_t& pk1, uint32_t& info) {
+        key = ld_glb(resid, j);
+        const uint64_t si = key_idx(key);
+        pk1 = ld_glb(p1k_g, j);
+        info = ld_glb(p1i_g, j) | (((ld_glb(clr_l, si >> 5) >> (si & 31)) & 1u) ? kP1Cleared : 0u);
+    };
+    if (PH2) {
+        for (uint64_t j = ln; j < npre; j += 64) {
+            uint64_t key, pk1;
+            uint32_t info;
+            ph2_load(j, key, pk1, info);
+            pre_k[j] = key;
+            pre_p[j] = pk1;
+            pre_i[j] = info;
+        }
+        __syncthreads();
+    }
 #ifdef TDA_PROFILE
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // scan, lookup, facet, cob-app, cob-res, reset, compact, total
     const uint64_t t_all = clock64();
@@ -466,23 +493,17 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
 
     auto emit_essential = [&](uint64_t j, float sdm, uint64_t sidx) {
         if (ln == 0) {
-            uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-            if (pos < pcap)
-                P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
-            else
-                atomicOr(&st->err, ERR_PAIR_CAP);
+            if (ecnt < pcap) P[ecnt] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
             rlen[j] = 0;
         }
+        ++ecnt;
     };
     auto emit_pair = [&](uint64_t j, float sdm, uint64_t sidx, float pd, uint64_t pidx, uint32_t plo) {
+        if (pd > sdm) {
+            if (ln == 0 && ecnt < pcap) P[ecnt] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
+            ++ecnt;
+        }
         if (ln == 0) {
-            if (pd > sdm) {
-                uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-                if (pos < pcap)
-                    P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
-                else
-                    atomicOr(&st->err, ERR_PAIR_CAP);
-            }
             map.insert(plo, (uint32_t)j);
             atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
             if (piv != pivg) atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
@@ -492,26 +513,41 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
     };
 
     for (uint64_t j = 0; j < nres && !err; ++j) {
-        const uint64_t key = ld_glb(resid, j);
+        uint64_t key, pk1 = 0;
+        uint32_t info = 0;
+        if (PH2) {
+            if (j < npre) {
+                key = ld_lds(pre_k, j);
+                pk1 = ld_lds(pre_p, j);
+                info = ld_lds(pre_i, j);
+            } else {
+                ph2_load(j, key, pk1, info);
+            }
+        } else {
+            key = ld_glb(resid, j);
+        }
         const uint64_t sidx = key_idx(key);
         const float sdm = key_diam(key);
         int vs[DIM + 1];
-        decode_wave<DIM>(sidx, n, vs, ln);
-        // clearing: skip columns that are H_{DIM-1} deaths
+        // clearing: skip columns that are H_{DIM-1} deaths (PH2: a set bit in
+        // the H_{DIM-1} pivot bitmap -- apparent pivots were never columns)
         bool cleared;
-        if (DIM == 1) {
-            cleared = (ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u;
+        if (PH2) {
+            cleared = (info & kP1Cleared) != 0;
+            info &= ~kP1Cleared;
         } else {
-            cleared = prev->find(row_payload<DIM + 1, PREV_PACKED>(vs), ln) >= 0;
+            decode_wave<DIM>(sidx, n, vs, ln);
+            if (DIM == 1)
+                cleared = (ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u;
+            else
+                cleared = prev->find(row_payload<DIM + 1, PREV_PACKED>(vs), ln) >= 0;
         }
         if (cleared) {
             ++nskip;
             if (ln == 0) rlen[j] = 0;
             continue;
         }
-        if (PH2 && !(ld_glb(sb->p1_info + (size_t)l * b.rcap, j) & kP1Overflow)) {
-            const uint32_t info = ld_glb(sb->p1_info + (size_t)l * b.rcap, j);
-            const uint64_t pk1 = ld_glb(sb->p1_key + (size_t)l * b.rcap, j);
+        if (PH2 && !(info & kP1Overflow)) {
             nadds += info;
             if (pk1 == kEmpty64) {
                 emit_essential(j, sdm, sidx);
@@ -542,6 +578,7 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
                 W.toggle_pass(e < ol ? ld_glb((const uint64_t*)rpool, o0 + e) : 0, e < ol, ln);
             }
         } else {
+            if (PH2) decode_wave<DIM>(sidx, n, vs, ln);
             if (!room((uint32_t)n)) break;
             cob(vs, sdm);
         }
@@ -671,6 +708,8 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
         if (err == 1) atomicOr(&st->err, LDSW ? (int32_t)ERR_LDS_SPILL : (int32_t)ERR_WORK_CAP);
         if (err == 2) atomicOr(&st->err, ERR_VPOOL_CAP);
         if (err == 3) atomicOr(&st->err, ERR_STEP_LIMIT);
+        if (ecnt > pcap) atomicOr(&st->err, ERR_PAIR_CAP);
+        st->count[DIM] = (int64_t)ecnt;
         atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)cs);
         atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)npairs);
         atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)nadds);
@@ -725,11 +764,12 @@ __global__ __launch_bounds__(64) void k_reduce_all(const float* __restrict__ dis
 }
 
 // Phase 2 of the split H2 reduction (N <= 64): one wave per layer walks the
-// H2 columns in order on top of k_reduce_small's phase-1 results.  LDS:
-// [16 B][distance matrix][H1 residual-pivot map][H2 map + W + pivot bitmap],
-// the k_reduce_all carve.
+// H2 columns in order on top of k_reduce_small's phase-1 results.  Clearing
+// reads the H1 pivot bitmap (k_apparent<1> + the H1 chain).  LDS: [16 B]
+// [distance matrix][per-column prefetch][H2 map + W + pivot bitmap], the
+// k_reduce_all carve with the H1-map area holding the prefetch.
 __global__ __launch_bounds__(64) void k_reduce_h2_finish(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
-                                                         DimBufs b2, Reduce2Bufs rb, ReduceAllCfg cfg, SmallBufs sb,
+                                                         DimBufs b1, DimBufs b2, Reduce2Bufs rb, ReduceAllCfg cfg, SmallBufs sb,
                                                          Pair* __restrict__ pairs2, uint64_t pcap2) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, ln = threadIdx.x;
@@ -746,27 +786,15 @@ __global__ __launch_bounds__(64) void k_reduce_h2_finish(const float* __restrict
     stage_to_lds(dl, dist + (size_t)l * n * n, 4ull * n * n, ln, 64);
     p += (4ull * n * n + 15) & ~15ull;
     c.D = dl;
-    // H1 residual pivot map: HBM mirror written by the H1 chain, staged to LDS
-    PivMap m1;
-    m1.k = rb.rmap_keys + ((size_t)l * 2) * rb.rmap_stride;
-    m1.v = rb.rmap_vals + ((size_t)l * 2) * rb.rmap_stride;
-    m1.mask = st->rmask[1];
-    const uint64_t cap1 = m1.mask + 1;
-    if (cap1 <= cfg.dim[1].rmap_lds_cap) {
-        uint64_t* k1 = (uint64_t*)p;
-        uint32_t* v1 = (uint32_t*)(p + 8ull * cap1);
-        for (uint64_t e = ln; e < cap1; e += 64) {
-            k1[e] = m1.k[e];
-            v1[e] = m1.v[e];
-        }
-        m1.k = k1;
-        m1.v = v1;
-    }
+    unsigned char* pre = p;
+    const uint32_t pre_cap = (uint32_t)(12ull * cfg.dim[1].rmap_lds_cap / 20);
     p += 12ull * cfg.dim[1].rmap_lds_cap;
     __syncthreads();
     PivMap m2;
+    DimBufs b = b2;
+    b.cleared_words = b1.piv_words;  // stride of the clearing bitmap below
     c.lds = p + 12ull * cfg.dim[2].rmap_lds_cap;
-    reduce_dim<2, true, true, true, true>(c, b2, rb, cfg.dim[2], m2, &m1, p, pairs2, pcap2, &sb);
+    reduce_dim<2, true, true, true, true>(c, b, rb, cfg.dim[2], m2, nullptr, p, pairs2, pcap2, &sb, b1.pivbits, pre, pre_cap);
 }
 
 }  // namespace tda

@@ -4,33 +4,50 @@
 //   * H1: a layer has <= 8 residual columns, but ONE of them can need ~170
 //     apparent additions in a row (layer 25: 168 of the layer's 173).  That
 //     chain is the critical path of the whole batch, so its per-addition cost
-//     is what matters.  The working column W becomes a dense LDS bitmap over
-//     all C(N,3) triangles (17,296 bits at N=48): a toggle is one ds_xor, no
-//     hashing, no log, no capacity.  The pivot (min diam, then max index) is
-//     found through per-diameter-class live counts: class = rank of the first
-//     edge of that length in the sorted edge list (k_edge_class), so the
-//     lowest non-empty class is one ballot over a 63-word summary, and its
-//     live triangles {a, b, v} (max edge (a, b)) are one lane per v.
+//     is what matters.  The working column W is a dense LDS bitmap over the
+//     triangles in FILTRATION order (k_h1_prep ranks them), so the pivot is
+//     simply the first set bit: every lane tests its 32*K-bit slice, one
+//     ballot picks the first non-empty slice.  A toggle is one fire-and-forget
+//     ds_xor at the triangle's rank, a stored reduced column R_j is a copy of
+//     the bitmap, and re-adding it is one XOR pass.
 //   * H2: up to ~76 residual columns per layer with <= 13 additions each, and
 //     over all 32 layers exactly one addition uses another RESIDUAL column;
 //     every other addition is an apparent column, which does not depend on
 //     any other column.  So H2 runs as phase 1 (apparent-only reduction,
-//     column-parallel: K waves per layer, concurrently with the H1 chain) and
-//     phase 2 (k_reduce_h2_finish: columns in order, O(1) each unless the
-//     phase-1 pivot is owned by an earlier residual column, in which case the
-//     stored working column is reloaded and reduced further, exactly like
-//     Ripser would have continued).
+//     column-parallel: kP1Blocks x kSmallW waves per layer pull columns from a
+//     per-layer counter, concurrently with the H1 chain) and phase 2
+//     (k_reduce_h2_finish: columns in order, O(1) each unless the phase-1
+//     pivot is owned by an earlier residual column, in which case the stored
+//     working column is reloaded and reduced further, exactly like Ripser
+//     would have continued).
 // Phase 1 of a column performs exactly the first steps Ripser's serial loop
 // performs on it (the serial loop consults residual owners first, and a
 // pivot owned by an apparent column is never a residual pivot), so the
 // result is bit-identical to the serial order.
+//
+// Triangle ranks (k_h1_prep).  Every triangle t <= thresh is assigned to its
+// youngest facet e(t) (longest edge, ties -> smallest edge index); that is the
+// facet an apparent pair would pair it with.  Edges are sorted by length and
+// edge e owns the rank block [off_e, off_e + |M_e|), M_e = bitmask of third
+// vertices w of its triangles {a, b, w}, ordered by w DESCENDING -- the colex
+// index of {a, b, w} grows with w, so inside a block rank order is Ripser's
+// (diam asc, index desc).  Edges of equal length form a class whose blocks are
+// contiguous; only inside such a tie class does rank order differ from
+// filtration order, and the pivot search resolves it by index (rare path).
+// Without a tie, t is an apparent pivot iff it is the FIRST triangle of its
+// block (the oldest cofacet of e(t) whose youngest facet is e(t)).
 #pragma once
 #include "rips_reduce.h"
 
 namespace tda {
 
 constexpr int kDenseMaxN = 64;
-constexpr int kP1Waves = 8;                 // H2 phase-1 waves per layer
+constexpr int kSmallT = 256;              // threads per k_reduce_small block
+constexpr int kSmallW = kSmallT / 64;     // waves per block
+constexpr int kP1Blocks = 4;              // H2 phase-1 blocks per layer
+constexpr uint32_t kP1WCap = 512;         // phase-1 toggle-set capacity per wave
+constexpr int kChainMaxCols = 512;        // non-cleared H1 residual columns / stored R_j per layer
+constexpr int kMaxK = 21;                 // bitmap words per lane: ceil(C(64,3) / 32 / 64)
 
 __device__ __forceinline__ uint32_t c2u(uint32_t x) { return x * (x - 1) / 2; }
 __device__ __forceinline__ uint32_t c3u(uint32_t x) { return x * (x - 1) * (x - 2) / 6; }
@@ -48,421 +65,469 @@ __device__ __forceinline__ void edge_verts(uint32_t q, int& a, int& b) {
     b = (int)(q - c2u(x));
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return (uint32_t)wave_max_u64((uint64_t)v); }
+// set bits of M above bit v
+__device__ __forceinline__ uint32_t bits_above(uint64_t M, int v) { return v >= 63 ? 0u : (uint32_t)__popcll(M >> (v + 1)); }
+// bit position of the k-th highest set bit of M (k = 0: the highest), one lane
+__device__ __forceinline__ int kth_highest(uint64_t M, uint32_t k) {
+    for (uint32_t i = 0; i < k; ++i) M &= ~(1ull << (63 - __clzll(M)));
+    return 63 - __clzll(M);
+}
+__device__ __forceinline__ void lds_xor(uint32_t* p, uint32_t v) {
+    __hip_atomic_fetch_xor((TDA_LDS uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
-// ---------------------------------------------------------------- edge classes
-// Per layer: edges sorted by (length, a, b); cls[e] = position of the first
-// edge with e's length (tied lengths share a class), srt[q] = a << 8 | b of
-// the q-th edge.  One 256-thread block per layer, bitonic sort in LDS.
-__global__ __launch_bounds__(256) void k_edge_class(const float* __restrict__ dist, int n, uint16_t* __restrict__ cls,
-                                                   uint16_t* __restrict__ srt, int E2) {
+// per edge (colex index), 16 B: one ds_read_b128
+struct EdgeRec {
+    uint64_t M;        // third vertices w of the triangles {a, b, w} <= thresh whose youngest facet is this edge
+    uint16_t off;      // first rank of the block
+    uint16_t cs, ce;   // rank range [cs, ce) of the edge's length class
+    uint8_t a, b;      // vertices, a > b
+};
+static_assert(sizeof(EdgeRec) == 16, "EdgeRec is one 16-B load");
+struct EdgeRecV {
+    uint64_t M;
+    uint32_t off, cs, ce;
+    int a, b;
+};
+__device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 q = ((const TDA_LDS u32x4*)R)[e];
+    EdgeRecV v;
+    v.M = (uint64_t)q.x | ((uint64_t)q.y << 32);
+    v.off = q.z & 0xFFFFu;
+    v.cs = q.z >> 16;
+    v.ce = q.w & 0xFFFFu;
+    v.a = (int)((q.w >> 16) & 0xFFu);
+    v.b = (int)(q.w >> 24);
+    return v;
+}
+
+struct DenseBufs {
+    EdgeRec* recs;      // [L][E]
+    uint16_t* inv;      // [L][inv_stride] rank -> edge
+    uint32_t E, inv_stride;
+    int K;              // bitmap words per lane (W = 64 K words)
+};
+
+// ---------------------------------------------------------------- ranks
+// One 1024-thread block per layer: sort edges <= thresh by length, build each
+// edge's block mask, the exclusive scan of block sizes (= ranks), the class
+// ranges and rank -> edge.  LDS: [16][D][keys E2][counts E2][masks E2].
+__global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
+                                                  float user_thresh, DenseBufs db, int E2, LayerStats* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t* s = (uint64_t*)smem;
-    const int l = blockIdx.x, t = threadIdx.x;
-    const float* D = dist + (size_t)l * n * n;
+    const int l = blockIdx.x, t = threadIdx.x, T = blockDim.x, ln = t & 63, wv = t >> 6, nw = T >> 6;
+    const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
+    float* D = (float*)(smem + 16);
+    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, T);
+    uint64_t* sk = (uint64_t*)(smem + 16 + ((4ull * n * n + 15) & ~15ull));
+    uint32_t* off = (uint32_t*)(sk + E2);
+    uint64_t* Ms = (uint64_t*)(off + E2);
+    uint32_t& s_ne = *(uint32_t*)(smem + 4);
+    uint32_t& s_tot = *(uint32_t*)(smem + 8);
     const int E = n * (n - 1) / 2;
-    for (int q = t; q < E2; q += 256) {
+    if (t == 0) s_ne = 0;
+    __syncthreads();
+    for (int q = t; q < E2; q += T) {
         uint64_t k = kEmpty64;
         if (q < E) {
             int a, b;
             edge_verts((uint32_t)q, a, b);
-            k = ((uint64_t)__float_as_uint(D[(size_t)a * n + b] + 0.0f) << 32) | ((uint32_t)a << 8) | (uint32_t)b;
+            const float d = D[a * n + b];
+            if (d <= r) k = ((uint64_t)__float_as_uint(d + 0.0f) << 32) | (uint32_t)q;
         }
-        s[q] = k;
+        sk[q] = k;
     }
     __syncthreads();
     for (int k = 2; k <= E2; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < E2; i += 256) {
+            for (int i = t; i < E2; i += T) {
                 const int ixj = i ^ j;
                 if (ixj > i) {
-                    const uint64_t x = s[i], y = s[ixj];
+                    const uint64_t x = sk[i], y = sk[ixj];
                     if ((x > y) == ((i & k) == 0)) {
-                        s[i] = y;
-                        s[ixj] = x;
+                        sk[i] = y;
+                        sk[ixj] = x;
                     }
                 }
             }
             __syncthreads();
         }
-    uint16_t* C = cls + (size_t)l * E2;
-    uint16_t* S = srt + (size_t)l * E2;
-    for (int q = t; q < E; q += 256) {
-        const uint64_t k = s[q];
-        const uint32_t len = (uint32_t)(k >> 32);
-        int lo = 0, hi = q;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if ((uint32_t)(s[mid] >> 32) < len)
-                lo = mid + 1;
-            else
-                hi = mid;
+    for (int q = t; q < E2; q += T)
+        if (sk[q] != kEmpty64 && (q + 1 == E2 || sk[q + 1] == kEmpty64)) s_ne = (uint32_t)(q + 1);
+    __syncthreads();
+    const int nE = (int)s_ne;
+    // block masks: one wave per edge, lane = third vertex
+    for (int q = wv; q < nE; q += nw) {
+        const uint64_t k = sk[q];
+        const uint32_t e = (uint32_t)k;
+        int a, b;
+        edge_verts(e, a, b);
+        const float le = __uint_as_float((uint32_t)(k >> 32));
+        const int v = ln;
+        bool ok = v < n && v != a && v != b;
+        if (ok) {
+            const float dav = D[a * n + v], dbv = D[b * n + v];
+            ok = dav <= le && dbv <= le;
+            if (ok && dav == le && edge_id(a, v) < e) ok = false;  // (a, v) is the younger facet
+            if (ok && dbv == le && edge_id(b, v) < e) ok = false;
         }
-        const int a = (int)((k >> 8) & 0xFF), b = (int)(k & 0xFF);
-        C[c2u(a) + b] = (uint16_t)lo;
-        S[q] = (uint16_t)((a << 8) | b);
+        const uint64_t m = __ballot(ok);
+        if (ln == 0) {
+            Ms[q] = m;
+            off[q] = (uint32_t)__popcll(m);
+        }
     }
+    __syncthreads();
+    if (wv == 0) {  // exclusive scan of the block sizes
+        uint32_t carry = 0;
+        for (int q0 = 0; q0 < nE; q0 += 64) {
+            const int q = q0 + ln;
+            const uint32_t c = q < nE ? off[q] : 0u;
+            uint32_t x = c;
+            for (int s = 1; s < 64; s <<= 1) {
+                const uint32_t y = __shfl_up(x, s, 64);
+                if (ln >= s) x += y;
+            }
+            if (q < nE) off[q] = carry + x - c;
+            carry += __shfl(x, 63, 64);
+        }
+        if (ln == 0) s_tot = carry;
+    }
+    __syncthreads();
+    EdgeRec* R = db.recs + (size_t)l * db.E;
+    for (int q = t; q < nE; q += T) {
+        const uint32_t lb = (uint32_t)(sk[q] >> 32);
+        int q0 = q, q1 = q;
+        while (q0 > 0 && (uint32_t)(sk[q0 - 1] >> 32) == lb) --q0;
+        while (q1 + 1 < nE && (uint32_t)(sk[q1 + 1] >> 32) == lb) ++q1;
+        const uint32_t e = (uint32_t)sk[q];
+        int a, b;
+        edge_verts(e, a, b);
+        EdgeRec rec;
+        rec.M = Ms[q];
+        rec.off = (uint16_t)off[q];
+        rec.cs = (uint16_t)off[q0];
+        rec.ce = (uint16_t)(off[q1] + (uint32_t)__popcll(Ms[q1]));
+        rec.a = (uint8_t)a;
+        rec.b = (uint8_t)b;
+        R[e] = rec;
+    }
+    for (int e = t; e < E; e += T) {  // edges above the threshold own no triangles
+        int a, b;
+        edge_verts((uint32_t)e, a, b);
+        if (!(D[a * n + b] <= r)) {
+            EdgeRec rec = {};
+            rec.a = (uint8_t)a;
+            rec.b = (uint8_t)b;
+            R[e] = rec;
+        }
+    }
+    uint16_t* inv = db.inv + (size_t)l * db.inv_stride;
+    for (int q = wv; q < nE; q += nw) {
+        const uint32_t c = (uint32_t)__popcll(Ms[q]);
+        if ((uint32_t)ln < c) inv[off[q] + ln] = (uint16_t)(uint32_t)sk[q];
+    }
+    if (t == 0) stats[l].ntri = s_tot;
 }
 
-// ---------------------------------------------------------------- dense H1
-struct DenseW {
-    const float* D;      // LDS distance matrix
-    uint32_t* W;         // LDS bitmap over triangles
-    uint32_t* cnt;       // LDS live triangles per class [E]
-    uint32_t* sum;       // LDS "class may be non-empty" bits [64]
-    const uint16_t* cls; // LDS class of edge [E]
-    const uint16_t* srt; // LDS sorted edges [E]
-    int n, E, wwords, swords;
-    float r;
-
-    // toggle the coboundary of edge (x, y) (length fd, class cf): lane v -> {x, y, v}
-    __device__ __forceinline__ void cob(int x, int y, float fd, uint32_t cf, int ln) const {
-        const int v = ln;
-        bool ok = v < n && v != x && v != y;
-        float dx = 0.0f, dy = 0.0f;
-        if (ok) {
-            dx = ld_lds(D, (size_t)x * n + v);
-            dy = ld_lds(D, (size_t)y * n + v);
-        }
-        const float cd = fmaxf(fd, fmaxf(dx, dy));
-        ok = ok && cd <= r;
-        const bool same = cd == fd;  // max edge has length fd: class cf
-        uint32_t c = cf;
-        if (ok && !same) c = ld_lds(cls, dx >= dy ? edge_id(x, v) : edge_id(y, v));
-        bool was = false;
-        if (ok) {
-            const uint32_t idx = tri_id(x, y, v);
-            const uint32_t bit = 1u << (idx & 31);
-            was = (atomicXor(&W[idx >> 5], bit) & bit) != 0;
-        }
-        // class cf: one aggregated update (many lanes share it)
-        const uint64_t mp = __ballot(ok && same && !was), mm = __ballot(ok && same && was);
-        if (ln == 0 && (mp | mm)) {
-            atomicAdd(&cnt[cf], (uint32_t)(__popcll(mp) - __popcll(mm)));
-            if (mp) atomicOr(&sum[cf >> 5], 1u << (cf & 31));
-        }
-        if (ok && !same) toggle_count(c, was);
-    }
-    __device__ __forceinline__ void toggle_count(uint32_t c, bool was) const {
-        if (was) {
-            atomicSub(&cnt[c], 1u);
-        } else {
-            atomicAdd(&cnt[c], 1u);
-            atomicOr(&sum[c >> 5], 1u << (c & 31));
-        }
-    }
-    // toggle stored keys (class << 32 | triangle index), distinct
-    __device__ __forceinline__ void toggle_keys(uint64_t k, bool ok) const {
-        if (!ok) return;
-        const uint32_t idx = (uint32_t)k, c = (uint32_t)(k >> 32);
-        const uint32_t bit = 1u << (idx & 31);
-        const bool was = (atomicXor(&W[idx >> 5], bit) & bit) != 0;
-        toggle_count(c, was);
-    }
-    // pivot = live triangle of min (diam, -idx).  Returns false if W is empty.
-    // Out: idx, vertices (a, b) = a max edge (a > b), v, the class and the
-    // lengths |av|, |bv|.
-    __device__ bool pivot(int ln, uint32_t& pidx, int& pa, int& pb, int& pv, uint32_t& pc, float& len, float& dav,
-                          float& dbv) const {
-        for (;;) {
-            const uint32_t sw = ln < swords ? ld_lds(sum, ln) : 0u;
-            const uint64_t nz = __ballot(sw != 0);
-            if (!nz) return false;
-            const int f = __builtin_ctzll(nz);
-            const uint32_t w = __builtin_amdgcn_readlane(sw, f);
-            const uint32_t c = (uint32_t)f * 32 + __builtin_ctz(w);
-            if (ld_lds(cnt, c) == 0) {  // lazily cleared summary bit
-                if (ln == 0) sum[c >> 5] = w & ~(1u << (c & 31));
-                continue;
-            }
-            uint32_t best = 0;
-            float lc = 0.0f;
-            for (int q = (int)c; q < E; ++q) {
-                const uint32_t e = ld_lds(srt, q);
-                const int a = (int)(e >> 8), b = (int)(e & 0xFF);
-                const float le = ld_lds(D, (size_t)a * n + b);
-                if (q == (int)c)
-                    lc = le;
-                else if (le != lc)
-                    break;
-                const int v = ln;
-                bool ok = v < n && v != a && v != b;
-                float x = 0.0f, y = 0.0f;
-                if (ok) {
-                    x = ld_lds(D, (size_t)a * n + v);
-                    y = ld_lds(D, (size_t)b * n + v);
-                    ok = x <= lc && y <= lc;
-                }
-                const uint32_t idx = tri_id(a, b, v);
-                ok = ok && ((ld_lds(W, idx >> 5) >> (idx & 31)) & 1u);
-                const uint32_t cand = ok ? idx + 1 : 0u;
-                const uint32_t m = wave_max_u32(cand);
-                if (m > best) {
-                    best = m;
-                    const int lane = __builtin_ctzll(__ballot(cand == m));
-                    pa = a;
-                    pb = b;
-                    pv = lane;
-                    dav = __shfl(x, lane, 64);
-                    dbv = __shfl(y, lane, 64);
-                }
-            }
-            if (best == 0) {  // counts and bitmap disagree: cannot happen
-                if (ln == 0) sum[c >> 5] = w & ~(1u << (c & 31));
-                continue;
-            }
-            pidx = best - 1;
-            pc = c;
-            len = lc;
-            return true;
-        }
-    }
-    // append (class << 32 | idx) of every live triangle to out; returns count
-    __device__ uint32_t gather(int ln, uint64_t* out) const {
-        uint32_t pos = 0;
-        for (int w0 = 0; w0 < wwords; w0 += 64) {
-            const int wi = w0 + ln;
-            uint32_t bits = wi < wwords ? ld_lds(W, wi) : 0u;
-            while (__ballot(bits != 0)) {
-                const bool has = bits != 0;
-                uint64_t key = 0;
-                if (has) {
-                    const uint32_t idx = (uint32_t)wi * 32 + __builtin_ctz(bits);
-                    bits &= bits - 1;
-                    int t[3];
-                    decode<2>(idx, n, t);
-                    const float d01 = ld_lds(D, (size_t)t[0] * n + t[1]), d02 = ld_lds(D, (size_t)t[0] * n + t[2]),
-                                d12 = ld_lds(D, (size_t)t[1] * n + t[2]);
-                    const uint32_t e = (d01 >= d02 && d01 >= d12) ? edge_id(t[0], t[1]) : (d02 >= d12 ? edge_id(t[0], t[2]) : edge_id(t[1], t[2]));
-                    key = ((uint64_t)ld_lds(cls, e) << 32) | idx;
-                }
-                const uint64_t m = __ballot(has);
-                if (has) out[pos + lanes_below(m)] = key;
-                pos += (uint32_t)__popcll(m);
-            }
-        }
-        return pos;
-    }
-    __device__ void reset(int ln) const {
-        for (int i = ln; i < wwords; i += 64) W[i] = 0;
-        for (int i = ln; i < E; i += 64) cnt[i] = 0;
-        for (int i = ln; i < swords; i += 64) sum[i] = 0;
-    }
-};
-
-
-// H1 of one layer with the dense working column (one wave).
-__device__ void reduce_h1_dense(const float* Dl, int n, float r, LayerStats* st, int l, const DimBufs& b, const Reduce2Bufs& rb,
-                                const SmallBufs& sb, unsigned char* lds, uint64_t step_limit, Pair* __restrict__ pairs,
-                                uint64_t pcap) {
-    const int ln = threadIdx.x;
+// ---------------------------------------------------------------- H1 chain
+// H1 of one layer.  All kSmallT threads stage the layer's tables and filter
+// the residual columns; then wave 0 alone runs the serial reduction (waves
+// 1..3 leave; no s_barrier is issued after that point).
+__device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const DimBufs& b, const Reduce2Bufs& rb,
+                         const DenseBufs& db, unsigned char* lds, uint64_t step_limit, Pair* __restrict__ pairs, uint64_t pcap) {
+    const int t = threadIdx.x, ln = t & 63, wv = t >> 6;
     const int E = n * (n - 1) / 2;
-    uint64_t nres = (uint64_t)st->n_residual[1];
-    if (nres > b.rcap) nres = b.rcap;
-    const uint64_t* resid = b.resid + (size_t)l * b.rcap;
-    uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
-
+    const int K = db.K;
+    const uint32_t WP = 64u * (uint32_t)K;
     unsigned char* p = lds;
     auto take = [&](size_t bytes) {
         unsigned char* q = p;
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
-    DenseW S;
-    S.D = Dl;
-    S.n = n;
-    S.E = E;
-    S.r = r;
-    S.wwords = (int)((binom((uint64_t)n, 3) + 31) / 32);
-    S.swords = (E + 31) / 32;
-    S.W = (uint32_t*)take(4ull * S.wwords);
-    S.cnt = (uint32_t*)take(4ull * E);
-    S.sum = (uint32_t*)take(4ull * 64);
-    uint16_t* cl = (uint16_t*)take(2ull * E);
-    uint16_t* sr = (uint16_t*)take(2ull * E);
-    uint32_t* piv = (uint32_t*)take(4ull * b.piv_words);
-    // residual pivot map: LDS copy for probes, mirrored to HBM for H2 clearing
-    uint64_t rcap2 = 16;
-    while (rcap2 < 2 * nres + 16) rcap2 <<= 1;
-    if (rcap2 > rb.rmap_stride) rcap2 = rb.rmap_stride;
-    PivMap mg;
-    mg.k = rb.rmap_keys + ((size_t)l * 2) * rb.rmap_stride;  // cleared by k_sort_resid
-    mg.v = rb.rmap_vals + ((size_t)l * 2) * rb.rmap_stride;
-    mg.mask = rcap2 - 1;
-    PivMap ml = mg;
-    const bool map_lds = rcap2 <= 1024;
-    if (map_lds) {
-        ml.k = (uint64_t*)take(8ull * rcap2);
-        ml.v = (uint32_t*)take(4ull * rcap2);
-        for (uint64_t e = ln; e < rcap2; e += 64) ml.k[e] = kEmpty64;
+    EdgeRec* R = (EdgeRec*)take(16ull * E);
+    uint16_t* inv = (uint16_t*)take(2ull * db.inv_stride);
+    uint32_t* W = (uint32_t*)take(4ull * WP);
+    uint32_t* res = (uint32_t*)take(4ull * WP);  // ranks that are residual pivots
+    uint32_t* piv = (uint32_t*)take(4ull * b.piv_words);  // colex bitmap of apparent pivots (tie classes)
+    uint64_t* cols = (uint64_t*)take(8ull * kChainMaxCols);
+    uint16_t* own = (uint16_t*)take(2ull * kChainMaxCols);
+    uint32_t* hdr = (uint32_t*)(lds - 16 - ((4ull * n * n + 15) & ~15ull));  // smem[0..16)
+
+    const uint32_t ntri = (uint32_t)st->ntri;
+    stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kSmallT);
+    stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kSmallT);
+    uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
+    stage_to_lds(piv, pivg, 4ull * b.piv_words, t, kSmallT);
+    for (uint32_t i = t; i < WP; i += kSmallT) {
+        W[i] = 0;
+        res[i] = 0;
     }
-    for (int i = ln; i < E; i += 64) {
-        cl[i] = sb.cls[(size_t)l * sb.E2 + i];
-        sr[i] = sb.srt[(size_t)l * sb.E2 + i];
+    uint64_t nres = (uint64_t)st->n_residual[1];
+    if (nres > b.rcap) nres = b.rcap;
+    if (wv == 0) {  // drop H0 deaths (spanning-forest edges: cleared columns), keep column order
+        const uint64_t* resid = b.resid + (size_t)l * b.rcap;
+        const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
+        uint32_t nc = 0, nskip = 0;
+        for (uint64_t j0 = 0; j0 < nres; j0 += 64) {
+            const uint64_t j = j0 + ln;
+            uint64_t key = 0;
+            bool keep = false;
+            if (j < nres) {
+                key = ld_glb(resid, j);
+                const uint32_t s = (uint32_t)key_idx(key);
+                keep = !((ld_glb(mst, s >> 5) >> (s & 31)) & 1u);
+            }
+            const uint64_t m = __ballot(keep);
+            const uint32_t pos = nc + lanes_below(m);
+            if (keep && pos < (uint32_t)kChainMaxCols) cols[pos] = key;
+            nc += (uint32_t)__popcll(m);
+            nskip += (uint32_t)__popcll(__ballot(j < nres)) - (uint32_t)__popcll(m);
+        }
+        if (ln == 0) {
+            hdr[0] = nc;
+            hdr[1] = nskip;
+        }
     }
-    stage_to_lds(piv, pivg, 4ull * b.piv_words, ln, 64);
-    S.cls = cl;
-    S.srt = sr;
-    S.reset(ln);
     __syncthreads();
+    if (wv != 0) return;
 
-    const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
-    uint64_t* roff = rb.roff + (size_t)l * b.rcap;
-    uint32_t* rlen = rb.rlen + (size_t)l * b.rcap;
-    uint64_t* rpool = rb.rpool + (size_t)l * rb.rpool_cap;
-    uint64_t rused = 0;
+    const float r = st->thresh;
+    const uint32_t nc = hdr[0], nskip = hdr[1];
     Pair* P = pairs + (size_t)l * pcap;
-    uint64_t cs = 0, npairs = 0, nadds = 0, nskip = 0;
-    int err = 0;
+    uint32_t* pool = (uint32_t*)(rb.rpool + (size_t)l * rb.rpool_cap);
+    const uint64_t pool_words = 2ull * rb.rpool_cap;
+    uint64_t ecnt = 0, cs = 0, npairs = 0, nadds = 0;
+    uint32_t nown = 0;
+    int err = nc > (uint32_t)kChainMaxCols ? 1 : 0;
+#ifdef TDA_PROFILE
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // total, pivot, tie pivots, cob-app, add-owner, new pair, -, pivots
+    const uint64_t t_all = clock64();
+    uint64_t ties = 0;
+#endif
 
-    for (uint64_t j = 0; j < nres && !err; ++j) {
-        const uint64_t key = ld_glb(resid, j);
+    // toggle the coboundary of edge (a, b) (length le <= r): lane v -> {a, b, v}
+    auto cob = [&](int a, int b, float le) {
+        const int v = ln;
+        bool ok = v < n && v != a && v != b;
+        float dav = 0.0f, dbv = 0.0f;
+        if (ok) {
+            dav = ld_lds(Dl, (size_t)a * n + v);
+            dbv = ld_lds(Dl, (size_t)b * n + v);
+            ok = fmaxf(dav, dbv) <= r;
+        }
+        if (ok) {
+            // youngest facet of {a, b, v}: longest edge, ties -> smallest index
+            float bl = le;
+            uint32_t be = edge_id(a, b);
+            int third = v;
+            const uint32_t eav = edge_id(a, v), ebv = edge_id(b, v);
+            if (dav > bl || (dav == bl && eav < be)) {
+                bl = dav;
+                be = eav;
+                third = b;
+            }
+            if (dbv > bl || (dbv == bl && ebv < be)) {
+                bl = dbv;
+                be = ebv;
+                third = a;
+            }
+            const EdgeRecV q = load_rec(R, be);
+            const uint32_t rk = q.off + bits_above(q.M, third);
+            lds_xor(&W[rk >> 5], 1u << (rk & 31));
+        }
+    };
+    // first set bit of W (wave-uniform), false if W is empty
+    auto first_bit = [&](uint32_t& rk) -> bool {
+        uint32_t w[kMaxK];
+#pragma unroll
+        for (int k = 0; k < kMaxK; ++k) w[k] = k < K ? ld_lds(W, (size_t)ln * K + k) : 0u;
+        int fk = -1;
+        uint32_t fv = 0;
+#pragma unroll
+        for (int k = kMaxK - 1; k >= 0; --k)
+            if (w[k]) {
+                fk = k;
+                fv = w[k];
+            }
+        const uint64_t m = __ballot(fk >= 0);
+        if (!m) return false;
+        const int f = __builtin_ctzll(m);
+        const int wk = __builtin_amdgcn_readlane(fk, f);
+        const uint32_t val = (uint32_t)__builtin_amdgcn_readlane((int)fv, f);
+        rk = ((uint32_t)f * (uint32_t)K + (uint32_t)wk) * 32u + (uint32_t)__builtin_ctz(val);
+        return true;
+    };
+
+    for (uint32_t j = 0; j < nc && !err; ++j) {
+        const uint64_t key = ld_lds(cols, j);
         const uint32_t sidx = (uint32_t)key_idx(key);
         const float sdm = key_diam(key);
-        if ((ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u) {  // H0 death: cleared
-            ++nskip;
-            if (ln == 0) rlen[j] = 0;
-            continue;
-        }
         int a0, b0;
         edge_verts(sidx, a0, b0);
-        S.cob(a0, b0, sdm, ld_lds(cl, sidx), ln);
-        __syncthreads();
+        cob(a0, b0, sdm);
+        wave_sync();
         for (uint64_t step = 0;; ++step) {
             if (step >= step_limit) {
-                if (ln == 0) printf("reduce_h1_dense: layer %d column %llu step limit\n", l, (unsigned long long)j);
+                if (ln == 0) printf("h1_chain: layer %d column %u step limit\n", l, j);
                 err = 3;
                 break;
             }
-            uint32_t pidx, pc;
-            int pa, pb, pv;
-            float pd, dav, dbv;
-            if (!S.pivot(ln, pidx, pa, pb, pv, pc, pd, dav, dbv)) {
-                if (ln == 0) {  // essential class
-                    const uint64_t pos = atomicAdd((unsigned long long*)&st->count[1], 1ull);
-                    if (pos < pcap)
-                        P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
-                    else
-                        atomicOr(&st->err, ERR_PAIR_CAP);
-                    rlen[j] = 0;
-                }
+            TDA_STAMP(t1);
+            uint32_t rk;
+            const bool found = first_bit(rk);
+#ifdef TDA_PROFILE
+            prof[7] += 1;
+#endif
+            if (!found) {  // zero column: essential class
+                if (ln == 0 && ecnt < pcap) P[ecnt] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
+                ++ecnt;
+                TDA_ACC(1, t1);
                 break;
             }
-            int t[3] = {pa, pb, pv};  // descending for the packed payload
-            if (t[1] < t[2]) { const int x = t[1]; t[1] = t[2]; t[2] = x; }
-            if (t[0] < t[1]) { const int x = t[0]; t[0] = t[1]; t[1] = x; }
-            if (t[1] < t[2]) { const int x = t[1]; t[1] = t[2]; t[2] = x; }
-            const uint32_t plo = RowLo<3>::pack(t);
-            const bool app = (ld_lds(piv, pidx >> 5) >> (pidx & 31)) & 1u;
-            const int64_t owner = app ? ml.find(plo, ln) : -1;
-            if (owner >= 0) {
-                const uint64_t o0 = ld_glb((const uint64_t*)roff, owner);
-                const uint32_t ol = ld_glb((const uint32_t*)rlen, owner);
-                for (uint32_t e0 = 0; e0 < ol; e0 += 64) {
-                    const uint32_t e = e0 + ln;
-                    S.toggle_keys(e < ol ? ld_glb((const uint64_t*)rpool, o0 + e) : 0, e < ol);
-                }
-                ++nadds;
-            } else if (app) {
-                // youngest facet: max length (= pd), ties -> smallest edge index
-                uint32_t fe = edge_id(pa, pb);
-                int fx = pa, fy = pb;
-                if (dav == pd && edge_id(pa, pv) < fe) {
-                    fe = edge_id(pa, pv);
-                    fx = pa;
-                    fy = pv;
-                }
-                if (dbv == pd && edge_id(pb, pv) < fe) {
-                    fe = edge_id(pb, pv);
-                    fx = pb;
-                    fy = pv;
-                }
-                S.cob(fx, fy, pd, pc, ln);
-                ++nadds;
+            uint32_t e = ld_lds(inv, rk);
+            EdgeRecV q = load_rec(R, e);
+            const bool tie = q.ce - q.cs != (uint32_t)__popcll(q.M);
+            int w;
+            if (!tie) {
+                const uint32_t k = rk - q.off;
+                const int v = ln;
+                w = __builtin_ctzll(__ballot(((q.M >> v) & 1ull) && bits_above(q.M, v) == k));
             } else {
-                if (ln == 0) {
-                    if (pd > sdm) {
-                        const uint64_t pos = atomicAdd((unsigned long long*)&st->count[1], 1ull);
-                        if (pos < pcap)
-                            P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
-                        else
-                            atomicOr(&st->err, ERR_PAIR_CAP);
+                // tie class: the pivot is the set triangle of [cs, ce) with the largest index
+#ifdef TDA_PROFILE
+                ++ties;
+#endif
+                uint32_t best = 0, brk = rk;
+                for (uint32_t base = q.cs; base < q.ce; base += 64) {
+                    const uint32_t rho = base + ln;
+                    uint32_t cand = 0;
+                    if (rho < q.ce && ((ld_lds(W, rho >> 5) >> (rho & 31)) & 1u)) {
+                        const EdgeRecV q2 = load_rec(R, ld_lds(inv, rho));
+                        const int w2 = kth_highest(q2.M, rho - q2.off);
+                        cand = tri_id(q2.a, q2.b, w2) + 1;
                     }
-                    if (map_lds) ml.insert(plo, (uint32_t)j);
-                    mg.insert(plo, (uint32_t)j);
-                    atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
-                    atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
+                    const uint32_t m = wave_max_u32(cand);
+                    if (m > best) {
+                        best = m;
+                        brk = base + (uint32_t)__builtin_ctzll(__ballot(cand == m));
+                    }
                 }
-                cs += pair_hash(sidx, pidx);
+                rk = brk;
+                e = ld_lds(inv, rk);
+                q = load_rec(R, e);
+                w = kth_highest(q.M, rk - q.off);
+            }
+            const int a = q.a, b2 = q.b;
+            const float pd = ld_lds(Dl, (size_t)a * n + b2);
+            const uint32_t tidx = tri_id(a, b2, w);
+            const bool isres = (ld_lds(res, rk >> 5) >> (rk & 31)) & 1u;
+            TDA_ACC(1, t1);
+            TDA_STAMP(t2);
+            if (isres) {
+                // add the stored reduced column of the residual column that owns rk
+                uint32_t s = 0;
+                for (uint32_t s0 = 0; s0 < nown; s0 += 64) {
+                    const uint32_t sl = s0 + ln;
+                    const uint64_t m = __ballot(sl < nown && ld_lds(own, sl) == rk);
+                    if (m) {
+                        s = s0 + (uint32_t)__builtin_ctzll(m);
+                        break;
+                    }
+                }
+                const uint32_t* src = pool + (size_t)s * WP;
+                for (int k = 0; k < K; ++k) W[(size_t)ln * K + k] ^= ld_glb(src, (size_t)k * 64 + ln);
+                ++nadds;
+                TDA_ACC(4, t2);
+            } else if (tie ? ((ld_lds(piv, tidx >> 5) >> (tidx & 31)) & 1u) : rk == q.off) {
+                // apparent pair (e, t): add the coboundary of the youngest facet e
+                cob(a, b2, pd);
+                ++nadds;
+                TDA_ACC(3, t2);
+            } else {
+                // new persistence pair (column, t); R_j = W
+                if (pd > sdm) {
+                    if (ln == 0 && ecnt < pcap) P[ecnt] = Pair{sdm, pd, (int64_t)sidx, (int64_t)tidx};
+                    ++ecnt;
+                }
+                cs += pair_hash(sidx, tidx);
                 npairs += 1;
-                // R_j = live triangles (bounded by C(N,3))
-                const uint64_t room = rb.rpool_cap - rused;
-                if (room < binom((uint64_t)n, 3)) {
+                if ((uint64_t)(nown + 1) * WP > pool_words || nown >= (uint32_t)kChainMaxCols) {
                     err = 2;
                     break;
                 }
-                const uint32_t wr = S.gather(ln, rpool + rused);
-                if (ln == 0) {
-                    roff[j] = rused;
-                    rlen[j] = wr;
+                uint32_t* dst = pool + (size_t)nown * WP;
+                for (int k = 0; k < K; ++k) {
+                    dst[(size_t)k * 64 + ln] = W[(size_t)ln * K + k];
+                    W[(size_t)ln * K + k] = 0u;
                 }
-                rused += wr;
+                if (ln == 0) {
+                    own[nown] = (uint16_t)rk;
+                    res[rk >> 5] |= 1u << (rk & 31);
+                    atomicOr(&pivg[tidx >> 5], 1u << (tidx & 31));  // H2 clearing reads this bitmap
+                }
+                ++nown;
+                TDA_ACC(5, t2);
                 break;
             }
-            __syncthreads();
+            wave_sync();
         }
-        __syncthreads();
-        S.reset(ln);
-        __syncthreads();
+        wave_sync();
     }
     if (ln == 0) {
+#ifdef TDA_PROFILE
+        prof[0] = clock64() - t_all;
+        prof[2] = ties;
+        for (int i = 0; i < 8; ++i) st->prof[0][i] = prof[i];
+#endif
+        if (err == 1) atomicOr(&st->err, ERR_LDS_SPILL);
         if (err == 2) atomicOr(&st->err, ERR_VPOOL_CAP);
         if (err == 3) atomicOr(&st->err, ERR_STEP_LIMIT);
+        if (ecnt > pcap) atomicOr(&st->err, ERR_PAIR_CAP);
+        st->count[1] = (int64_t)ecnt;
         atomicAdd((unsigned long long*)&st->checksum[1], (unsigned long long)cs);
         atomicAdd((unsigned long long*)&st->all_pairs[1], (unsigned long long)npairs);
         atomicAdd((unsigned long long*)&st->n_adds[1], (unsigned long long)nadds);
         atomicAdd((unsigned long long*)&st->n_columns[1], (unsigned long long)(0ull - nskip));
-        st->rmask[1] = rcap2 - 1;  // H2 clearing probes the HBM mirror with this mask
         st->nskip[1] = nskip;
     }
 }
 
-// H2 phase 1 of one layer: wave w of kP1Waves takes residual columns w, w+K, ...
-// and reduces each with apparent columns only.
+// ---------------------------------------------------------------- H2 phase 1
+// Every wave of the layer's phase-1 blocks pulls residual H2 columns from a
+// per-layer counter and reduces each with apparent columns only, in its own
+// LDS toggle-set.  Waves run independently (wave_sync only).
 template <bool PACKED>
-__device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l, int w, const DimBufs& b, const SmallBufs& sb,
+__device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l, const DimBufs& b, const SmallBufs& sb,
                           unsigned char* lds, uint64_t step_limit) {
     constexpr int DIM = 2, NV = 4;
     using Lo = RowLo<NV>;
-    const int ln = threadIdx.x;
+    const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint64_t nres = (uint64_t)st->n_residual[2];
     if (nres > b.rcap) nres = b.rcap;
-    if ((uint64_t)w >= nres) return;
     const uint64_t* resid = b.resid + (size_t)l * b.rcap;
     const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
 
-    unsigned char* p = lds;
+    const uint32_t wcap = sb.p1_wcap;
+    const size_t wbytes = 8ull * wcap + 16ull * wcap + ((4ull * (2 * wcap / 8) + 15) & ~15ull) + 16ull * wcap;
+    unsigned char* p = lds + wbytes * wv;
     auto take = [&](size_t bytes) {
         unsigned char* q = p;
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
     KeySet W;
-    const uint32_t wcap = sb.p1_wcap;
     W.log = (uint64_t*)take(8ull * wcap);
     W.index = (uint64_t*)take(16ull * wcap);
     W.fill = (uint32_t*)take(4ull * (2 * wcap / 8));
     W.tmp = (uint64_t*)take(8ull * 2 * wcap);
     W.imask = 2 * wcap - 1;
     W.cnt = 0;
-    const uint32_t* piv = pivg;
-    if (sb.p1_piv_lds) {
-        uint32_t* pl = (uint32_t*)take(4ull * b.piv_words);
-        stage_to_lds(pl, pivg, 4ull * b.piv_words, ln, 64);
-        piv = pl;
-    }
     for (uint32_t e = ln; e <= W.imask; e += 64) W.index[e] = 0;
     for (uint32_t e = ln; e <= (W.imask >> 3); e += 64) W.fill[e] = 0;
-    __syncthreads();
+    wave_sync();
     const uint32_t wlim = (wcap >> 1) + (wcap >> 2);
 
     uint64_t* p1k = sb.p1_key + (size_t)l * b.rcap;
@@ -504,14 +569,21 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
         W.toggle_pass(key, ok, ln);
     };
 
-    for (uint64_t j = (uint64_t)w; j < nres; j += kP1Waves) {
+#ifdef TDA_PROFILE
+    const uint64_t t_p1 = clock64();
+#endif
+    for (;;) {
+        uint32_t jn = 0;
+        if (ln == 0) jn = atomicAdd(&sb.p1_next[l], 1u);
+        const uint64_t j = (uint64_t)__shfl(jn, 0, 64);
+        if (j >= nres) break;
         const uint64_t key = ld_glb(resid, j);
         const uint64_t sidx = key_idx(key);
         const float sdm = key_diam(key);
         int vs[DIM + 1];
         decode_wave<DIM>(sidx, n, vs, ln);
         cob(vs, sdm);
-        __syncthreads();
+        wave_sync();
         uint32_t adds = 0, flags = 0;
         uint64_t out_key = kEmpty64;
         for (uint64_t step = 0;; ++step) {
@@ -534,7 +606,7 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
                 pidx = plo;
                 decode_wave<DIM + 1>(pidx, n, t, ln);
             }
-            const uint32_t pw = sb.p1_piv_lds ? ld_lds(piv, pidx >> 5) : ld_glb(piv, pidx >> 5);
+            const uint32_t pw = ld_glb(pivg, pidx >> 5);
             if (!((pw >> (pidx & 31)) & 1u)) {  // not apparent: phase 1 ends here
                 out_key = pk;
                 const uint32_t nl = nlive;
@@ -590,35 +662,37 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
             }
             cob(fv, fd);
             ++adds;
-            __syncthreads();
+            wave_sync();
         }
         if (ln == 0) {
             p1k[j] = out_key;
             p1i[j] = adds | flags;
         }
-        __syncthreads();
+        wave_sync();
         W.reset(ln);
     }
+#ifdef TDA_PROFILE
+    if (ln == 0) atomicMax((unsigned long long*)&st->prof[1][0], (unsigned long long)(clock64() - t_p1));
+#endif
 }
 
 // One launch, two roles: blockIdx.y == 0 runs the H1 chain of layer
-// blockIdx.x (dense working column), blockIdx.y = 1..kP1Waves run H2 phase 1.
-template <bool P2>
-__global__ __launch_bounds__(64) void k_reduce_small(const float* __restrict__ dist, int n, int maxdim,
-                                                     LayerStats* __restrict__ stats, DimBufs b1, DimBufs b2, Reduce2Bufs rb,
-                                                     SmallBufs sb, uint64_t step_limit, Pair* __restrict__ pairs1, uint64_t pcap1) {
+// blockIdx.x, blockIdx.y = 1..kP1Blocks run H2 phase 1 (kSmallW waves each).
+__global__ __launch_bounds__(kSmallT) void k_reduce_small(const float* __restrict__ dist, int n, int maxdim,
+                                                          LayerStats* __restrict__ stats, DimBufs b1, DimBufs b2, Reduce2Bufs rb,
+                                                          SmallBufs sb, DenseBufs db, uint64_t step_limit, Pair* __restrict__ pairs1,
+                                                          uint64_t pcap1) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, role = blockIdx.y, ln = threadIdx.x;
+    const int l = blockIdx.x, role = blockIdx.y;
     LayerStats* st = stats + l;
-    const float r = st->thresh;
     float* Dl = (float*)(smem + 16);
-    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, ln, 64);
+    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, threadIdx.x, kSmallT);
     unsigned char* p = smem + 16 + ((4ull * n * n + 15) & ~15ull);
     __syncthreads();
     if (role == 0)
-        reduce_h1_dense(Dl, n, r, st, l, b1, rb, sb, p, step_limit, pairs1, pcap1);
+        h1_chain(Dl, n, st, l, b1, rb, db, p, step_limit, pairs1, pcap1);
     else if (maxdim >= 2)
-        h2_phase1<P2>(Dl, n, r, st, l, role - 1, b2, sb, p, step_limit);
+        h2_phase1<true>(Dl, n, st->thresh, st, l, b2, sb, p, step_limit);
 }
 
 }  // namespace tda
