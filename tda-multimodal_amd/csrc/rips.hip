@@ -67,14 +67,15 @@ struct Plan {
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
     bool dense = false;  // N <= 64: dense-bitmap H1 chain + column-parallel H2 phase 1 (rips_reduce_small.h)
     int E2 = 0;          // edge count rounded up to a power of two (k_h1_prep sort)
-    int dK = 0;          // dense H1 bitmap words per lane
+    int dK = 0;          // dense H1 bitmap words per lane (a k_h1_chain instantiation)
     uint32_t inv_stride = 0;  // rank -> edge table stride (C(N,3) rounded up)
-    uint32_t small_lds = 0;   // dynamic LDS of k_reduce_small
+    uint32_t chain_lds = 0;   // dynamic LDS of k_h1_chain
+    uint32_t p1_lds = 0;      // dynamic LDS of k_h2_phase1
     uint32_t prep_lds = 0;    // dynamic LDS of k_h1_prep
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -153,21 +154,24 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         const uint64_t E = binom(N, 2), T3 = binom(N, 3);
         p.E2 = 1;
         while ((uint64_t)p.E2 < E) p.E2 <<= 1;
-        p.dK = (int)std::max<uint64_t>(1, (((T3 + 31) / 32) + 63) / 64);
+        const int kneed = (int)std::max<uint64_t>(1, (((T3 + 31) / 32) + 63) / 64);
+        p.dK = 0;
+        for (int k : kChainKs)
+            if (k >= kneed) {
+                p.dK = k;
+                break;
+            }
         p.inv_stride = (uint32_t)align_up(T3, 8);
         auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
         const uint64_t pre = 16 + al(4 * N * N);
         const uint64_t WP = 64ull * p.dK;
-        const uint64_t h1 = al(16 * E) + al(2ull * p.inv_stride) + 2 * al(4 * WP) + al(4 * p.piv_words[1]) +
-                            al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols);
-        uint64_t h2 = 0;
-        if (p.maxdim >= 2) {
-            const uint64_t w = kP1WCap;
-            h2 = (uint64_t)kSmallW * (8 * w + 16 * w + al(4 * (2 * w / 8)) + 16 * w);
-        }
-        p.small_lds = (uint32_t)(pre + std::max(h1, h2));
+        p.chain_lds = (uint32_t)(pre + al(16 * E) + al(2ull * p.inv_stride) + 2 * al(4 * WP) + al(4 * p.piv_words[1]) +
+                                 al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols));
+        const uint64_t w = kP1WCap;
+        p.p1_lds = (uint32_t)(pre + al(8 * w) + al(16 * w) + al(4 * (2 * w / 8)) + al(16 * w));
         p.prep_lds = (uint32_t)(pre + (uint64_t)p.E2 * 20);
-        if (p.small_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.dK > kMaxK) p.dense = false;
+        if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
+            p.dense = false;
     }
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
@@ -208,10 +212,12 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
         if (p.dense) {
             p.o_recs = take(L * binom(N, 2) * 16);
+            p.o_cls = take(L * binom(N, 2) * 4);
             p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
             if (p.maxdim >= 2) {
                 p.o_p1k = take(L * p.rcap[2] * 8);
                 p.o_p1i = take(L * p.rcap[2] * 4);
+                p.o_p1x = take(L * p.rcap[2] * 4);
                 p.o_roff2 = take(L * p.rcap[2] * 8);
                 p.o_rlen2 = take(L * p.rcap[2] * 4);
                 p.o_rpool2 = take(L * p.vpool_cap * 8);
@@ -233,8 +239,8 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
 struct Workspace {
     int device = -1;
     bool init = false;
-    hipStream_t stream = nullptr, stream2 = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr, evs = nullptr, evp = nullptr;
     char* dbuf = nullptr;
     size_t dcap = 0;
     OutPair* hout = nullptr;  // host-mapped
@@ -246,6 +252,7 @@ struct Workspace {
     size_t houtoff_cap = 0;
     std::vector<hipEvent_t> stage_ev;  // stage-time events (TDA_FLAG_STAGE_TIMES)
     std::vector<hipEvent_t> stage_ev2; // ... on the side stream
+    std::vector<hipEvent_t> stage_ev3; // ... on the third stream
     std::mutex mu;
 };
 
@@ -296,6 +303,9 @@ int ws_prepare(Workspace& w, const Plan& p) {
     if (!w.init) {
         HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
         HIPC(hipStreamCreateWithFlags(&w.stream2, hipStreamNonBlocking));
+        HIPC(hipStreamCreateWithFlags(&w.stream3, hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&w.evs, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&w.evp, hipEventDisableTiming));
         HIPC(hipEventCreate(&w.ev0));
         HIPC(hipEventCreate(&w.ev1));
         HIPC(hipEventCreateWithFlags(&w.evf, hipEventDisableTiming));
@@ -354,7 +364,11 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, true, false);
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
-    HIPC(hipFuncSetAttribute((const void*)k_reduce_small, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_h2_phase1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+#define TDA_ATTR_CHAIN(K) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    TDA_ATTR_CHAIN(1) TDA_ATTR_CHAIN(2) TDA_ATTR_CHAIN(3) TDA_ATTR_CHAIN(4) TDA_ATTR_CHAIN(6) TDA_ATTR_CHAIN(9)
+    TDA_ATTR_CHAIN(12) TDA_ATTR_CHAIN(16) TDA_ATTR_CHAIN(21)
+#undef TDA_ATTR_CHAIN
     HIPC(hipFuncSetAttribute((const void*)k_h1_prep, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -464,6 +478,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     hipStream_t s2 = w.stream2;
     HIPC(hipStreamWaitEvent(s2, w.evf, 0));
     StageTimer tm2{w2ev, s2, tm.on, {}};
+    StageTimer tm3{w.stage_ev3, w.stream3, tm.on, {}};
     if (int rc = tm2.begin()) return rc;
     if (n <= kSmallN) {
         hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s2, dist, n, a.thresh, stats,
@@ -484,6 +499,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     DenseBufs dnb = {};
     if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
         dnb.recs = (EdgeRec*)(B + p.o_recs);
+        dnb.cls = (uint32_t*)(B + p.o_cls);
         dnb.inv = (uint16_t*)(B + p.o_inv);
         dnb.E = (uint32_t)binom((uint64_t)n, 2);
         dnb.inv_stride = p.inv_stride;
@@ -552,6 +568,30 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipMemsetAsync(rb.windex, 0, (size_t)L * p.wcap_g * 2 * 8, s));
             HIPC(hipMemsetAsync(rb.wfill, 0, (size_t)L * p.wcap_g / 4 * 4, s));
         }
+        SmallBufs sb = {};
+        if (p.dense) {
+            sb.p1_next = (uint32_t*)(B + p.o_p1next);
+            sb.p1_key = (uint64_t*)(B + p.o_p1k);
+            sb.p1_info = (uint32_t*)(B + p.o_p1i);
+            sb.p1_pidx = (uint32_t*)(B + p.o_p1x);
+            sb.roff2 = (uint64_t*)(B + p.o_roff2);
+            sb.rlen2 = (uint32_t*)(B + p.o_rlen2);
+            sb.rpool2 = (uint64_t*)(B + p.o_rpool2);
+            sb.rpool2_cap = p.vpool_cap;
+            sb.p1_used = (unsigned long long*)(B + p.o_p1used);
+            sb.p1_wcap = kP1WCap;
+        }
+        if (p.dense && p.maxdim >= 2) {
+            // H2 phase 1 on a third stream: one wave per column, overlapping the H1 chains
+            HIPC(hipEventRecord(w.evs, s));
+            HIPC(hipStreamWaitEvent(w.stream3, w.evs, 0));
+            if (int rc = tm3.begin()) return rc;
+            hipLaunchKernelGGL(k_h2_phase1<true>, dim3(L, kP1Grid), dim3(64), p.p1_lds, w.stream3, dist, n, stats, db[2], sb,
+                               step_limit());
+            HIPC(hipGetLastError());
+            if (int rc = tm3.mark("k_h2_phase1")) return rc;
+            HIPC(hipEventRecord(w.evp, w.stream3));
+        }
         HIPC(hipStreamWaitEvent(s, w.evj, 0));  // join: forest edges (clearing of H1 columns)
         const bool p1 = n <= 1024, p2 = n <= 256;
         Pair* pairs1 = (Pair*)(B + p.o_pairs[1]);
@@ -561,22 +601,21 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     hipLaunchKernelGGL((k_reduce_all<LW, P1, P2>), dim3(L), dim3(64), rc.bytes, s, dist, n, p.maxdim, stats, db[1], db[2], rb, rc, \
                        pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
         if (p.dense) {
-            SmallBufs sb = {};
-            sb.p1_next = (uint32_t*)(B + p.o_p1next);
-            sb.p1_key = (uint64_t*)(B + p.o_p1k);
-            sb.p1_info = (uint32_t*)(B + p.o_p1i);
-            sb.roff2 = (uint64_t*)(B + p.o_roff2);
-            sb.rlen2 = (uint32_t*)(B + p.o_rlen2);
-            sb.rpool2 = (uint64_t*)(B + p.o_rpool2);
-            sb.rpool2_cap = p.vpool_cap;
-            sb.p1_used = (unsigned long long*)(B + p.o_p1used);
-            sb.p1_wcap = kP1WCap;
-            const int roles = 1 + (p.maxdim >= 2 ? kP1Blocks : 0);
-            hipLaunchKernelGGL(k_reduce_small, dim3(L, roles), dim3(kSmallT), p.small_lds, s, dist, n, p.maxdim, stats, db[1], db[2],
-                               rb, sb, dnb, step_limit(), pairs1, p.pcap[1]);
+            switch (p.dK) {
+#define TDA_CHAIN(K)                                                                                                          \
+    case K:                                                                                                                   \
+        hipLaunchKernelGGL(k_h1_chain<K>, dim3(L), dim3(kChainT), p.chain_lds, s, dist, n, stats, db[1], rb, dnb, step_limit(), \
+                           pairs1, p.pcap[1]);                                                                                \
+        break;
+                TDA_CHAIN(1) TDA_CHAIN(2) TDA_CHAIN(3) TDA_CHAIN(4) TDA_CHAIN(6) TDA_CHAIN(9) TDA_CHAIN(12) TDA_CHAIN(16) TDA_CHAIN(21)
+#undef TDA_CHAIN
+                default:
+                    return fail(TDA_E_INVALID, "no k_h1_chain instantiation for this N");
+            }
             HIPC(hipGetLastError());
-            MARK("k_reduce_small");
+            MARK("k_h1_chain");
             if (p.maxdim >= 2) {
+                HIPC(hipStreamWaitEvent(s, w.evp, 0));  // phase-1 results
                 hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[1], db[2], rb, rc, sb,
                                    pairs2, p.pcap[2]);
                 HIPC(hipGetLastError());
@@ -682,6 +721,20 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 arg, (long long)w.hstats[arg].n_adds[1], (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[7],
                 (unsigned long long)q[2], (unsigned long long)q[3], (unsigned long long)q[4], (unsigned long long)q[5],
                 (unsigned long long)p1max);
+        uint64_t sc = 0, cb = 0, tt = 0, ad = 0, mx = 0, mxa = 0;
+        for (int l = 0; l < L; ++l) {
+            sc += w.hstats[l].prof[1][4];
+            cb += w.hstats[l].prof[1][5];
+            tt += w.hstats[l].prof[1][6];
+            ad += w.hstats[l].prof[1][7];
+            if (w.hstats[l].prof[1][2] > mx) {
+                mx = w.hstats[l].prof[1][2];
+                mxa = w.hstats[l].prof[1][3] & 0xFFFF;
+            }
+        }
+        fprintf(stderr, "[tda-prof] H2 phase 1: all columns %llu cycles (scan %llu cob %llu), %llu adds; slowest column %llu cycles (%llu adds)\n",
+                (unsigned long long)tt, (unsigned long long)sc, (unsigned long long)cb, (unsigned long long)ad, (unsigned long long)mx,
+                (unsigned long long)mxa);
     }
     for (int d = 1; d <= p.maxdim; ++d) {
         uint64_t mx[8] = {0};
@@ -772,6 +825,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         (void)hipEventElapsedTime(&t, w.stage_ev2[i], w.stage_ev2[i + 1]);
         R->stage_ms.push_back(t);
         R->stage_name.push_back(tm2.names[i]);
+    }
+    for (size_t i = 0; i < tm3.names.size(); ++i) {  // third stream: H2 phase 1
+        float t = 0.0f;
+        (void)hipEventElapsedTime(&t, w.stage_ev3[i], w.stage_ev3[i + 1]);
+        R->stage_ms.push_back(t);
+        R->stage_name.push_back(tm3.names[i]);
     }
     o.n_stages = (int32_t)R->stage_name.size();
     o.stage_name = R->stage_name.data();

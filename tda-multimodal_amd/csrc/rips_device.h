@@ -131,6 +131,55 @@ template <typename T>
 __device__ __forceinline__ T ld_lds(const T* p, size_t i) { return ((const TDA_LDS T*)p)[i]; }
 template <typename T>
 __device__ __forceinline__ T ld_glb(const T* p, size_t i) { return ((const TDA_GLB T*)p)[i]; }
+template <typename T>
+__device__ __forceinline__ void st_lds(T* p, size_t i, T v) { ((TDA_LDS T*)p)[i] = v; }
+template <typename T>
+__device__ __forceinline__ void st_glb(T* p, size_t i, T v) { ((TDA_GLB T*)p)[i] = v; }
+// address-space-typed access chosen at compile time (LDS = true: local)
+template <bool LDS, typename T>
+__device__ __forceinline__ T mld(const T* p, size_t i) {
+    if constexpr (LDS) return ((const TDA_LDS T*)p)[i];
+    else return ((const TDA_GLB T*)p)[i];
+}
+template <bool LDS, typename T>
+__device__ __forceinline__ void mst(T* p, size_t i, T v) {
+    if constexpr (LDS) ((TDA_LDS T*)p)[i] = v;
+    else ((TDA_GLB T*)p)[i] = v;
+}
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+template <bool LDS>
+__device__ __forceinline__ u64x2 mld2(const uint64_t* p, size_t i) {  // 16-B load of p[i], p[i + 1]
+    if constexpr (LDS) return *(const TDA_LDS u64x2*)((const TDA_LDS uint64_t*)p + i);
+    else return *(const TDA_GLB u64x2*)((const TDA_GLB uint64_t*)p + i);
+}
+template <bool LDS, typename T>
+__device__ __forceinline__ T matomic_add(T* p, T v) {
+    if constexpr (LDS) return __hip_atomic_fetch_add((TDA_LDS T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else return __hip_atomic_fetch_add((TDA_GLB T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool LDS, typename T>
+__device__ __forceinline__ void matomic_xor(T* p, T v) {
+    if constexpr (LDS) __hip_atomic_fetch_xor((TDA_LDS T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_xor((TDA_GLB T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool LDS, typename T>
+__device__ __forceinline__ T matomic_cas(T* p, T cmp, T v) {  // returns the old value
+    if constexpr (LDS)
+        __hip_atomic_compare_exchange_strong((TDA_LDS T*)p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+        __hip_atomic_compare_exchange_strong((TDA_GLB T*)p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return cmp;
+}
+template <bool LDS, typename T>
+__device__ __forceinline__ void matomic_min(T* p, T v) {
+    if constexpr (LDS) __hip_atomic_fetch_min((TDA_LDS T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_min((TDA_GLB T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool LDS, typename T>
+__device__ __forceinline__ void matomic_or(T* p, T v) {
+    if constexpr (LDS) __hip_atomic_fetch_or((TDA_LDS T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_fetch_or((TDA_GLB T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // ---------------------------------------------------------------- staging
 // Copy nbytes (multiple of 4) global -> LDS with 16-B loads, 8 in flight per

@@ -22,6 +22,13 @@ struct Pair {
     float birth, death;
     int64_t birth_idx, death_idx;
 };
+// typed (non-FLAT) store of one pair to HBM
+__device__ __forceinline__ void store_pair(Pair* P, uint64_t i, float b, float d, int64_t bi, int64_t di) {
+    uint64_t* q = (uint64_t*)(P + i);
+    st_glb(q, 0, (uint64_t)__float_as_uint(b) | ((uint64_t)__float_as_uint(d) << 32));
+    st_glb(q, 1, (uint64_t)bi);
+    st_glb(q, 2, (uint64_t)di);
+}
 
 struct LayerStats {  // zeroed every call; copied to the host result
     float thresh;

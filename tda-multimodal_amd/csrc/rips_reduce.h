@@ -88,11 +88,15 @@ struct RowLo {
 // toggles one set of DISTINCT keys with the whole wave; new keys take
 // consecutive log positions [cnt, cnt + new) from the wave-uniform counter.
 constexpr uint64_t kDead = 1ull << 63;
+// LDS: log / index / fill live in LDS (else HBM); TLDS: the scratch `tmp` does.
+// Every access is address-space typed (no FLAT), so LDS round trips never
+// wait on the wave's outstanding HBM traffic.
+template <bool LDS, bool TLDS = LDS>
 struct KeySet {
     uint64_t* index;  // icap entries, 0 = free
     uint32_t* fill;   // per-bucket fill count (icap / 8)
     uint64_t* log;    // cap keys (| kDead when cancelled)
-    uint64_t* tmp;    // scratch >= 2 * cap keys (HBM)
+    uint64_t* tmp;    // scratch >= 2 * cap keys
     uint32_t imask;   // icap - 1
     uint32_t cnt;     // log length (wave-uniform register)
 
@@ -110,8 +114,9 @@ struct KeySet {
             bool want = false;
             uint32_t target = 0;
             if (pending) {
-                const ulonglong2* bp = (const ulonglong2*)&index[(size_t)bkt * 8];
-                const ulonglong2 q0 = bp[0], q1 = bp[1], q2 = bp[2], q3 = bp[3];
+                const size_t bo = (size_t)bkt * 8;
+                const u64x2 q0 = mld2<LDS>(index, bo), q1 = mld2<LDS>(index, bo + 2), q2 = mld2<LDS>(index, bo + 4),
+                            q3 = mld2<LDS>(index, bo + 6);
                 const uint64_t e[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
                 uint64_t eh = 0;
                 bool full = true;
@@ -121,10 +126,10 @@ struct KeySet {
                     full &= e[u] != 0;
                 }
                 if (eh) {
-                    atomicXor((unsigned long long*)&log[(uint32_t)eh - 1], (unsigned long long)kDead);  // flip parity
+                    matomic_xor<LDS>(&log[(uint32_t)eh - 1], kDead);  // flip parity
                     pending = false;
                 } else if (!full) {
-                    const uint32_t slot = atomicAdd(&fill[bkt], 1u);
+                    const uint32_t slot = matomic_add<LDS>(&fill[bkt], 1u);
                     if (slot < 8) {
                         want = true;
                         target = bkt * 8 + slot;
@@ -138,8 +143,8 @@ struct KeySet {
             const uint64_t need = __ballot(want);
             if (want) {
                 mine = cnt + lanes_below(need) + 1;
-                log[mine - 1] = k;  // new entry: live
-                index[target] = ((uint64_t)fp << 32) | mine;
+                mst<LDS>(log, mine - 1, k);  // new entry: live
+                mst<LDS>(index, target, ((uint64_t)fp << 32) | mine);
                 pending = false;
             }
             cnt += (uint32_t)__popcll(need);
@@ -149,26 +154,27 @@ struct KeySet {
     __device__ void reset(int ln) {
         const uint32_t c = cnt;
         if (c * 4 >= imask) {
-            for (uint32_t e = ln; e <= (imask >> 3); e += 64) fill[e] = 0;
-            for (uint32_t e = ln; e <= imask; e += 64) index[e] = 0;
+            for (uint32_t e = ln; e <= (imask >> 3); e += 64) mst<LDS>(fill, e, 0u);
+            for (uint32_t e = ln; e <= imask; e += 64) mst<LDS>(index, e, (uint64_t)0);
         } else {
             // probe each logged key's slot, then zero (two phases)
             uint32_t* slots = (uint32_t*)tmp;
             const uint32_t bmask = imask >> 3;
             for (uint32_t e = ln; e < c; e += 64) {
-                const uint32_t fp = (uint32_t)log[e];
+                const uint32_t fp = (uint32_t)mld<LDS>(log, e);
                 uint32_t h = (mix32(fp) & bmask) * 8;
                 for (;;) {
-                    const uint64_t cur = index[h];
+                    const uint64_t cur = mld<LDS>(index, h);
                     if (cur == 0 || (uint32_t)(cur >> 32) == fp) break;
                     h = (h + 1) & imask;  // buckets are filled in slot order
                 }
-                slots[e] = h;
+                mst<TLDS>(slots, e, h);
             }
             wave_sync();
             for (uint32_t e = ln; e < c; e += 64) {
-                index[slots[e]] = 0;
-                fill[slots[e] >> 3] = 0;
+                const uint32_t h = mld<TLDS>(slots, e);
+                mst<LDS>(index, h, (uint64_t)0);
+                mst<LDS>(fill, h >> 3, 0u);
             }
         }
         cnt = 0;
@@ -181,8 +187,8 @@ struct KeySet {
         uint32_t nl = 0;
         uint32_t e = 2 * ln;
         for (; e + 384 + 1 < c; e += 512) {  // 4 x 16-B loads in flight
-            const ulonglong2 a0 = *(const ulonglong2*)&log[e], a1 = *(const ulonglong2*)&log[e + 128];
-            const ulonglong2 a2 = *(const ulonglong2*)&log[e + 256], a3 = *(const ulonglong2*)&log[e + 384];
+            const u64x2 a0 = mld2<LDS>(log, e), a1 = mld2<LDS>(log, e + 128);
+            const u64x2 a2 = mld2<LDS>(log, e + 256), a3 = mld2<LDS>(log, e + 384);
             nl += (a0.x < kDead) + (a0.y < kDead) + (a1.x < kDead) + (a1.y < kDead) + (a2.x < kDead) + (a2.y < kDead) +
                   (a3.x < kDead) + (a3.y < kDead);
             uint64_t m0 = a0.x < a0.y ? a0.x : a0.y, m1 = a1.x < a1.y ? a1.x : a1.y;
@@ -193,8 +199,8 @@ struct KeySet {
             b = m0 < b ? m0 : b;
         }
         for (; e < c; e += 128) {
-            const uint64_t k0 = log[e];
-            const uint64_t k1 = e + 1 < c ? log[e + 1] : kEmpty64;
+            const uint64_t k0 = mld<LDS>(log, e);
+            const uint64_t k1 = e + 1 < c ? mld<LDS>(log, e + 1) : kEmpty64;
             nl += (k0 < kDead) + (k1 < kDead);
             const uint64_t m = k0 < k1 ? k0 : k1;
             b = m < b ? m : b;
@@ -204,15 +210,16 @@ struct KeySet {
         nlive = (uint32_t)wave_sum_u64(nl);
     }
     // write the live keys to out[] (whole wave), returns how many
+    template <bool OLDS = false>
     __device__ uint32_t gather_live(int ln, uint64_t* out) const {
         const uint32_t c = cnt;
         uint32_t pos = 0;
         for (uint32_t e0 = 0; e0 < c; e0 += 64) {
             uint32_t e = e0 + ln;
-            const uint64_t k = e < c ? log[e] : kEmpty64;
+            const uint64_t k = e < c ? mld<LDS>(log, e) : kEmpty64;
             const bool lv = k < kDead;
             uint64_t m = __ballot(lv);
-            if (lv) out[pos + lanes_below(m)] = k;
+            if (lv) mst<OLDS>(out, pos + lanes_below(m), k);
             pos += (uint32_t)__popcll(m);
         }
         return pos;
@@ -220,12 +227,12 @@ struct KeySet {
     // keep only live keys (whole wave)
     __device__ void compact(int ln) {
         uint64_t* kept = tmp + (imask + 1) / 2;  // after the slot scratch
-        const uint32_t pos = gather_live(ln, kept);
+        const uint32_t pos = gather_live<TLDS>(ln, kept);
         wave_sync();
         reset(ln);
         for (uint32_t e0 = 0; e0 < pos; e0 += 64) {
             const uint32_t e = e0 + ln;
-            toggle_pass(e < pos ? kept[e] : 0, e < pos, ln);
+            toggle_pass(e < pos ? mld<TLDS>(kept, e) : 0, e < pos, ln);
         }
         wave_sync();
     }
@@ -255,6 +262,7 @@ struct SmallBufs {
     uint32_t* p1_next;    // [L] next H2 column for a phase-1 wave (zeroed per call)
     uint64_t* p1_key;     // [L][rcap2] pivot key after phase 1 (kEmpty64: zero column)
     uint32_t* p1_info;    // [L][rcap2] additions | kP1Overflow
+    uint32_t* p1_pidx;    // [L][rcap2] index of the phase-1 pivot (when p1_key is a pivot)
     uint64_t* roff2;      // [L][rcap2] phase-1 working column, then R_j, in rpool2
     uint32_t* rlen2;
     uint64_t* rpool2;     // [L][rpool2_cap]
@@ -278,25 +286,49 @@ struct ReduceAllCfg {
 
 enum : int32_t { ERR_LDS_SPILL = 32, ERR_STEP_LIMIT = 64 };  // STEP_LIMIT: a column exceeded the pivot budget
 
-// residual pivot map of one dim: open addressing, key = row payload lo32
+// residual pivot map of one dim: open addressing, key = row payload lo32.
+// lds: the table lives in LDS (typed accesses), else in HBM.
 struct PivMap {
     uint64_t* k;
     uint32_t* v;
     uint64_t mask;
-    __device__ int64_t find(uint32_t lo, int ln) const {  // wave-parallel probe
+    bool lds;
+    template <bool L>
+    __device__ int64_t find_t(uint32_t lo, int ln) const {  // wave-parallel probe
         for (uint64_t h0 = mix32(lo);; h0 += 64) {
-            const uint64_t kk = k[(h0 + ln) & mask];
+            const uint64_t kk = mld<L>(k, (h0 + ln) & mask);
             const uint64_t mhit = __ballot(kk == lo), mend = __ballot(kk == kEmpty64);
             const uint64_t below_end = mend ? ((mend & (~mend + 1)) - 1) : ~0ull;
-            if (mhit & below_end) return (int64_t)v[(h0 + __builtin_ctzll(mhit & below_end)) & mask];
+            if (mhit & below_end) return (int64_t)mld<L>(v, (h0 + __builtin_ctzll(mhit & below_end)) & mask);
             if (mend) return -1;
         }
     }
-    __device__ void insert(uint32_t lo, uint32_t val) const {  // one lane
+    template <bool L>
+    __device__ void insert_t(uint32_t lo, uint32_t val) const {  // one lane
         uint64_t h = mix32(lo) & mask;
-        while (k[h] != kEmpty64) h = (h + 1) & mask;
-        k[h] = lo;
-        v[h] = val;
+        while (mld<L>(k, h) != kEmpty64) h = (h + 1) & mask;
+        mst<L>(k, h, (uint64_t)lo);
+        mst<L>(v, h, val);
+    }
+    __device__ int64_t find(uint32_t lo, int ln) const { return lds ? find_t<true>(lo, ln) : find_t<false>(lo, ln); }
+    // any number of lanes at once; keys must be distinct and absent
+    template <bool L>
+    __device__ void insert_par_t(uint32_t lo, uint32_t val) const {
+        uint64_t h = mix32(lo) & mask;
+        while (matomic_cas<L>(&k[h], kEmpty64, (uint64_t)lo) != kEmpty64) h = (h + 1) & mask;
+        mst<L>(v, h, val);
+    }
+    __device__ void insert_par(uint32_t lo, uint32_t val) const {
+        if (lds)
+            insert_par_t<true>(lo, val);
+        else
+            insert_par_t<false>(lo, val);
+    }
+    __device__ void insert(uint32_t lo, uint32_t val) const {
+        if (lds)
+            insert_t<true>(lo, val);
+        else
+            insert_t<false>(lo, val);
     }
 };
 
@@ -350,11 +382,13 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
         rcap2 = cfg.rmap_lds_cap;
         map.k = (uint64_t*)map_lds;
         map.v = (uint32_t*)(map_lds + 8ull * rcap2);
+        map.lds = true;
         for (uint64_t e = ln; e < rcap2; e += 64) map.k[e] = kEmpty64;
     } else {
         if (rcap2 > rb.rmap_stride) rcap2 = rb.rmap_stride;
         map.k = rb.rmap_keys + ((size_t)l * 2 + (DIM - 1)) * rb.rmap_stride;  // cleared by k_sort_resid
         map.v = rb.rmap_vals + ((size_t)l * 2 + (DIM - 1)) * rb.rmap_stride;
+        map.lds = false;
     }
     map.mask = rcap2 - 1;
     if (nres == 0) {
@@ -369,7 +403,7 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
-    KeySet W;
+    KeySet<LDSW, false> W;
     uint32_t wcap;
     if (LDSW) {
         wcap = cfg.wcap;
@@ -417,6 +451,7 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
     uint64_t* pre_k = (uint64_t*)pre_lds;
     uint64_t* pre_p = pre_k + pre_cap;
     uint32_t* pre_i = (uint32_t*)(pre_p + pre_cap);
+    uint32_t* pre_x = pre_i + pre_cap;
     const uint64_t npre = PH2 ? (nres < pre_cap ? nres : pre_cap) : 0;
     const uint64_t* p1k_g = PH2 ? sb->p1_key + (size_t)l * b.rcap : nullptr;
     const uint32_t* p1i_g = PH2 ? sb->p1_info + (size_t)l * b.rcap : nullptr;
@@ -432,11 +467,105 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
             uint64_t key, pk1;
             uint32_t info;
             ph2_load(j, key, pk1, info);
-            pre_k[j] = key;
-            pre_p[j] = pk1;
-            pre_i[j] = info;
+            st_lds(pre_k, j, key);
+            st_lds(pre_p, j, pk1);
+            st_lds(pre_i, j, info);
+            st_lds(pre_x, j, ld_glb(sb->p1_pidx + (size_t)l * b.rcap, j));
         }
         __syncthreads();
+    }
+    // PH2 prologue: column j pairs with its phase-1 pivot unless an earlier
+    // column already owns that pivot (or phase 1 overflowed).  Every column
+    // before the first such conflict is final, so they are emitted in
+    // parallel; the serial walk starts at the conflict.
+    uint64_t jstart = 0;
+    if (PH2 && LDSW && npre == nres) {
+        uint32_t tcap = 16;
+        while (tcap < 2 * nres + 16) tcap <<= 1;
+        if ((uint64_t)tcap * 8 <= 16ull * wcap) {
+            uint32_t* tk = (uint32_t*)W.index;  // temp table over the (still unused) W index
+            uint32_t* tv = tk + tcap;
+            for (uint32_t e = ln; e < tcap; e += 64) {
+                st_lds(tk, e, 0xFFFFFFFFu);
+                st_lds(tv, e, 0xFFFFFFFFu);
+            }
+            wave_sync();
+            for (uint64_t j = ln; j < nres; j += 64) {
+                const uint32_t info = ld_lds(pre_i, j);
+                const uint64_t pk1 = ld_lds(pre_p, j);
+                if (!(info & (kP1Cleared | kP1Overflow)) && pk1 != kEmpty64) {
+                    const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk1;
+                    uint32_t h = mix32(plo) & (tcap - 1);
+                    for (;;) {
+                        const uint32_t old = matomic_cas<true>(&tk[h], 0xFFFFFFFFu, plo);
+                        if (old == 0xFFFFFFFFu || old == plo) {
+                            matomic_min<true>(&tv[h], (uint32_t)j);
+                            break;
+                        }
+                        h = (h + 1) & (tcap - 1);
+                    }
+                }
+            }
+            wave_sync();
+            uint32_t jc = (uint32_t)nres;
+            for (uint64_t j = ln; j < nres; j += 64) {
+                const uint32_t info = ld_lds(pre_i, j);
+                const uint64_t pk1 = ld_lds(pre_p, j);
+                bool serial = false;
+                if (!(info & kP1Cleared)) {
+                    if (info & kP1Overflow) {
+                        serial = true;
+                    } else if (pk1 != kEmpty64) {
+                        const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk1;
+                        uint32_t h = mix32(plo) & (tcap - 1);
+                        while (ld_lds(tk, h) != plo) h = (h + 1) & (tcap - 1);
+                        serial = ld_lds(tv, h) != (uint32_t)j;
+                    }
+                }
+                if (serial) jc = min(jc, (uint32_t)j);
+            }
+            jc = wave_min_u32(jc);
+            uint64_t pcs = 0, pnp = 0, pad = 0, psk = 0;
+            for (uint32_t j0 = 0; j0 < jc; j0 += 64) {
+                const uint32_t j = j0 + ln;
+                const bool act = j < jc;
+                uint32_t info = 0;
+                uint64_t pk1 = kEmpty64, key = 0;
+                uint32_t pidx1 = 0;
+                if (act) {
+                    info = ld_lds(pre_i, j);
+                    pk1 = ld_lds(pre_p, j);
+                    key = ld_lds(pre_k, j);
+                    pidx1 = ld_lds(pre_x, j);
+                }
+                const bool cl = act && (info & kP1Cleared);
+                const bool ess = act && !cl && pk1 == kEmpty64;
+                const bool pr = act && !cl && pk1 != kEmpty64;
+                const float sdm = key_diam(key), pd = __uint_as_float((uint32_t)(pk1 >> 32));
+                const uint64_t sidx = key_idx(key);
+                const bool emit = ess || (pr && pd > sdm);
+                const uint64_t m = __ballot(emit);
+                const uint64_t pos = ecnt + lanes_below(m);
+                if (emit && pos < pcap) store_pair(P, pos, sdm, ess ? INFINITY : pd, (int64_t)sidx, ess ? -1 : (int64_t)pidx1);
+                ecnt += (uint64_t)__popcll(m);
+                if (pr) {
+                    pcs += pair_hash(sidx, pidx1);
+                    ++pnp;
+                    map.insert_par(0xFFFFFFFFu - (uint32_t)pk1, j);
+                    if (cfg.piv_lds) matomic_or<true>(&piv[pidx1 >> 5], 1u << (pidx1 & 31));
+                    matomic_or<false>(&pivg[pidx1 >> 5], 1u << (pidx1 & 31));
+                }
+                if (act && !cl) pad += info & ~kP1Overflow;
+                psk += cl;
+            }
+            cs += wave_sum_u64(pcs);
+            npairs += wave_sum_u64(pnp);
+            nadds += wave_sum_u64(pad);
+            nskip += wave_sum_u64(psk);
+            jstart = jc;
+            for (uint32_t e = ln; e <= W.imask; e += 64) st_lds(W.index, e, (uint64_t)0);
+            wave_sync();
+        }
     }
 #ifdef TDA_PROFILE
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // scan, lookup, facet, cob-app, cob-res, reset, compact, total
@@ -493,26 +622,27 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
 
     auto emit_essential = [&](uint64_t j, float sdm, uint64_t sidx) {
         if (ln == 0) {
-            if (ecnt < pcap) P[ecnt] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
+            if (ecnt < pcap) store_pair(P, ecnt, sdm, INFINITY, (int64_t)sidx, -1);
             rlen[j] = 0;
         }
         ++ecnt;
     };
     auto emit_pair = [&](uint64_t j, float sdm, uint64_t sidx, float pd, uint64_t pidx, uint32_t plo) {
         if (pd > sdm) {
-            if (ln == 0 && ecnt < pcap) P[ecnt] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
+            if (ln == 0 && ecnt < pcap) store_pair(P, ecnt, sdm, pd, (int64_t)sidx, (int64_t)pidx);
             ++ecnt;
         }
         if (ln == 0) {
             map.insert(plo, (uint32_t)j);
-            atomicOr(&piv[pidx >> 5], 1u << (pidx & 31));
-            if (piv != pivg) atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
+            if (cfg.piv_lds) matomic_or<true>(&piv[pidx >> 5], 1u << (pidx & 31));
+            matomic_or<false>(&pivg[pidx >> 5], 1u << (pidx & 31));
         }
         cs += pair_hash(sidx, pidx);
         npairs += 1;
     };
 
-    for (uint64_t j = 0; j < nres && !err; ++j) {
+    for (uint64_t j = jstart; j < nres && !err; ++j) {
+        TDA_STAMP(tA);
         uint64_t key, pk1 = 0;
         uint32_t info = 0;
         if (PH2) {
@@ -563,10 +693,15 @@ __device__ void reduce_dim(const ReduceCtx& c, const DimBufs& b, const Reduce2Bu
                 pidx1 = plo1;
             }
             // not apparent (phase 1 stopped there): a set bit is an earlier residual pivot
+            TDA_ACC(1, tA);
+            TDA_STAMP(tB);
             const uint32_t pw1 = cfg.piv_lds ? ld_lds(piv, pidx1 >> 5) : ld_glb((const uint32_t*)pivg, pidx1 >> 5);
             const int64_t own1 = ((pw1 >> (pidx1 & 31)) & 1u) ? map.find(plo1, ln) : -1;
+            TDA_ACC(2, tB);
             if (own1 < 0) {  // new pair; R_j is the stored phase-1 column
+                TDA_STAMP(tC);
                 emit_pair(j, sdm, sidx, __uint_as_float((uint32_t)(pk1 >> 32)), pidx1, plo1);
+                TDA_ACC(3, tC);
                 continue;
             }
             // continue Ripser's loop from the stored working column
@@ -787,7 +922,7 @@ __global__ __launch_bounds__(64) void k_reduce_h2_finish(const float* __restrict
     p += (4ull * n * n + 15) & ~15ull;
     c.D = dl;
     unsigned char* pre = p;
-    const uint32_t pre_cap = (uint32_t)(12ull * cfg.dim[1].rmap_lds_cap / 20);
+    const uint32_t pre_cap = (uint32_t)(12ull * cfg.dim[1].rmap_lds_cap / 24);
     p += 12ull * cfg.dim[1].rmap_lds_cap;
     __syncthreads();
     PivMap m2;

@@ -327,6 +327,7 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
     map.k = rb.rmap_keys + ((size_t)l * 2 + (DIM - 1)) * rb.rmap_stride;  // cleared by k_sort_resid
     map.v = rb.rmap_vals + ((size_t)l * 2 + (DIM - 1)) * rb.rmap_stride;
     map.mask = rcap2 - 1;
+    map.lds = false;
 
     BigHeap H;
     H.log = gb.log + (size_t)l * gb.cap;

@@ -42,10 +42,9 @@
 namespace tda {
 
 constexpr int kDenseMaxN = 64;
-constexpr int kSmallT = 256;              // threads per k_reduce_small block
-constexpr int kSmallW = kSmallT / 64;     // waves per block
-constexpr int kP1Blocks = 4;              // H2 phase-1 blocks per layer
-constexpr uint32_t kP1WCap = 512;         // phase-1 toggle-set capacity per wave
+constexpr int kChainT = 256;              // threads per k_h1_chain block (staging; the chain is wave 0)
+constexpr int kP1Grid = 96;               // k_h2_phase1 blocks per layer (one wave each, strided columns)
+constexpr uint32_t kP1WCap = 512;         // phase-1 toggle-set capacity
 constexpr int kChainMaxCols = 512;        // non-cleared H1 residual columns / stored R_j per layer
 constexpr int kMaxK = 21;                 // bitmap words per lane: ceil(C(64,3) / 32 / 64)
 
@@ -80,14 +79,16 @@ __device__ __forceinline__ void lds_xor(uint32_t* p, uint32_t v) {
 struct EdgeRec {
     uint64_t M;        // third vertices w of the triangles {a, b, w} <= thresh whose youngest facet is this edge
     uint16_t off;      // first rank of the block
-    uint16_t cs, ce;   // rank range [cs, ce) of the edge's length class
-    uint8_t a, b;      // vertices, a > b
+    uint16_t ab;       // a | b << 6 | tie << 12  (a > b; tie: the length class holds other edges)
+    float len;         // edge length
 };
 static_assert(sizeof(EdgeRec) == 16, "EdgeRec is one 16-B load");
 struct EdgeRecV {
     uint64_t M;
-    uint32_t off, cs, ce;
+    uint32_t off;
     int a, b;
+    bool tie;
+    float len;
 };
 __device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -95,15 +96,16 @@ __device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) {
     EdgeRecV v;
     v.M = (uint64_t)q.x | ((uint64_t)q.y << 32);
     v.off = q.z & 0xFFFFu;
-    v.cs = q.z >> 16;
-    v.ce = q.w & 0xFFFFu;
-    v.a = (int)((q.w >> 16) & 0xFFu);
-    v.b = (int)(q.w >> 24);
+    v.a = (int)((q.z >> 16) & 63u);
+    v.b = (int)((q.z >> 22) & 63u);
+    v.tie = (q.z >> 28) & 1u;
+    v.len = __uint_as_float(q.w);
     return v;
 }
 
 struct DenseBufs {
     EdgeRec* recs;      // [L][E]
+    uint32_t* cls;      // [L][E] rank range of the edge's length class: cs | ce << 16 (tie path)
     uint16_t* inv;      // [L][inv_stride] rank -> edge
     uint32_t E, inv_stride;
     int K;              // bitmap words per lane (W = 64 K words)
@@ -207,19 +209,19 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
         EdgeRec rec;
         rec.M = Ms[q];
         rec.off = (uint16_t)off[q];
-        rec.cs = (uint16_t)off[q0];
-        rec.ce = (uint16_t)(off[q1] + (uint32_t)__popcll(Ms[q1]));
-        rec.a = (uint8_t)a;
-        rec.b = (uint8_t)b;
+        rec.ab = (uint16_t)(a | (b << 6) | ((q0 != q1) << 12));
+        rec.len = __uint_as_float(lb);
         R[e] = rec;
+        db.cls[(size_t)l * db.E + e] = off[q0] | ((off[q1] + (uint32_t)__popcll(Ms[q1])) << 16);
     }
     for (int e = t; e < E; e += T) {  // edges above the threshold own no triangles
         int a, b;
         edge_verts((uint32_t)e, a, b);
-        if (!(D[a * n + b] <= r)) {
+        const float d = D[a * n + b];
+        if (!(d <= r)) {
             EdgeRec rec = {};
-            rec.a = (uint8_t)a;
-            rec.b = (uint8_t)b;
+            rec.ab = (uint16_t)(a | (b << 6));
+            rec.len = d;
             R[e] = rec;
         }
     }
@@ -232,21 +234,27 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
 }
 
 // ---------------------------------------------------------------- H1 chain
-// H1 of one layer.  All kSmallT threads stage the layer's tables and filter
+// H1 of one layer.  All kChainT threads stage the layer's tables and filter
 // the residual columns; then wave 0 alone runs the serial reduction (waves
-// 1..3 leave; no s_barrier is issued after that point).
-__device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const DimBufs& b, const Reduce2Bufs& rb,
-                         const DenseBufs& db, unsigned char* lds, uint64_t step_limit, Pair* __restrict__ pairs, uint64_t pcap) {
-    const int t = threadIdx.x, ln = t & 63, wv = t >> 6;
+// 1..3 leave; no s_barrier is issued after that point).  K = bitmap words per
+// lane (compile time: the pivot scan is K independent loads and a min tree).
+// LDS: [16][D][recs E][inv][W 64K][res 64K][piv][cols][own].
+template <int K>
+__global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                      DimBufs b, Reduce2Bufs rb, DenseBufs db, uint64_t step_limit,
+                                                      Pair* __restrict__ pairs, uint64_t pcap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr uint32_t WP = 64u * K;
+    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    LayerStats* st = stats + l;
     const int E = n * (n - 1) / 2;
-    const int K = db.K;
-    const uint32_t WP = 64u * (uint32_t)K;
-    unsigned char* p = lds;
+    unsigned char* p = smem + 16;
     auto take = [&](size_t bytes) {
         unsigned char* q = p;
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
+    float* Dl = (float*)take(4ull * n * n);
     EdgeRec* R = (EdgeRec*)take(16ull * E);
     uint16_t* inv = (uint16_t*)take(2ull * db.inv_stride);
     uint32_t* W = (uint32_t*)take(4ull * WP);
@@ -254,16 +262,17 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
     uint32_t* piv = (uint32_t*)take(4ull * b.piv_words);  // colex bitmap of apparent pivots (tie classes)
     uint64_t* cols = (uint64_t*)take(8ull * kChainMaxCols);
     uint16_t* own = (uint16_t*)take(2ull * kChainMaxCols);
-    uint32_t* hdr = (uint32_t*)(lds - 16 - ((4ull * n * n + 15) & ~15ull));  // smem[0..16)
+    uint32_t* hdr = (uint32_t*)smem;
 
     const uint32_t ntri = (uint32_t)st->ntri;
-    stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kSmallT);
-    stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kSmallT);
+    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, t, kChainT);
+    stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kChainT);
+    stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kChainT);
     uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
-    stage_to_lds(piv, pivg, 4ull * b.piv_words, t, kSmallT);
-    for (uint32_t i = t; i < WP; i += kSmallT) {
-        W[i] = 0;
-        res[i] = 0;
+    stage_to_lds(piv, pivg, 4ull * b.piv_words, t, kChainT);
+    for (uint32_t i = t; i < WP; i += kChainT) {
+        st_lds(W, i, 0u);
+        st_lds(res, i, 0u);
     }
     uint64_t nres = (uint64_t)st->n_residual[1];
     if (nres > b.rcap) nres = b.rcap;
@@ -282,7 +291,7 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
             }
             const uint64_t m = __ballot(keep);
             const uint32_t pos = nc + lanes_below(m);
-            if (keep && pos < (uint32_t)kChainMaxCols) cols[pos] = key;
+            if (keep && pos < (uint32_t)kChainMaxCols) st_lds(cols, pos, key);
             nc += (uint32_t)__popcll(m);
             nskip += (uint32_t)__popcll(__ballot(j < nres)) - (uint32_t)__popcll(m);
         }
@@ -299,6 +308,7 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
     Pair* P = pairs + (size_t)l * pcap;
     uint32_t* pool = (uint32_t*)(rb.rpool + (size_t)l * rb.rpool_cap);
     const uint64_t pool_words = 2ull * rb.rpool_cap;
+    const uint32_t* clsg = db.cls + (size_t)l * db.E;
     uint64_t ecnt = 0, cs = 0, npairs = 0, nadds = 0;
     uint32_t nown = 0;
     int err = nc > (uint32_t)kChainMaxCols ? 1 : 0;
@@ -341,23 +351,20 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
     };
     // first set bit of W (wave-uniform), false if W is empty
     auto first_bit = [&](uint32_t& rk) -> bool {
-        uint32_t w[kMaxK];
+        uint32_t w[K];
 #pragma unroll
-        for (int k = 0; k < kMaxK; ++k) w[k] = k < K ? ld_lds(W, (size_t)ln * K + k) : 0u;
-        int fk = -1;
-        uint32_t fv = 0;
+        for (int k = 0; k < K; ++k) w[k] = ld_lds(W, (size_t)ln * K + k);
+        uint32_t pos[K];
 #pragma unroll
-        for (int k = kMaxK - 1; k >= 0; --k)
-            if (w[k]) {
-                fk = k;
-                fv = w[k];
-            }
-        const uint64_t m = __ballot(fk >= 0);
+        for (int k = 0; k < K; ++k) pos[k] = w[k] ? (uint32_t)k * 32u + (uint32_t)__builtin_ctz(w[k]) : 0xFFFFu;
+#pragma unroll
+        for (int s = 1; s < K; s <<= 1)
+#pragma unroll
+            for (int k = 0; k + s < K; k += 2 * s) pos[k] = min(pos[k], pos[k + s]);
+        const uint64_t m = __ballot(pos[0] != 0xFFFFu);
         if (!m) return false;
         const int f = __builtin_ctzll(m);
-        const int wk = __builtin_amdgcn_readlane(fk, f);
-        const uint32_t val = (uint32_t)__builtin_amdgcn_readlane((int)fv, f);
-        rk = ((uint32_t)f * (uint32_t)K + (uint32_t)wk) * 32u + (uint32_t)__builtin_ctz(val);
+        rk = (uint32_t)f * (32u * K) + (uint32_t)__builtin_amdgcn_readlane((int)pos[0], f);
         return true;
     };
 
@@ -382,16 +389,16 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
             prof[7] += 1;
 #endif
             if (!found) {  // zero column: essential class
-                if (ln == 0 && ecnt < pcap) P[ecnt] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
+                if (ln == 0 && ecnt < pcap) store_pair(P, ecnt, sdm, INFINITY, (int64_t)sidx, -1);
                 ++ecnt;
                 TDA_ACC(1, t1);
                 break;
             }
             uint32_t e = ld_lds(inv, rk);
+            uint32_t resw = ld_lds(res, rk >> 5);
             EdgeRecV q = load_rec(R, e);
-            const bool tie = q.ce - q.cs != (uint32_t)__popcll(q.M);
             int w;
-            if (!tie) {
+            if (!q.tie) {
                 const uint32_t k = rk - q.off;
                 const int v = ln;
                 w = __builtin_ctzll(__ballot(((q.M >> v) & 1ull) && bits_above(q.M, v) == k));
@@ -400,14 +407,14 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
 #ifdef TDA_PROFILE
                 ++ties;
 #endif
+                const uint32_t cc = ld_glb(clsg, e), c0 = cc & 0xFFFFu, c1 = cc >> 16;
                 uint32_t best = 0, brk = rk;
-                for (uint32_t base = q.cs; base < q.ce; base += 64) {
+                for (uint32_t base = c0; base < c1; base += 64) {
                     const uint32_t rho = base + ln;
                     uint32_t cand = 0;
-                    if (rho < q.ce && ((ld_lds(W, rho >> 5) >> (rho & 31)) & 1u)) {
+                    if (rho < c1 && ((ld_lds(W, rho >> 5) >> (rho & 31)) & 1u)) {
                         const EdgeRecV q2 = load_rec(R, ld_lds(inv, rho));
-                        const int w2 = kth_highest(q2.M, rho - q2.off);
-                        cand = tri_id(q2.a, q2.b, w2) + 1;
+                        cand = tri_id(q2.a, q2.b, kth_highest(q2.M, rho - q2.off)) + 1;
                     }
                     const uint32_t m = wave_max_u32(cand);
                     if (m > best) {
@@ -417,16 +424,16 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
                 }
                 rk = brk;
                 e = ld_lds(inv, rk);
+                resw = ld_lds(res, rk >> 5);
                 q = load_rec(R, e);
                 w = kth_highest(q.M, rk - q.off);
             }
             const int a = q.a, b2 = q.b;
-            const float pd = ld_lds(Dl, (size_t)a * n + b2);
+            const float pd = q.len;
             const uint32_t tidx = tri_id(a, b2, w);
-            const bool isres = (ld_lds(res, rk >> 5) >> (rk & 31)) & 1u;
             TDA_ACC(1, t1);
             TDA_STAMP(t2);
-            if (isres) {
+            if ((resw >> (rk & 31)) & 1u) {
                 // add the stored reduced column of the residual column that owns rk
                 uint32_t s = 0;
                 for (uint32_t s0 = 0; s0 < nown; s0 += 64) {
@@ -438,10 +445,14 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
                     }
                 }
                 const uint32_t* src = pool + (size_t)s * WP;
-                for (int k = 0; k < K; ++k) W[(size_t)ln * K + k] ^= ld_glb(src, (size_t)k * 64 + ln);
+                uint32_t x[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) x[k] = ld_glb(src, (size_t)k * 64 + ln);
+#pragma unroll
+                for (int k = 0; k < K; ++k) st_lds(W, (size_t)ln * K + k, ld_lds(W, (size_t)ln * K + k) ^ x[k]);
                 ++nadds;
                 TDA_ACC(4, t2);
-            } else if (tie ? ((ld_lds(piv, tidx >> 5) >> (tidx & 31)) & 1u) : rk == q.off) {
+            } else if (q.tie ? ((ld_lds(piv, tidx >> 5) >> (tidx & 31)) & 1u) : rk == q.off) {
                 // apparent pair (e, t): add the coboundary of the youngest facet e
                 cob(a, b2, pd);
                 ++nadds;
@@ -449,7 +460,7 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
             } else {
                 // new persistence pair (column, t); R_j = W
                 if (pd > sdm) {
-                    if (ln == 0 && ecnt < pcap) P[ecnt] = Pair{sdm, pd, (int64_t)sidx, (int64_t)tidx};
+                    if (ln == 0 && ecnt < pcap) store_pair(P, ecnt, sdm, pd, (int64_t)sidx, (int64_t)tidx);
                     ++ecnt;
                 }
                 cs += pair_hash(sidx, tidx);
@@ -459,14 +470,15 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
                     break;
                 }
                 uint32_t* dst = pool + (size_t)nown * WP;
+#pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    dst[(size_t)k * 64 + ln] = W[(size_t)ln * K + k];
-                    W[(size_t)ln * K + k] = 0u;
+                    st_glb(dst, (size_t)k * 64 + ln, ld_lds(W, (size_t)ln * K + k));
+                    st_lds(W, (size_t)ln * K + k, 0u);
                 }
                 if (ln == 0) {
-                    own[nown] = (uint16_t)rk;
-                    res[rk >> 5] |= 1u << (rk & 31);
-                    atomicOr(&pivg[tidx >> 5], 1u << (tidx & 31));  // H2 clearing reads this bitmap
+                    st_lds(own, nown, (uint16_t)rk);
+                    st_lds(res, rk >> 5, resw | (1u << (rk & 31)));
+                    matomic_or<false>(&pivg[tidx >> 5], 1u << (tidx & 31));  // H2 clearing reads this bitmap
                 }
                 ++nown;
                 TDA_ACC(5, t2);
@@ -494,39 +506,47 @@ __device__ void h1_chain(const float* Dl, int n, LayerStats* st, int l, const Di
         st->nskip[1] = nskip;
     }
 }
+// bitmap words per lane supported by k_h1_chain instantiations
+constexpr int kChainKs[] = {1, 2, 3, 4, 6, 9, 12, 16, 21};
 
 // ---------------------------------------------------------------- H2 phase 1
-// Every wave of the layer's phase-1 blocks pulls residual H2 columns from a
-// per-layer counter and reduces each with apparent columns only, in its own
-// LDS toggle-set.  Waves run independently (wave_sync only).
+// One wave per block; block (l, g) takes the layer's residual H2 columns
+// g, g + kP1Grid, ... and reduces each with apparent columns only, in an LDS
+// toggle-set.  Thousands of independent columns fill the chip while the H1
+// chains run.  LDS: [16][D][log][index][fill][tmp].
 template <bool PACKED>
-__device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l, const DimBufs& b, const SmallBufs& sb,
-                          unsigned char* lds, uint64_t step_limit) {
+__global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats, DimBufs b,
+                                                  SmallBufs sb, uint64_t step_limit) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int DIM = 2, NV = 4;
     using Lo = RowLo<NV>;
-    const int ln = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int l = blockIdx.x, ln = threadIdx.x;
+    LayerStats* st = stats + l;
     uint64_t nres = (uint64_t)st->n_residual[2];
     if (nres > b.rcap) nres = b.rcap;
+    if (blockIdx.y >= nres) return;
+    const float r = st->thresh;
     const uint64_t* resid = b.resid + (size_t)l * b.rcap;
     const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
+    float* Dl = (float*)(smem + 16);
+    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, ln, 64);
 
     const uint32_t wcap = sb.p1_wcap;
-    const size_t wbytes = 8ull * wcap + 16ull * wcap + ((4ull * (2 * wcap / 8) + 15) & ~15ull) + 16ull * wcap;
-    unsigned char* p = lds + wbytes * wv;
+    unsigned char* p = smem + 16 + ((4ull * n * n + 15) & ~15ull);
     auto take = [&](size_t bytes) {
         unsigned char* q = p;
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
-    KeySet W;
+    KeySet<true, true> W;
     W.log = (uint64_t*)take(8ull * wcap);
     W.index = (uint64_t*)take(16ull * wcap);
     W.fill = (uint32_t*)take(4ull * (2 * wcap / 8));
     W.tmp = (uint64_t*)take(8ull * 2 * wcap);
     W.imask = 2 * wcap - 1;
     W.cnt = 0;
-    for (uint32_t e = ln; e <= W.imask; e += 64) W.index[e] = 0;
-    for (uint32_t e = ln; e <= (W.imask >> 3); e += 64) W.fill[e] = 0;
+    for (uint32_t e = ln; e <= W.imask; e += 64) st_lds(W.index, e, (uint64_t)0);
+    for (uint32_t e = ln; e <= (W.imask >> 3); e += 64) st_lds(W.fill, e, 0u);
     wave_sync();
     const uint32_t wlim = (wcap >> 1) + (wcap >> 2);
 
@@ -535,13 +555,15 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
     uint64_t* roff = sb.roff2 + (size_t)l * b.rcap;
     uint32_t* rlen = sb.rlen2 + (size_t)l * b.rcap;
 
-    auto cob = [&](const int (&vs)[DIM + 1], float sd) {
+    // coboundary entry of lane v: key, validity; returns the ballot of lanes
+    // whose cofacet has diameter sd (the oldest cofacet is its highest lane)
+    auto cob_key = [&](const int (&vs)[DIM + 1], float sd, uint64_t& key, bool& ok) -> uint64_t {
         const int v = ln;
-        bool ok = v < n;
+        ok = v < n;
 #pragma unroll
         for (int i = 0; i <= DIM; ++i) ok &= (vs[i] != v);
         float cd = sd;
-        uint64_t key = 0;
+        key = 0;
         if (ok) {
 #pragma unroll
             for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, ld_lds(Dl, (size_t)vs[i] * n + v));
@@ -566,17 +588,23 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
             }
             key = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | (0xFFFFFFFFu - lo);
         }
+        return __ballot(ok && cd == sd);
+    };
+    auto cob = [&](const int (&vs)[DIM + 1], float sd) {
+        uint64_t key;
+        bool ok;
+        (void)cob_key(vs, sd, key, ok);
         W.toggle_pass(key, ok, ln);
     };
 
 #ifdef TDA_PROFILE
     const uint64_t t_p1 = clock64();
 #endif
-    for (;;) {
-        uint32_t jn = 0;
-        if (ln == 0) jn = atomicAdd(&sb.p1_next[l], 1u);
-        const uint64_t j = (uint64_t)__shfl(jn, 0, 64);
-        if (j >= nres) break;
+    for (uint64_t j = blockIdx.y; j < nres; j += gridDim.y) {
+#ifdef TDA_PROFILE
+        const uint64_t tcol = clock64();
+        uint64_t tscan = 0, tcob = 0;
+#endif
         const uint64_t key = ld_glb(resid, j);
         const uint64_t sidx = key_idx(key);
         const float sdm = key_diam(key);
@@ -584,17 +612,22 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
         decode_wave<DIM>(sidx, n, vs, ln);
         cob(vs, sdm);
         wave_sync();
-        uint32_t adds = 0, flags = 0;
+        uint32_t adds = 0, flags = 0, out_idx = 0;
         uint64_t out_key = kEmpty64;
         for (uint64_t step = 0;; ++step) {
             uint64_t pk;
             uint32_t nlive;
+#ifdef TDA_PROFILE
+            const uint64_t ts0 = clock64();
+#endif
             W.scan(ln, pk, nlive);
+#ifdef TDA_PROFILE
+            tscan += clock64() - ts0;
+#endif
             if (step >= step_limit) {
                 flags = kP1Overflow;  // phase 2 redoes it from scratch (and enforces the limit)
                 break;
             }
-            if (W.cnt > 2 * nlive + 256) W.compact(ln);
             if (pk == kEmpty64) break;
             const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
             int t[NV];
@@ -606,25 +639,7 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
                 pidx = plo;
                 decode_wave<DIM + 1>(pidx, n, t, ln);
             }
-            const uint32_t pw = ld_glb(pivg, pidx >> 5);
-            if (!((pw >> (pidx & 31)) & 1u)) {  // not apparent: phase 1 ends here
-                out_key = pk;
-                const uint32_t nl = nlive;
-                unsigned long long base = 0;
-                if (ln == 0) base = atomicAdd(&sb.p1_used[l], (unsigned long long)nl);
-                base = __shfl(base, 0, 64);
-                if (base + nl > sb.rpool2_cap) {
-                    flags = kP1Overflow;
-                    break;
-                }
-                const uint32_t wr = W.gather_live(ln, sb.rpool2 + (size_t)l * sb.rpool2_cap + base);
-                if (ln == 0) {
-                    roff[j] = base;
-                    rlen[j] = wr;
-                }
-                break;
-            }
-            // apparent column: youngest facet's coboundary
+            // youngest facet f of the pivot t (max diameter, ties -> smallest index)
             float dd[NV][NV];
 #pragma unroll
             for (int i = 0; i < NV; ++i)
@@ -646,12 +661,41 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
                 }
             }
             int fv[DIM + 1];
+            int tv = t[0];
 #pragma unroll
             for (int u = 0; u < NV; ++u) {
                 if (u != fu) continue;
+                tv = t[u];
 #pragma unroll
                 for (int i = 0, q = 0; i < NV; ++i)
                     if (i != u) fv[q++] = t[i];
+            }
+            // (f, t) is an apparent pair iff diam t == diam f and t is the
+            // oldest cofacet of f: the highest vertex v with diam(f u v) ==
+            // diam f.  Apparent pairs form a matching [upstream ripser.cpp
+            // get_zero_apparent_facet], so this equals k_apparent's bitmap.
+            uint64_t ckey;
+            bool cok;
+            const uint64_t eq = cob_key(fv, fd, ckey, cok);
+            const float pd = __uint_as_float((uint32_t)(pk >> 32));
+            const bool app = pd == fd && eq && 63 - __clzll(eq) == tv;
+            if (!app) {  // not apparent: phase 1 ends here
+                out_key = pk;
+                out_idx = (uint32_t)pidx;
+                const uint32_t nl = nlive;
+                unsigned long long base = 0;
+                if (ln == 0) base = atomicAdd(&sb.p1_used[l], (unsigned long long)nl);
+                base = __shfl(base, 0, 64);
+                if (base + nl > sb.rpool2_cap) {
+                    flags = kP1Overflow;
+                    break;
+                }
+                const uint32_t wr = W.template gather_live<false>(ln, sb.rpool2 + (size_t)l * sb.rpool2_cap + base);
+                if (ln == 0) {
+                    st_glb(roff, j, (uint64_t)base);
+                    st_glb(rlen, j, wr);
+                }
+                break;
             }
             if (W.cnt + (uint32_t)n > wlim) {
                 W.compact(ln);
@@ -660,13 +704,29 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
                     break;
                 }
             }
-            cob(fv, fd);
+#ifdef TDA_PROFILE
+            const uint64_t tc0 = clock64();
+#endif
+            W.toggle_pass(ckey, cok, ln);
             ++adds;
             wave_sync();
+#ifdef TDA_PROFILE
+            tcob += clock64() - tc0;
+#endif
         }
         if (ln == 0) {
-            p1k[j] = out_key;
-            p1i[j] = adds | flags;
+            st_glb(p1k, j, out_key);
+            st_glb(p1i, j, adds | flags);
+            st_glb(sb.p1_pidx + (size_t)l * b.rcap, j, out_idx);
+#ifdef TDA_PROFILE
+            const uint64_t tt = clock64() - tcol;
+            atomicMax((unsigned long long*)&st->prof[1][2], (unsigned long long)tt);
+            atomicMax((unsigned long long*)&st->prof[1][3], (unsigned long long)((tt << 16) | (adds & 0xFFFF)));
+            atomicAdd((unsigned long long*)&st->prof[1][4], (unsigned long long)tscan);
+            atomicAdd((unsigned long long*)&st->prof[1][5], (unsigned long long)tcob);
+            atomicAdd((unsigned long long*)&st->prof[1][6], (unsigned long long)tt);
+            atomicAdd((unsigned long long*)&st->prof[1][7], (unsigned long long)adds);
+#endif
         }
         wave_sync();
         W.reset(ln);
@@ -674,25 +734,6 @@ __device__ void h2_phase1(const float* Dl, int n, float r, LayerStats* st, int l
 #ifdef TDA_PROFILE
     if (ln == 0) atomicMax((unsigned long long*)&st->prof[1][0], (unsigned long long)(clock64() - t_p1));
 #endif
-}
-
-// One launch, two roles: blockIdx.y == 0 runs the H1 chain of layer
-// blockIdx.x, blockIdx.y = 1..kP1Blocks run H2 phase 1 (kSmallW waves each).
-__global__ __launch_bounds__(kSmallT) void k_reduce_small(const float* __restrict__ dist, int n, int maxdim,
-                                                          LayerStats* __restrict__ stats, DimBufs b1, DimBufs b2, Reduce2Bufs rb,
-                                                          SmallBufs sb, DenseBufs db, uint64_t step_limit, Pair* __restrict__ pairs1,
-                                                          uint64_t pcap1) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, role = blockIdx.y;
-    LayerStats* st = stats + l;
-    float* Dl = (float*)(smem + 16);
-    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, threadIdx.x, kSmallT);
-    unsigned char* p = smem + 16 + ((4ull * n * n + 15) & ~15ull);
-    __syncthreads();
-    if (role == 0)
-        h1_chain(Dl, n, st, l, b1, rb, db, p, step_limit, pairs1, pcap1);
-    else if (maxdim >= 2)
-        h2_phase1<true>(Dl, n, st->thresh, st, l, b2, sb, p, step_limit);
 }
 
 }  // namespace tda
