@@ -253,7 +253,27 @@ struct Workspace {
     std::vector<hipEvent_t> stage_ev;  // stage-time events (TDA_FLAG_STAGE_TIMES)
     std::vector<hipEvent_t> stage_ev2; // ... on the side stream
     std::vector<hipEvent_t> stage_ev3; // ... on the third stream
+    hipEvent_t evin = nullptr;         // caller's stream -> library stream
+    char* hin = nullptr;               // pinned staging of host inputs (stable graph source)
+    size_t hin_cap = 0;
+    uint64_t gen = 0;                  // bumped whenever a buffer baked into graphs moves
+    std::vector<struct GraphEntry> graphs;
     std::mutex mu;
+};
+
+// one captured launch sequence (everything between ev0 and ev1), replayed with
+// a single hipGraphLaunch when the same plan, input address and flags recur
+struct GraphKey {
+    int64_t L, N, D;
+    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big;
+    float thresh;
+    const void* x;
+    uint64_t gen;
+    bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
+};
+struct GraphEntry {
+    GraphKey key;
+    hipGraphExec_t exec;
 };
 
 // records an event after each stage when stage timing is on
@@ -262,6 +282,7 @@ struct StageTimer {
     hipStream_t s;
     bool on;
     std::vector<const char*> names;
+    hipError_t rec(hipEvent_t e) { return hipEventRecord(e, s); }
     int mark(const char* name) {
         if (!on) return 0;
         size_t i = names.size() + 1;
@@ -270,7 +291,7 @@ struct StageTimer {
             HIPC(hipEventCreate(&e));
             ev.push_back(e);
         }
-        HIPC(hipEventRecord(ev[i], s));
+        HIPC(rec(ev[i]));
         names.push_back(name);
         return 0;
     }
@@ -281,7 +302,7 @@ struct StageTimer {
             HIPC(hipEventCreate(&e));
             ev.push_back(e);
         }
-        HIPC(hipEventRecord(ev[0], s));
+        HIPC(rec(ev[0]));
         return 0;
     }
 };
@@ -299,6 +320,12 @@ Workspace* get_ws(int dev) {
     return w;
 }
 
+void drop_graphs(Workspace& w) {
+    for (auto& g : w.graphs) (void)hipGraphExecDestroy(g.exec);
+    w.graphs.clear();
+    ++w.gen;
+}
+
 int ws_prepare(Workspace& w, const Plan& p) {
     if (!w.init) {
         HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
@@ -310,9 +337,11 @@ int ws_prepare(Workspace& w, const Plan& p) {
         HIPC(hipEventCreate(&w.ev1));
         HIPC(hipEventCreateWithFlags(&w.evf, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evj, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&w.evin, hipEventDisableTiming));
         w.init = true;
     }
     if (w.dcap < p.total) {
+        drop_graphs(w);
         if (w.dbuf) HIPC(hipFree(w.dbuf));
         w.dbuf = nullptr;
         size_t cap = std::max<size_t>(p.total, w.dcap + w.dcap / 2);
@@ -320,17 +349,20 @@ int ws_prepare(Workspace& w, const Plan& p) {
         w.dcap = cap;
     }
     if (w.hstats_cap < (size_t)p.L) {
+        drop_graphs(w);
         if (w.hstats) HIPC(hipHostFree(w.hstats));
         HIPC(hipHostMalloc((void**)&w.hstats, sizeof(LayerStats) * p.L, hipHostMallocDefault));
         w.hstats_cap = p.L;
     }
     if (w.houtoff_cap < (size_t)p.L * 4) {
+        drop_graphs(w);
         if (w.houtoff) HIPC(hipHostFree(w.houtoff));
         HIPC(hipHostMalloc((void**)&w.houtoff, sizeof(int64_t) * p.L * 4, hipHostMallocDefault));
         w.houtoff_cap = p.L * 4;
     }
     size_t want = std::max<size_t>(1 << 16, (size_t)p.L * 256);
     if (w.hout_cap < want) {
+        drop_graphs(w);
         if (w.hout) HIPC(hipHostFree(w.hout));
         HIPC(hipHostMalloc((void**)&w.hout, sizeof(OutPair) * want, hipHostMallocMapped));
         HIPC(hipHostGetDevicePointer((void**)&w.hout_dev, w.hout, 0));
@@ -340,6 +372,7 @@ int ws_prepare(Workspace& w, const Plan& p) {
 }
 
 int grow_hout(Workspace& w, size_t need) {
+    drop_graphs(w);
     if (w.hout) HIPC(hipHostFree(w.hout));
     w.hout = nullptr;
     size_t cap = std::max(need, 2 * w.hout_cap);
@@ -417,28 +450,82 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     std::unique_lock<std::mutex> guard(w.mu);  // released before any retry (which re-enters)
     if (int rc = ws_prepare(w, p)) return rc;
     if (int rc = set_lds_attrs(dev)) return rc;
-    hipStream_t s = a.stream ? (hipStream_t)a.stream : w.stream;
+    // all work runs on the library stream, ordered after the caller's stream
+    hipStream_t s = w.stream;
+    if (a.stream) {
+        HIPC(hipEventRecord(w.evin, (hipStream_t)a.stream));
+        HIPC(hipStreamWaitEvent(s, w.evin, 0));
+    }
     char* B = w.dbuf;
     const int n = (int)p.N, L = (int)p.L;
     float* dist = (float*)(B + p.o_dist);
     LayerStats* stats = (LayerStats*)(B + p.o_stats);
+    const size_t esz = p.dtype == TDA_F64 ? 8 : 4;
+    PairSet ps = {};
+    for (int d = 0; d <= p.maxdim; ++d) {
+        ps.p[d] = (Pair*)(B + p.o_pairs[d]);
+        ps.cap[d] = p.pcap[d];
+    }
+
+    // host inputs go through a pinned staging buffer: a stable graph source
+    const void* xsrc = host_or_dev;
+    if (!a.x_on_device || input_kind == 2) {
+        const size_t xbytes = input_kind == 2 ? binom((uint64_t)n, 2) * 4
+                                              : (size_t)L * n * (input_kind == 1 ? (size_t)n : (size_t)p.D) * esz;
+        if (w.hin_cap < xbytes) {
+            drop_graphs(w);
+            if (w.hin) HIPC(hipHostFree(w.hin));
+            w.hin = nullptr;
+            HIPC(hipHostMalloc((void**)&w.hin, std::max<size_t>(xbytes, 1 << 16), hipHostMallocDefault));
+            w.hin_cap = std::max<size_t>(xbytes, 1 << 16);
+        }
+        if (xbytes) std::memcpy(w.hin, host_or_dev, xbytes);
+        xsrc = w.hin;
+    }
 
     StageTimer tm{w.stage_ev, s, (a.flags & TDA_FLAG_STAGE_TIMES) != 0, {}};
-    std::vector<hipEvent_t>& w2ev = w.stage_ev2;
+    StageTimer tm2{w.stage_ev2, w.stream2, tm.on, {}};
+    StageTimer tm3{w.stage_ev3, w.stream3, tm.on, {}};
+    GraphKey gk;
+    std::memset(&gk, 0, sizeof(gk));
+    gk.L = p.L;
+    gk.N = p.N;
+    gk.D = p.D;
+    gk.maxdim = p.maxdim;
+    gk.dtype = p.dtype;
+    gk.input_kind = input_kind;
+    gk.x_on_device = a.x_on_device;
+    gk.flags = a.flags;
+    gk.force_global = force_global;
+    gk.scale = scale;
+    gk.force_big = force_big;
+    gk.thresh = a.thresh;
+    gk.x = xsrc;
+    gk.gen = w.gen;
+    GraphEntry* ge = nullptr;
+    // stage-timed calls run eagerly: timing events inside a capture need
+    // external event nodes, which torch's bundled HIP runtime rejects
+    const bool use_graph = !getenv_is("TDA_GRAPH", "0") && !tm.on;
+    if (use_graph)
+        for (auto& g : w.graphs)
+            if (g.key == gk) ge = &g;
+    const bool capture = use_graph && !ge;
+    // ev0 / ev1 bracket the whole sequence; a graph replay records them around the launch
+    auto rec_t = [&](hipEvent_t e) { return capture ? hipSuccess : hipEventRecord(e, s); };
 #define MARK(name) \
     do {           \
         if (int rc_ = tm.mark(name)) return rc_; \
     } while (0)
-    HIPC(hipEventRecord(w.ev0, s));
+    auto enqueue = [&]() -> int {
+    HIPC(rec_t(w.ev0));
     if (int rc = tm.begin()) return rc;
     HIPC(hipMemsetAsync(B + p.memset_lo, 0, p.memset_hi - p.memset_lo, s));
     MARK("memset");
 
     // ---- distances (+ row maxima for the enclosing radius)
-    const size_t esz = p.dtype == TDA_F64 ? 8 : 4;
     uint32_t* rowmax = (uint32_t*)(B + p.o_rowmax);
     if (input_kind == 0) {
-        const void* x = host_or_dev;
+        const void* x = xsrc;
         if (!a.x_on_device) {
             HIPC(hipMemcpyAsync(B + p.o_x, x, (size_t)L * n * p.D * esz, hipMemcpyHostToDevice, s));
             x = B + p.o_x;
@@ -449,7 +536,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         else
             hipLaunchKernelGGL(k_distance<float>, grid, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax);
     } else {
-        const void* x = host_or_dev;
+        const void* x = xsrc;
         unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
         if (input_kind == 1) {
             if (!a.x_on_device) {
@@ -477,8 +564,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(hipEventRecord(w.evf, s));
     hipStream_t s2 = w.stream2;
     HIPC(hipStreamWaitEvent(s2, w.evf, 0));
-    StageTimer tm2{w2ev, s2, tm.on, {}};
-    StageTimer tm3{w.stage_ev3, w.stream3, tm.on, {}};
     if (int rc = tm2.begin()) return rc;
     if (n <= kSmallN) {
         hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s2, dist, n, a.thresh, stats,
@@ -645,29 +730,50 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 
     // ---- emission order + compaction into host-mapped memory
-    Pair* hptr[4] = {nullptr, nullptr, nullptr, nullptr};
-    uint64_t hpcap[4] = {0, 0, 0, 0};
-    for (int d = 0; d <= p.maxdim; ++d) {
-        hptr[d] = (Pair*)(B + p.o_pairs[d]);
-        hpcap[d] = p.pcap[d];
-    }
-    HIPC(hipMemcpyAsync(B + p.o_pptr, hptr, sizeof(hptr), hipMemcpyHostToDevice, s));
-    HIPC(hipMemcpyAsync(B + p.o_pcap, hpcap, sizeof(hpcap), hipMemcpyHostToDevice, s));
     if (p.maxdim >= 1) {
-        hipLaunchKernelGGL(k_finalize, dim3(L), dim3(1024), 8192 * 12, s, stats, p.maxdim, (Pair* const*)(B + p.o_pptr),
-                           (const uint64_t*)(B + p.o_pcap), (uint64_t*)(B + p.o_fk), (uint32_t*)(B + p.o_fv), p.sstride, 13);
+        hipLaunchKernelGGL(k_finalize, dim3(L), dim3(1024), 8192 * 12, s, stats, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
+                           (uint32_t*)(B + p.o_fv), p.sstride, 13);
         HIPC(hipGetLastError());
         MARK("k_finalize");
     }
     const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
-                       (const uint64_t*)(B + p.o_pcap), (int64_t*)(B + p.o_outoff), w.hout_dev, (uint64_t)w.hout_cap);
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, (int64_t*)(B + p.o_outoff), w.hout_dev,
+                       (uint64_t)w.hout_cap);
     HIPC(hipGetLastError());
     MARK("k_compact");
     HIPC(hipMemcpyAsync(w.hstats, stats, sizeof(LayerStats) * L, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(w.houtoff, B + p.o_outoff, sizeof(int64_t) * L * (p.maxdim + 1), hipMemcpyDeviceToHost, s));
     MARK("d2h_stats");
-    HIPC(hipEventRecord(w.ev1, s));
+    HIPC(rec_t(w.ev1));
+    return 0;
+    };  // enqueue
+    if (ge) {
+        HIPC(hipEventRecord(w.ev0, s));
+        HIPC(hipGraphLaunch(ge->exec, s));
+        HIPC(hipEventRecord(w.ev1, s));
+    } else if (capture) {
+        HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        const int rc = enqueue();
+        hipGraph_t graph = nullptr;
+        const hipError_t ce = hipStreamEndCapture(s, &graph);
+        if (rc) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
+        if (ce != hipSuccess) return fail(TDA_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+        GraphEntry e;
+        e.key = gk;
+        const hipError_t ie = hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ie != hipSuccess) return fail(TDA_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+        if (w.graphs.size() >= 16) drop_graphs(w), e.key.gen = w.gen;
+        w.graphs.push_back(e);
+        HIPC(hipEventRecord(w.ev0, s));
+        HIPC(hipGraphLaunch(w.graphs.back().exec, s));
+        HIPC(hipEventRecord(w.ev1, s));
+    } else {
+        if (int rc = enqueue()) return rc;
+    }
     HIPC(hipStreamSynchronize(s));
 
     int errs = 0;
@@ -680,8 +786,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         for (int l = 0; l < L; ++l) w.hstats[l].err = 0;
         HIPC(hipMemcpyAsync(stats, w.hstats, sizeof(LayerStats) * L, hipMemcpyHostToDevice, s));
         const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, (Pair* const*)(B + p.o_pptr),
-                           (const uint64_t*)(B + p.o_pcap), (int64_t*)(B + p.o_outoff), w.hout_dev, (uint64_t)w.hout_cap);
+        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, (int64_t*)(B + p.o_outoff), w.hout_dev,
+                           (uint64_t)w.hout_cap);
         HIPC(hipGetLastError());
         HIPC(hipMemcpyAsync(w.hstats, stats, sizeof(LayerStats) * L, hipMemcpyDeviceToHost, s));
         HIPC(hipMemcpyAsync(w.houtoff, B + p.o_outoff, sizeof(int64_t) * L * (p.maxdim + 1), hipMemcpyDeviceToHost, s));
@@ -732,6 +838,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 mxa = w.hstats[l].prof[1][3] & 0xFFFF;
             }
         }
+        const uint64_t* pp = w.hstats[0].prof[3];
+        fprintf(stderr, "[tda-prof] k_h1_prep layer 0: keys %llu sort %llu masks %llu scan %llu recs %llu inv %llu cycles\n",
+                (unsigned long long)pp[1], (unsigned long long)pp[2], (unsigned long long)pp[3], (unsigned long long)pp[4],
+                (unsigned long long)pp[5], (unsigned long long)pp[6]);
         fprintf(stderr, "[tda-prof] H2 phase 1: all columns %llu cycles (scan %llu cob %llu), %llu adds; slowest column %llu cycles (%llu adds)\n",
                 (unsigned long long)tt, (unsigned long long)sc, (unsigned long long)cb, (unsigned long long)ad, (unsigned long long)mx,
                 (unsigned long long)mxa);

@@ -43,7 +43,7 @@ struct LayerStats {  // zeroed every call; copied to the host result
     int64_t nskip[4];      // residual columns cleared by the serial reduction (host: n_residual - nskip)
     uint64_t rmask[4];     // residual pivot map mask used by the dim's reducer (HBM map consumers)
     int64_t ntri;          // N <= 64: triangles <= thresh (k_h1_prep ranks)
-    uint64_t prof[3][8];   // -DTDA_PROFILE builds: cycle counters of k_reduce2 per dim
+    uint64_t prof[4][8];   // -DTDA_PROFILE builds: cycle counters (per dim; [3]: k_h1_prep)
 };
 enum : int32_t { ERR_RESID_CAP = 1, ERR_PAIR_CAP = 2, ERR_WORK_CAP = 4, ERR_VPOOL_CAP = 8, ERR_OUT_CAP = 16 };
 
@@ -708,12 +708,17 @@ __global__ __launch_bounds__(1024) void k_sort_resid(LayerStats* __restrict__ st
     for (uint64_t e = threadIdx.x; e < cap; e += blockDim.x) rk[e] = kEmpty64;
 }
 
+// per-dim pair buffers, passed by value (no host-side pointer tables)
+struct PairSet {
+    Pair* p[4];
+    uint64_t cap[4];
+};
+
 // ------------------------------------------------------------------ finalize
 // Emission order of dims >= 1 (reference: births_and_deaths_by_dim filled in
 // column order, i.e. birth desc / column index asc; pinned 32/32 by
 // summary_stats.json all_h1_persistence_values).
-__global__ __launch_bounds__(1024) void k_finalize(LayerStats* __restrict__ stats, int maxdim, Pair* const* __restrict__ pairs,
-                                                   const uint64_t* __restrict__ pcap, uint64_t* __restrict__ skeys,
+__global__ __launch_bounds__(1024) void k_finalize(LayerStats* __restrict__ stats, int maxdim, PairSet ps, uint64_t* __restrict__ skeys,
                                                    uint32_t* __restrict__ svals, uint64_t sstride, int sort_log2) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x;
@@ -722,9 +727,9 @@ __global__ __launch_bounds__(1024) void k_finalize(LayerStats* __restrict__ stat
     uint32_t* sv = (uint32_t*)(sk + CH);
     for (int d = 1; d <= maxdim; ++d) {
         uint64_t cnt = (uint64_t)stats[l].count[d];
-        if (cnt > pcap[d]) cnt = pcap[d];
+        if (cnt > ps.cap[d]) cnt = ps.cap[d];
         if (cnt < 2) continue;
-        Pair* P = pairs[d] + (size_t)l * pcap[d];
+        Pair* P = ps.p[d] + (size_t)l * ps.cap[d];
         uint64_t* k = skeys + (size_t)l * sstride * 2;
         uint32_t* v = svals + (size_t)l * sstride * 2;
         for (uint64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
@@ -748,8 +753,7 @@ struct OutPair {
     float birth, death;
     int64_t birth_idx, death_idx;
 };
-__global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats, int L, int maxdim, Pair* const* __restrict__ pairs,
-                                                  const uint64_t* __restrict__ pcap, int64_t* __restrict__ out_off,
+__global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats, int L, int maxdim, PairSet ps, int64_t* __restrict__ out_off,
                                                   OutPair* __restrict__ out, uint64_t out_cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int64_t* off = (int64_t*)smem;  // L*nd + 1
@@ -757,7 +761,7 @@ __global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats
     for (int i = t; i < S; i += blockDim.x) {
         int l = i / nd, d = i % nd;
         int64_t c = stats[l].count[d];
-        if ((uint64_t)c > pcap[d]) c = (int64_t)pcap[d];
+        if ((uint64_t)c > ps.cap[d]) c = (int64_t)ps.cap[d];
         off[i + 1] = c;
     }
     __syncthreads();
@@ -774,7 +778,7 @@ __global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats
     for (int i = w; i < S; i += nw) {
         const int l = i / nd, d = i % nd;
         const int64_t c = off[i + 1] - off[i];
-        const Pair* P = pairs[d] + (size_t)l * pcap[d];
+        const Pair* P = ps.p[d] + (size_t)l * ps.cap[d];
         OutPair* o = out + off[i];
         for (int64_t e = ln; e < c; e += 64) o[e] = OutPair{P[e].birth, P[e].death, P[e].birth_idx, P[e].death_idx};
     }

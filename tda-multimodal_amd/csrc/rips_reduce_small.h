@@ -119,6 +119,13 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
                                                   float user_thresh, DenseBufs db, int E2, LayerStats* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, t = threadIdx.x, T = blockDim.x, ln = t & 63, wv = t >> 6, nw = T >> 6;
+#ifdef TDA_PROFILE
+    uint64_t tp[8];
+    tp[0] = clock64();
+#define TDA_PREP_STAMP(i) tp[i] = clock64()
+#else
+#define TDA_PREP_STAMP(i)
+#endif
     const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
     float* D = (float*)(smem + 16);
     stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, T);
@@ -141,6 +148,7 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
         sk[q] = k;
     }
     __syncthreads();
+    TDA_PREP_STAMP(1);
     for (int k = 2; k <= E2; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = t; i < E2; i += T) {
@@ -155,6 +163,7 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
             }
             __syncthreads();
         }
+    TDA_PREP_STAMP(2);
     for (int q = t; q < E2; q += T)
         if (sk[q] != kEmpty64 && (q + 1 == E2 || sk[q + 1] == kEmpty64)) s_ne = (uint32_t)(q + 1);
     __syncthreads();
@@ -181,6 +190,7 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
         }
     }
     __syncthreads();
+    TDA_PREP_STAMP(3);
     if (wv == 0) {  // exclusive scan of the block sizes
         uint32_t carry = 0;
         for (int q0 = 0; q0 < nE; q0 += 64) {
@@ -197,6 +207,7 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
         if (ln == 0) s_tot = carry;
     }
     __syncthreads();
+    TDA_PREP_STAMP(4);
     EdgeRec* R = db.recs + (size_t)l * db.E;
     for (int q = t; q < nE; q += T) {
         const uint32_t lb = (uint32_t)(sk[q] >> 32);
@@ -225,12 +236,19 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
             R[e] = rec;
         }
     }
+    TDA_PREP_STAMP(5);
     uint16_t* inv = db.inv + (size_t)l * db.inv_stride;
     for (int q = wv; q < nE; q += nw) {
         const uint32_t c = (uint32_t)__popcll(Ms[q]);
         if ((uint32_t)ln < c) inv[off[q] + ln] = (uint16_t)(uint32_t)sk[q];
     }
     if (t == 0) stats[l].ntri = s_tot;
+#ifdef TDA_PROFILE
+    TDA_PREP_STAMP(6);
+    if (t == 0)
+        for (int i = 1; i < 7; ++i) stats[l].prof[3][i] = tp[i] - tp[i - 1];
+#endif
+#undef TDA_PREP_STAMP
 }
 
 // ---------------------------------------------------------------- H1 chain

@@ -17,28 +17,75 @@ from __future__ import annotations
 
 import ctypes
 import warnings
-from dataclasses import dataclass, field
 
 import numpy as np
 
 from . import _lib
 
 
-@dataclass
-class LayerResult:
-    """Persistence of one layer (all arrays on the host)."""
+class _Batch:
+    """Host copies of one batched call's outputs; LayerResults are views into it."""
 
-    dgms: list
-    birth_idx: list
-    death_idx: list
-    num_edges: int
-    thresh: float
-    checksum: list = field(default_factory=list)
-    n_all_pairs: list = field(default_factory=list)
-    n_columns: list = field(default_factory=list)
-    n_residual: list = field(default_factory=list)
-    n_adds: list = field(default_factory=list)
-    dist: np.ndarray | None = None
+    __slots__ = ("L", "nd", "N", "pairs", "bounds", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist")
+
+
+class LayerResult:
+    """Persistence of one layer (all arrays on the host).
+
+    ``dgms`` (list of (n_k, 2) float64 arrays, ripser's emission order) is
+    built eagerly; the remaining fields are views into the batch's shared
+    arrays, materialised on access.
+    """
+
+    __slots__ = ("dgms", "_b", "_l")
+
+    def __init__(self, dgms, batch, layer):
+        self.dgms = dgms
+        self._b = batch
+        self._l = layer
+
+    def _seg(self, arr):
+        return [arr[a:e] for a, e in self._b.bounds[self._l]]
+
+    @property
+    def birth_idx(self):
+        return self._seg(self._b.bidx)
+
+    @property
+    def death_idx(self):
+        return self._seg(self._b.didx)
+
+    @property
+    def num_edges(self) -> int:
+        return int(self._b.ne[self._l])
+
+    @property
+    def thresh(self) -> float:
+        return float(self._b.thr[self._l])
+
+    @property
+    def checksum(self) -> list:
+        return self._b.cs[self._l].tolist()
+
+    @property
+    def n_all_pairs(self) -> list:
+        return self._b.na[self._l].tolist()
+
+    @property
+    def n_columns(self) -> list:
+        return self._b.nc[self._l].tolist()
+
+    @property
+    def n_residual(self) -> list:
+        return self._b.nr[self._l].tolist()
+
+    @property
+    def n_adds(self) -> list:
+        return self._b.nadd[self._l].tolist()
+
+    @property
+    def dist(self):
+        return None if self._b.dist is None else self._b.dist[self._l]
 
 
 def _arr(ptr, n, dtype):
@@ -48,10 +95,12 @@ def _arr(ptr, n, dtype):
     return np.frombuffer(ctypes.string_at(ptr, n * np.dtype(dtype).itemsize), dtype=dtype)
 
 
-def _unpack(res_p, want_dist: bool) -> tuple[list, float]:
+def _unpack(res_p, want_dist: bool) -> tuple[list, dict]:
     r = res_p.contents
     L, md, N = int(r.L), int(r.maxdim), int(r.N)
     nd = md + 1
+    b = _Batch()
+    b.L, b.nd, b.N = L, nd, N
     cnt = _arr(r.count, L * nd, np.int64)
     off = _arr(r.offset, L * nd, np.int64)
     total = int(cnt.sum())
@@ -59,28 +108,19 @@ def _unpack(res_p, want_dist: bool) -> tuple[list, float]:
     pairs = np.empty((total, 2), dtype=np.float64)
     pairs[:, 0] = _arr(r.birth, total, np.float32)
     pairs[:, 1] = _arr(r.death, total, np.float32)
-    bidx = _arr(r.birth_idx, total, np.int64)
-    didx = _arr(r.death_idx, total, np.int64)
-    thr = _arr(r.thresh, L, np.float32).tolist()
-    ne = _arr(r.num_edges, L, np.int64).tolist()
-    cs = _arr(r.checksum, L * nd, np.uint64).reshape(L, nd).tolist()
-    na = _arr(r.n_all_pairs, L * nd, np.int64).reshape(L, nd).tolist()
-    nc = _arr(r.n_columns, L * nd, np.int64).reshape(L, nd).tolist()
-    nr = _arr(r.n_residual, L * nd, np.int64).reshape(L, nd).tolist()
-    na2 = _arr(r.n_adds, L * nd, np.int64).reshape(L, nd).tolist()
-    dist = None
-    if want_dist and bool(r.dist):
-        dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N)
-    bounds = np.stack([off, off + cnt], axis=1).reshape(L, nd, 2).tolist()
-    out = []
-    for l in range(L):
-        bl = bounds[l]
-        out.append(LayerResult(
-            dgms=[pairs[a:b] for a, b in bl], birth_idx=[bidx[a:b] for a, b in bl],
-            death_idx=[didx[a:b] for a, b in bl], num_edges=ne[l], thresh=thr[l], checksum=cs[l],
-            n_all_pairs=na[l], n_columns=nc[l], n_residual=nr[l], n_adds=na2[l],
-            dist=None if dist is None else dist[l],
-        ))
+    b.pairs = pairs
+    b.bidx = _arr(r.birth_idx, total, np.int64)
+    b.didx = _arr(r.death_idx, total, np.int64)
+    b.thr = _arr(r.thresh, L, np.float32)
+    b.ne = _arr(r.num_edges, L, np.int64)
+    b.cs = _arr(r.checksum, L * nd, np.uint64).reshape(L, nd)
+    b.na = _arr(r.n_all_pairs, L * nd, np.int64).reshape(L, nd)
+    b.nc = _arr(r.n_columns, L * nd, np.int64).reshape(L, nd)
+    b.nr = _arr(r.n_residual, L * nd, np.int64).reshape(L, nd)
+    b.nadd = _arr(r.n_adds, L * nd, np.int64).reshape(L, nd)
+    b.dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N) if want_dist and bool(r.dist) else None
+    b.bounds = np.stack([off, off + cnt], axis=1).reshape(L, nd, 2).tolist()
+    out = [LayerResult([pairs[a:e] for a, e in bl], b, l) for l, bl in enumerate(b.bounds)]
     stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(int(r.n_stages))]
     return out, {"device_ms": float(r.device_ms), "stages": stages}
 
