@@ -69,13 +69,15 @@ struct Plan {
     int E2 = 0;          // edge count rounded up to a power of two (k_h1_prep sort)
     int dK = 0;          // dense H1 bitmap words per lane (a k_h1_chain instantiation)
     uint32_t inv_stride = 0;  // rank -> edge table stride (C(N,3) rounded up)
+    uint32_t tri_stride = 0;  // triangle -> rank table stride (C(N,3) rounded up)
+    bool fast = false;        // k_h1_chain FAST variant (rank_of + inv32 tables fit LDS)
     uint32_t chain_lds = 0;   // dynamic LDS of k_h1_chain
     uint32_t p1_lds = 0;      // dynamic LDS of k_h2_phase1
     uint32_t prep_lds = 0;    // dynamic LDS of k_h1_prep
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -165,11 +167,14 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         auto al = [](uint64_t x) { return (x + 15) & ~15ull; };
         const uint64_t pre = 16 + al(4 * N * N);
         const uint64_t WP = 64ull * p.dK;
-        p.chain_lds = (uint32_t)(pre + al(16 * E) + al(2ull * p.inv_stride) + 2 * al(4 * WP) + al(4 * p.piv_words[1]) +
-                                 al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols));
+        p.tri_stride = (uint32_t)align_up(T3, 8);
+        const uint64_t tail = 2 * al(4 * WP) + al(4 * p.piv_words[1]) + al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols);
+        const uint64_t fast_lds = pre + al(2ull * p.tri_stride) + al(4ull * p.inv_stride) + tail;
+        p.fast = p.dK <= kChainFastMaxK && fast_lds <= (uint64_t)kLdsMax && !getenv_is("TDA_CHAIN", "general");
+        p.chain_lds = (uint32_t)(p.fast ? fast_lds : pre + al(16 * E) + al(2ull * p.inv_stride) + tail);
         const uint64_t w = kP1WCap;
         p.p1_lds = (uint32_t)(pre + al(8 * w) + al(16 * w) + al(4 * (2 * w / 8)) + al(16 * w));
-        p.prep_lds = (uint32_t)(pre + (uint64_t)p.E2 * 20);
+        p.prep_lds = (uint32_t)(pre + 2048ull * 20);
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
     }
@@ -193,6 +198,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
     p.o_rowmax = take(L * N * 4);
     p.o_p1used = take(L * 8);
     p.o_p1next = take(L * 4);
+    if (p.dense) p.o_res1 = take(L * p.piv_words[1] * 4);
     p.memset_hi = o;
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
     p.o_tmp = take(L * 2 * p.max_rcap * 8);
@@ -214,6 +220,10 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
             p.o_recs = take(L * binom(N, 2) * 16);
             p.o_cls = take(L * binom(N, 2) * 4);
             p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
+            if (p.fast) {
+                p.o_inv32 = take(L * (uint64_t)p.inv_stride * 4);
+                p.o_rof = take(L * (uint64_t)p.tri_stride * 2);
+            }
             if (p.maxdim >= 2) {
                 p.o_p1k = take(L * p.rcap[2] * 8);
                 p.o_p1i = take(L * p.rcap[2] * 4);
@@ -265,7 +275,7 @@ struct Workspace {
 // a single hipGraphLaunch when the same plan, input address and flags recur
 struct GraphKey {
     int64_t L, N, D;
-    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big;
+    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant;
     float thresh;
     const void* x;
     uint64_t gen;
@@ -398,9 +408,11 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-#define TDA_ATTR_CHAIN(K) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    TDA_ATTR_CHAIN(1) TDA_ATTR_CHAIN(2) TDA_ATTR_CHAIN(3) TDA_ATTR_CHAIN(4) TDA_ATTR_CHAIN(6) TDA_ATTR_CHAIN(9)
-    TDA_ATTR_CHAIN(12) TDA_ATTR_CHAIN(16) TDA_ATTR_CHAIN(21)
+#define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    TDA_ATTR_CHAIN(1, false) TDA_ATTR_CHAIN(2, false) TDA_ATTR_CHAIN(3, false) TDA_ATTR_CHAIN(4, false) TDA_ATTR_CHAIN(6, false)
+    TDA_ATTR_CHAIN(9, false) TDA_ATTR_CHAIN(12, false) TDA_ATTR_CHAIN(16, false) TDA_ATTR_CHAIN(21, false)
+    TDA_ATTR_CHAIN(1, true) TDA_ATTR_CHAIN(2, true) TDA_ATTR_CHAIN(3, true) TDA_ATTR_CHAIN(4, true) TDA_ATTR_CHAIN(6, true)
+    TDA_ATTR_CHAIN(9, true) TDA_ATTR_CHAIN(12, true)
 #undef TDA_ATTR_CHAIN
     HIPC(hipFuncSetAttribute((const void*)k_h1_prep, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -499,6 +511,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.force_global = force_global;
     gk.scale = scale;
     gk.force_big = force_big;
+    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0);
     gk.thresh = a.thresh;
     gk.x = xsrc;
     gk.gen = w.gen;
@@ -585,11 +598,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
         dnb.recs = (EdgeRec*)(B + p.o_recs);
         dnb.cls = (uint32_t*)(B + p.o_cls);
+        dnb.res1 = (uint32_t*)(B + p.o_res1);
+        dnb.inv32 = (uint32_t*)(B + p.o_inv32);
+        dnb.rank_of = (uint16_t*)(B + p.o_rof);
+        dnb.tri_stride = p.tri_stride;
         dnb.inv = (uint16_t*)(B + p.o_inv);
         dnb.E = (uint32_t)binom((uint64_t)n, 2);
         dnb.inv_stride = p.inv_stride;
         dnb.K = p.dK;
-        hipLaunchKernelGGL(k_h1_prep, dim3(L), dim3(1024), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.E2, stats);
+        hipLaunchKernelGGL(k_h1_prep, dim3(L), dim3(1024), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.fast ? 1 : 0, stats);
         HIPC(hipGetLastError());
         if (int rc = tm2.mark("k_h1_prep")) return rc;
     }
@@ -605,24 +622,24 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         db[d].resid = (uint64_t*)(B + p.o_resid[d]);
         db[d].rcap = p.rcap[d];
         db[d].ncand = p.ncand[d];
+    }
+    auto launch_apparent = [&](int d, hipStream_t st) {
         uint64_t blocks = (p.ncand[d] + 255) / 256;
         unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, 4096 / L)));
         const bool dl = n <= kAppLdsMaxN;
         const size_t alds = 16 + (dl ? (size_t)n * n * 4 : 0);
         if (d == 1) {
             if (dl)
-                hipLaunchKernelGGL((k_apparent<1, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+                hipLaunchKernelGGL((k_apparent<1, true>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
             else
-                hipLaunchKernelGGL((k_apparent<1, false>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+                hipLaunchKernelGGL((k_apparent<1, false>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
         } else {
             if (dl)
-                hipLaunchKernelGGL((k_apparent<2, true>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+                hipLaunchKernelGGL((k_apparent<2, true>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
             else
-                hipLaunchKernelGGL((k_apparent<2, false>), dim3(gx, L), dim3(256), alds, s, dist, n, stats, db[d], rowmax, a.thresh);
+                hipLaunchKernelGGL((k_apparent<2, false>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
         }
-        HIPC(hipGetLastError());
-        MARK(d == 1 ? "k_apparent<1>" : "k_apparent<2>");
-    }
+    };
     Reduce2Bufs rb;
     rb.rmap_keys = (uint64_t*)(B + p.o_rmk);
     rb.rmap_vals = (uint32_t*)(B + p.o_rmv);
@@ -639,43 +656,70 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     rb.wcap = p.wcap_g;
     rb.mst = (const uint32_t*)(B + p.o_mst);
     rb.mst_words = p.mst_words;
+    SortArgs sa = {};
+    for (int d = 1; d <= p.maxdim; ++d) {
+        sa.resid[d] = db[d].resid;
+        sa.rcap[d] = db[d].rcap;
+    }
+    auto launch_sort = [&](int d0, int nd, hipStream_t st) {
+        // LDS chunk: the largest residual list of these dims, at most 16384 keys
+        uint64_t cap = 64;
+        for (int d = d0; d < d0 + nd; ++d) cap = std::max<uint64_t>(cap, std::min<uint64_t>(next_pow2(p.rcap[d]), 16384));
+        hipLaunchKernelGGL(k_sort_resid, dim3(L, nd), dim3(1024), cap * 8, st, stats, sa, (uint64_t*)(B + p.o_tmp), p.max_rcap,
+                           rb.rmap_keys, rb.rmap_stride, ilog2(cap), d0);
+    };
+    SmallBufs sb = {};
+    if (p.dense) {
+        sb.p1_next = (uint32_t*)(B + p.o_p1next);
+        sb.p1_key = (uint64_t*)(B + p.o_p1k);
+        sb.p1_info = (uint32_t*)(B + p.o_p1i);
+        sb.p1_pidx = (uint32_t*)(B + p.o_p1x);
+        sb.roff2 = (uint64_t*)(B + p.o_roff2);
+        sb.rlen2 = (uint32_t*)(B + p.o_rlen2);
+        sb.rpool2 = (uint64_t*)(B + p.o_rpool2);
+        sb.rpool2_cap = p.vpool_cap;
+        sb.p1_used = (unsigned long long*)(B + p.o_p1used);
+        sb.p1_wcap = kP1WCap;
+    }
+    // N <= 64 with H2: the H2 columns (apparent<2>, their sort, phase 1) run
+    // on a third stream beside the H1 chain; they only need apparent<1>'s
+    // pivot bitmap, and the chain records its residual pivots separately
+    const bool split2 = p.dense && p.maxdim >= 2;
     if (p.maxdim >= 1) {
-        SortArgs sa = {};
-        for (int d = 1; d <= p.maxdim; ++d) {
-            sa.resid[d] = db[d].resid;
-            sa.rcap[d] = db[d].rcap;
-        }
-        hipLaunchKernelGGL(k_sort_resid, dim3(L, p.maxdim), dim3(1024), 16384 * 8, s, stats, sa, (uint64_t*)(B + p.o_tmp),
-                           p.max_rcap, rb.rmap_keys, rb.rmap_stride, 14);
+        launch_apparent(1, s);
         HIPC(hipGetLastError());
-        MARK("k_sort_resid");
-        if (!p.lds_mode) {
-            HIPC(hipMemsetAsync(rb.windex, 0, (size_t)L * p.wcap_g * 2 * 8, s));
-            HIPC(hipMemsetAsync(rb.wfill, 0, (size_t)L * p.wcap_g / 4 * 4, s));
-        }
-        SmallBufs sb = {};
-        if (p.dense) {
-            sb.p1_next = (uint32_t*)(B + p.o_p1next);
-            sb.p1_key = (uint64_t*)(B + p.o_p1k);
-            sb.p1_info = (uint32_t*)(B + p.o_p1i);
-            sb.p1_pidx = (uint32_t*)(B + p.o_p1x);
-            sb.roff2 = (uint64_t*)(B + p.o_roff2);
-            sb.rlen2 = (uint32_t*)(B + p.o_rlen2);
-            sb.rpool2 = (uint64_t*)(B + p.o_rpool2);
-            sb.rpool2_cap = p.vpool_cap;
-            sb.p1_used = (unsigned long long*)(B + p.o_p1used);
-            sb.p1_wcap = kP1WCap;
-        }
-        if (p.dense && p.maxdim >= 2) {
-            // H2 phase 1 on a third stream: one wave per column, overlapping the H1 chains
+        MARK("k_apparent<1>");
+        if (split2) {
             HIPC(hipEventRecord(w.evs, s));
             HIPC(hipStreamWaitEvent(w.stream3, w.evs, 0));
             if (int rc = tm3.begin()) return rc;
+            launch_apparent(2, w.stream3);
+            HIPC(hipGetLastError());
+            if (int rc = tm3.mark("k_apparent<2>")) return rc;
+            launch_sort(2, 1, w.stream3);
+            HIPC(hipGetLastError());
+            if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
             hipLaunchKernelGGL(k_h2_phase1<true>, dim3(L, kP1Grid), dim3(64), p.p1_lds, w.stream3, dist, n, stats, db[2], sb,
                                step_limit());
             HIPC(hipGetLastError());
             if (int rc = tm3.mark("k_h2_phase1")) return rc;
             HIPC(hipEventRecord(w.evp, w.stream3));
+            launch_sort(1, 1, s);
+            HIPC(hipGetLastError());
+            MARK("k_sort_resid<1>");
+        } else {
+            for (int d = 2; d <= p.maxdim; ++d) {
+                launch_apparent(d, s);
+                HIPC(hipGetLastError());
+                MARK("k_apparent<2>");
+            }
+            launch_sort(1, p.maxdim, s);
+            HIPC(hipGetLastError());
+            MARK("k_sort_resid");
+        }
+        if (!p.lds_mode) {
+            HIPC(hipMemsetAsync(rb.windex, 0, (size_t)L * p.wcap_g * 2 * 8, s));
+            HIPC(hipMemsetAsync(rb.wfill, 0, (size_t)L * p.wcap_g / 4 * 4, s));
         }
         HIPC(hipStreamWaitEvent(s, w.evj, 0));  // join: forest edges (clearing of H1 columns)
         const bool p1 = n <= 1024, p2 = n <= 256;
@@ -686,13 +730,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     hipLaunchKernelGGL((k_reduce_all<LW, P1, P2>), dim3(L), dim3(64), rc.bytes, s, dist, n, p.maxdim, stats, db[1], db[2], rb, rc, \
                        pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
         if (p.dense) {
-            switch (p.dK) {
-#define TDA_CHAIN(K)                                                                                                          \
-    case K:                                                                                                                   \
-        hipLaunchKernelGGL(k_h1_chain<K>, dim3(L), dim3(kChainT), p.chain_lds, s, dist, n, stats, db[1], rb, dnb, step_limit(), \
-                           pairs1, p.pcap[1]);                                                                                \
+            switch (p.dK * 2 + (p.fast ? 1 : 0)) {
+#define TDA_CHAIN(K, F)                                                                                                          \
+    case K * 2 + F:                                                                                                              \
+        hipLaunchKernelGGL((k_h1_chain<K, F>), dim3(L), dim3(kChainT), p.chain_lds, s, dist, n, stats, db[1], rb, dnb, step_limit(), \
+                           pairs1, p.pcap[1]);                                                                                   \
         break;
-                TDA_CHAIN(1) TDA_CHAIN(2) TDA_CHAIN(3) TDA_CHAIN(4) TDA_CHAIN(6) TDA_CHAIN(9) TDA_CHAIN(12) TDA_CHAIN(16) TDA_CHAIN(21)
+                TDA_CHAIN(1, 0) TDA_CHAIN(2, 0) TDA_CHAIN(3, 0) TDA_CHAIN(4, 0) TDA_CHAIN(6, 0) TDA_CHAIN(9, 0) TDA_CHAIN(12, 0)
+                TDA_CHAIN(16, 0) TDA_CHAIN(21, 0)
+                TDA_CHAIN(1, 1) TDA_CHAIN(2, 1) TDA_CHAIN(3, 1) TDA_CHAIN(4, 1) TDA_CHAIN(6, 1) TDA_CHAIN(9, 1) TDA_CHAIN(12, 1)
 #undef TDA_CHAIN
                 default:
                     return fail(TDA_E_INVALID, "no k_h1_chain instantiation for this N");
@@ -702,7 +748,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             if (p.maxdim >= 2) {
                 HIPC(hipStreamWaitEvent(s, w.evp, 0));  // phase-1 results
                 hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[1], db[2], rb, rc, sb,
-                                   pairs2, p.pcap[2]);
+                                   (const uint32_t*)dnb.res1, pairs2, p.pcap[2]);
                 HIPC(hipGetLastError());
                 MARK("k_reduce_h2_finish");
             }

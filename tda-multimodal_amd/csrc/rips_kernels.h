@@ -691,9 +691,9 @@ struct SortArgs {
 };
 __global__ __launch_bounds__(1024) void k_sort_resid(LayerStats* __restrict__ stats, SortArgs sa, uint64_t* __restrict__ tmp,
                                                      uint64_t tmp_stride, uint64_t* __restrict__ rmap_keys, uint64_t rmap_stride,
-                                                     int sort_log2) {
+                                                     int sort_log2, int dim0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, dim = blockIdx.y + 1;
+    const int l = blockIdx.x, dim = blockIdx.y + dim0;
     uint64_t* resid = sa.resid[dim];
     const uint64_t rcap = sa.rcap[dim];
     uint64_t cnt = (uint64_t)stats[l].n_residual[dim];

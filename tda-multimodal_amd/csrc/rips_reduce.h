@@ -905,7 +905,7 @@ __global__ __launch_bounds__(64) void k_reduce_all(const float* __restrict__ dis
 // k_reduce_all carve with the H1-map area holding the prefetch.
 __global__ __launch_bounds__(64) void k_reduce_h2_finish(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
                                                          DimBufs b1, DimBufs b2, Reduce2Bufs rb, ReduceAllCfg cfg, SmallBufs sb,
-                                                         Pair* __restrict__ pairs2, uint64_t pcap2) {
+                                                         const uint32_t* __restrict__ res1, Pair* __restrict__ pairs2, uint64_t pcap2) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, ln = threadIdx.x;
     LayerStats* st = stats + l;
@@ -929,7 +929,7 @@ __global__ __launch_bounds__(64) void k_reduce_h2_finish(const float* __restrict
     DimBufs b = b2;
     b.cleared_words = b1.piv_words;  // stride of the clearing bitmap below
     c.lds = p + 12ull * cfg.dim[2].rmap_lds_cap;
-    reduce_dim<2, true, true, true, true>(c, b, rb, cfg.dim[2], m2, nullptr, p, pairs2, pcap2, &sb, b1.pivbits, pre, pre_cap);
+    reduce_dim<2, true, true, true, true>(c, b, rb, cfg.dim[2], m2, nullptr, p, pairs2, pcap2, &sb, res1, pre, pre_cap);
 }
 
 }  // namespace tda

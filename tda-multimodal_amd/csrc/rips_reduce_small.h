@@ -106,17 +106,69 @@ __device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) {
 struct DenseBufs {
     EdgeRec* recs;      // [L][E]
     uint32_t* cls;      // [L][E] rank range of the edge's length class: cs | ce << 16 (tie path)
-    uint16_t* inv;      // [L][inv_stride] rank -> edge
+    uint16_t* inv;      // [L][inv_stride] rank -> edge (general path)
+    uint32_t* inv32;    // [L][inv_stride] rank -> a | b << 6 | w << 12 | first << 18 | tie << 19 (FAST path)
+    uint16_t* rank_of;  // [L][tri_stride] triangle colex index -> rank, 0xFFFF above thresh (FAST path)
+    uint32_t tri_stride;
+    uint32_t* res1;     // [L][piv_words1] colex bitmap of residual H1 pivots (H2 clearing; zeroed per call)
     uint32_t E, inv_stride;
     int K;              // bitmap words per lane (W = 64 K words)
 };
 
 // ---------------------------------------------------------------- ranks
-// One 1024-thread block per layer: sort edges <= thresh by length, build each
-// edge's block mask, the exclusive scan of block sizes (= ranks), the class
-// ranges and rank -> edge.  LDS: [16][D][keys E2][counts E2][masks E2].
+// 2048 u64 keys in one 1024-thread block, ascending: two keys per thread in
+// registers; compare-exchange distances below 128 are in-wave shuffles, only
+// the 10 stages with distance >= 128 go through LDS (sk).
+__device__ __forceinline__ void sort2048(uint64_t& k0, uint64_t& k1, uint64_t* sk) {
+    const int t = threadIdx.x;
+    for (int k = 2; k <= 2048; k <<= 1) {
+        const bool up = ((2 * t) & k) == 0;
+        int j = k >> 1;
+        if (j >= 128) {
+            sk[2 * t] = k0;
+            sk[2 * t + 1] = k1;
+            __syncthreads();
+            for (; j >= 128; j >>= 1) {
+                // element pairs (i, i ^ j) with i < i ^ j: one per thread
+                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                const uint64_t x = sk[i], y = sk[i ^ j];
+                const bool u = (i & k) == 0;
+                if ((x > y) == u) {
+                    sk[i] = y;
+                    sk[i ^ j] = x;
+                }
+                __syncthreads();
+            }
+            k0 = sk[2 * t];
+            k1 = sk[2 * t + 1];
+            __syncthreads();
+        }
+        for (; j >= 2; j >>= 1) {
+            const int m = j >> 1;  // partner thread t ^ m (same wave: m < 64)
+            const uint64_t p0 = shfl_xor_u64(k0, m), p1 = shfl_xor_u64(k1, m);
+            const bool lower = (t & m) == 0;
+            const bool keep_min = lower == up;
+            k0 = keep_min ? (k0 < p0 ? k0 : p0) : (k0 > p0 ? k0 : p0);
+            k1 = keep_min ? (k1 < p1 ? k1 : p1) : (k1 > p1 ? k1 : p1);
+        }
+        {  // j == 1: inside the thread
+            const uint64_t lo = k0 < k1 ? k0 : k1, hi = k0 < k1 ? k1 : k0;
+            k0 = up ? lo : hi;
+            k1 = up ? hi : lo;
+        }
+    }
+}
+
+// One 1024-thread block per layer: sort the edges <= thresh by length, build
+// each edge's block mask, the exclusive scan of block sizes (= ranks), the
+// class ranges and the rank tables:
+//   recs[e], inv16[rank] = e           (general path)
+//   rank_of[triangle] (0xFFFF: above thresh), inv32[rank] = a | b << 6 |
+//   w << 12 | first-of-block << 18 | tie << 19      (FAST path, N <= ~51)
+// Keys are (length bits << 32 | e << 12 | a << 6 | b): no index decode after
+// the sort.  LDS: [16][D][keys 2048][counts 2048][masks 2048].
 __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
-                                                  float user_thresh, DenseBufs db, int E2, LayerStats* __restrict__ stats) {
+                                                  float user_thresh, DenseBufs db, int fast, LayerStats* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, t = threadIdx.x, T = blockDim.x, ln = t & 63, wv = t >> 6, nw = T >> 6;
 #ifdef TDA_PROFILE
@@ -130,63 +182,67 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
     float* D = (float*)(smem + 16);
     stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, T);
     uint64_t* sk = (uint64_t*)(smem + 16 + ((4ull * n * n + 15) & ~15ull));
-    uint32_t* off = (uint32_t*)(sk + E2);
-    uint64_t* Ms = (uint64_t*)(off + E2);
+    uint32_t* off = (uint32_t*)(sk + 2048);
+    uint64_t* Ms = (uint64_t*)(off + 2048);
     uint32_t& s_ne = *(uint32_t*)(smem + 4);
     uint32_t& s_tot = *(uint32_t*)(smem + 8);
     const int E = n * (n - 1) / 2;
     if (t == 0) s_ne = 0;
+    if (fast) {  // every triangle starts "above the threshold"
+        uint32_t* ro = (uint32_t*)(db.rank_of + (size_t)l * db.tri_stride);
+        for (uint32_t i = t; i < db.tri_stride / 2; i += T) st_glb(ro, i, 0xFFFFFFFFu);
+    }
     __syncthreads();
-    for (int q = t; q < E2; q += T) {
+    uint64_t k0 = kEmpty64, k1 = kEmpty64;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int q = 2 * t + c;
         uint64_t k = kEmpty64;
         if (q < E) {
             int a, b;
             edge_verts((uint32_t)q, a, b);
             const float d = D[a * n + b];
-            if (d <= r) k = ((uint64_t)__float_as_uint(d + 0.0f) << 32) | (uint32_t)q;
+            if (d <= r) k = ((uint64_t)__float_as_uint(d + 0.0f) << 32) | ((uint32_t)q << 12) | ((uint32_t)a << 6) | (uint32_t)b;
         }
-        sk[q] = k;
+        (c == 0 ? k0 : k1) = k;
     }
-    __syncthreads();
     TDA_PREP_STAMP(1);
-    for (int k = 2; k <= E2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < E2; i += T) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t x = sk[i], y = sk[ixj];
-                    if ((x > y) == ((i & k) == 0)) {
-                        sk[i] = y;
-                        sk[ixj] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    TDA_PREP_STAMP(2);
-    for (int q = t; q < E2; q += T)
-        if (sk[q] != kEmpty64 && (q + 1 == E2 || sk[q + 1] == kEmpty64)) s_ne = (uint32_t)(q + 1);
+    sort2048(k0, k1, sk);
+    sk[2 * t] = k0;
+    sk[2 * t + 1] = k1;
     __syncthreads();
+    // the thread holding the last real key publishes the edge count
+    if (k0 != kEmpty64 && k1 == kEmpty64) s_ne = (uint32_t)(2 * t + 1);
+    if (k1 != kEmpty64 && (t == T - 1 || sk[2 * t + 2] == kEmpty64)) s_ne = (uint32_t)(2 * t + 2);
+    __syncthreads();
+    TDA_PREP_STAMP(2);
     const int nE = (int)s_ne;
-    // block masks: one wave per edge, lane = third vertex
-    for (int q = wv; q < nE; q += nw) {
-        const uint64_t k = sk[q];
-        const uint32_t e = (uint32_t)k;
-        int a, b;
-        edge_verts(e, a, b);
-        const float le = __uint_as_float((uint32_t)(k >> 32));
-        const int v = ln;
-        bool ok = v < n && v != a && v != b;
-        if (ok) {
-            const float dav = D[a * n + v], dbv = D[b * n + v];
-            ok = dav <= le && dbv <= le;
-            if (ok && dav == le && edge_id(a, v) < e) ok = false;  // (a, v) is the younger facet
-            if (ok && dbv == le && edge_id(b, v) < e) ok = false;
+    // block masks: one wave per edge (4 edges in flight), lane = third vertex
+    for (int q0 = wv; q0 < nE; q0 += 4 * nw) {
+        uint64_t kk[4];
+        float dav[4], dbv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = q0 + u * nw;
+            kk[u] = q < nE ? sk[q] : kEmpty64;
+            const int a = (int)((kk[u] >> 6) & 63u), b = (int)(kk[u] & 63u);
+            dav[u] = ln < n ? D[a * n + ln] : 0.0f;
+            dbv[u] = ln < n ? D[b * n + ln] : 0.0f;
         }
-        const uint64_t m = __ballot(ok);
-        if (ln == 0) {
-            Ms[q] = m;
-            off[q] = (uint32_t)__popcll(m);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = q0 + u * nw;
+            const uint32_t e = (uint32_t)(kk[u] >> 12) & 0xFFFFFu;
+            const int a = (int)((kk[u] >> 6) & 63u), b = (int)(kk[u] & 63u), v = ln;
+            const float le = __uint_as_float((uint32_t)(kk[u] >> 32));
+            bool ok = q < nE && v < n && v != a && v != b && dav[u] <= le && dbv[u] <= le;
+            if (ok && dav[u] == le && edge_id(a, v) < e) ok = false;  // (a, v) is the younger facet
+            if (ok && dbv[u] == le && edge_id(b, v) < e) ok = false;
+            const uint64_t m = __ballot(ok);
+            if (ln == 0 && q < nE) {
+                Ms[q] = m;
+                off[q] = (uint32_t)__popcll(m);
+            }
         }
     }
     __syncthreads();
@@ -214,9 +270,8 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
         int q0 = q, q1 = q;
         while (q0 > 0 && (uint32_t)(sk[q0 - 1] >> 32) == lb) --q0;
         while (q1 + 1 < nE && (uint32_t)(sk[q1 + 1] >> 32) == lb) ++q1;
-        const uint32_t e = (uint32_t)sk[q];
-        int a, b;
-        edge_verts(e, a, b);
+        const uint32_t e = (uint32_t)(sk[q] >> 12) & 0xFFFFFu;
+        const int a = (int)((sk[q] >> 6) & 63u), b = (int)(sk[q] & 63u);
         EdgeRec rec;
         rec.M = Ms[q];
         rec.off = (uint16_t)off[q];
@@ -236,11 +291,27 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
             R[e] = rec;
         }
     }
+    __syncthreads();
     TDA_PREP_STAMP(5);
     uint16_t* inv = db.inv + (size_t)l * db.inv_stride;
+    uint32_t* inv32 = db.inv32 + (size_t)l * db.inv_stride;
+    uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
     for (int q = wv; q < nE; q += nw) {
-        const uint32_t c = (uint32_t)__popcll(Ms[q]);
-        if ((uint32_t)ln < c) inv[off[q] + ln] = (uint16_t)(uint32_t)sk[q];
+        const uint64_t key = sk[q];
+        const uint32_t e = (uint32_t)(key >> 12) & 0xFFFFFu;
+        const int a = (int)((key >> 6) & 63u), b = (int)(key & 63u);
+        const uint32_t lb = (uint32_t)(key >> 32);
+        const bool tie = (q > 0 && (uint32_t)(sk[q - 1] >> 32) == lb) || (q + 1 < nE && (uint32_t)(sk[q + 1] >> 32) == lb);
+        const uint64_t M = Ms[q];
+        const uint32_t o = off[q];
+        if (!fast) {
+            const uint32_t c = (uint32_t)__popcll(M);
+            if ((uint32_t)ln < c) inv[o + ln] = (uint16_t)e;
+        } else if (ln < n && ((M >> ln) & 1ull)) {
+            const uint32_t rk = o + bits_above(M, ln);
+            st_glb(inv32, rk, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(rk == o) << 18) | ((uint32_t)tie << 19));
+            st_glb(ro, tri_id(a, b, ln), (uint16_t)rk);
+        }
     }
     if (t == 0) stats[l].ntri = s_tot;
 #ifdef TDA_PROFILE
@@ -256,8 +327,10 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
 // the residual columns; then wave 0 alone runs the serial reduction (waves
 // 1..3 leave; no s_barrier is issued after that point).  K = bitmap words per
 // lane (compile time: the pivot scan is K independent loads and a min tree).
-// LDS: [16][D][recs E][inv][W 64K][res 64K][piv][cols][own].
-template <int K>
+// FAST (N <= ~51): a toggle is rank_of[triangle] -> ds_xor and the pivot's
+// vertices are one inv32 load; otherwise edge records (recs, inv16).
+// LDS: [16][D][recs E | rank_of][inv16 | inv32][W 64K][res 64K][piv][cols][own].
+template <int K, bool FAST>
 __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
                                                       DimBufs b, Reduce2Bufs rb, DenseBufs db, uint64_t step_limit,
                                                       Pair* __restrict__ pairs, uint64_t pcap) {
@@ -273,8 +346,10 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
         return q;
     };
     float* Dl = (float*)take(4ull * n * n);
-    EdgeRec* R = (EdgeRec*)take(16ull * E);
-    uint16_t* inv = (uint16_t*)take(2ull * db.inv_stride);
+    EdgeRec* R = FAST ? nullptr : (EdgeRec*)take(16ull * E);
+    uint16_t* inv = FAST ? nullptr : (uint16_t*)take(2ull * db.inv_stride);
+    uint16_t* rof = FAST ? (uint16_t*)take(2ull * db.tri_stride) : nullptr;
+    uint32_t* inv32 = FAST ? (uint32_t*)take(4ull * db.inv_stride) : nullptr;
     uint32_t* W = (uint32_t*)take(4ull * WP);
     uint32_t* res = (uint32_t*)take(4ull * WP);  // ranks that are residual pivots
     uint32_t* piv = (uint32_t*)take(4ull * b.piv_words);  // colex bitmap of apparent pivots (tie classes)
@@ -284,9 +359,15 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
 
     const uint32_t ntri = (uint32_t)st->ntri;
     stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, t, kChainT);
-    stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kChainT);
-    stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kChainT);
-    uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
+    if constexpr (FAST) {
+        stage_to_lds(rof, db.rank_of + (size_t)l * db.tri_stride, 2ull * db.tri_stride, t, kChainT);
+        stage_to_lds(inv32, db.inv32 + (size_t)l * db.inv_stride, 4ull * ntri, t, kChainT);
+    } else {
+        stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kChainT);
+        stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kChainT);
+    }
+    const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
+    uint32_t* res1 = db.res1 + (size_t)l * b.piv_words;
     stage_to_lds(piv, pivg, 4ull * b.piv_words, t, kChainT);
     for (uint32_t i = t; i < WP; i += kChainT) {
         st_lds(W, i, 0u);
@@ -339,6 +420,13 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
     // toggle the coboundary of edge (a, b) (length le <= r): lane v -> {a, b, v}
     auto cob = [&](int a, int b, float le) {
         const int v = ln;
+        if constexpr (FAST) {
+            if (v < n && v != a && v != b) {
+                const uint32_t rk = ld_lds(rof, tri_id(a, b, v));
+                if (rk != 0xFFFFu) lds_xor(&W[rk >> 5], 1u << (rk & 31));
+            }
+            return;
+        }
         bool ok = v < n && v != a && v != b;
         float dav = 0.0f, dbv = 0.0f;
         if (ok) {
@@ -412,27 +500,44 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 TDA_ACC(1, t1);
                 break;
             }
-            uint32_t e = ld_lds(inv, rk);
             uint32_t resw = ld_lds(res, rk >> 5);
-            EdgeRecV q = load_rec(R, e);
-            int w;
-            if (!q.tie) {
+            int a, b2, w;
+            bool tie, first;
+            if constexpr (FAST) {
+                const uint32_t q = ld_lds(inv32, rk);
+                a = (int)(q & 63u);
+                b2 = (int)((q >> 6) & 63u);
+                w = (int)((q >> 12) & 63u);
+                first = (q >> 18) & 1u;
+                tie = (q >> 19) & 1u;
+            } else {
+                const EdgeRecV q = load_rec(R, ld_lds(inv, rk));
+                a = q.a;
+                b2 = q.b;
+                tie = q.tie;
+                first = rk == q.off;
                 const uint32_t k = rk - q.off;
                 const int v = ln;
                 w = __builtin_ctzll(__ballot(((q.M >> v) & 1ull) && bits_above(q.M, v) == k));
-            } else {
+            }
+            if (tie) {
                 // tie class: the pivot is the set triangle of [cs, ce) with the largest index
 #ifdef TDA_PROFILE
                 ++ties;
 #endif
-                const uint32_t cc = ld_glb(clsg, e), c0 = cc & 0xFFFFu, c1 = cc >> 16;
+                const uint32_t cc = ld_glb(clsg, edge_id(a, b2)), c0 = cc & 0xFFFFu, c1 = cc >> 16;
                 uint32_t best = 0, brk = rk;
                 for (uint32_t base = c0; base < c1; base += 64) {
                     const uint32_t rho = base + ln;
                     uint32_t cand = 0;
                     if (rho < c1 && ((ld_lds(W, rho >> 5) >> (rho & 31)) & 1u)) {
-                        const EdgeRecV q2 = load_rec(R, ld_lds(inv, rho));
-                        cand = tri_id(q2.a, q2.b, kth_highest(q2.M, rho - q2.off)) + 1;
+                        if constexpr (FAST) {
+                            const uint32_t q2 = ld_lds(inv32, rho);
+                            cand = tri_id((int)(q2 & 63u), (int)((q2 >> 6) & 63u), (int)((q2 >> 12) & 63u)) + 1;
+                        } else {
+                            const EdgeRecV q2 = load_rec(R, ld_lds(inv, rho));
+                            cand = tri_id(q2.a, q2.b, kth_highest(q2.M, rho - q2.off)) + 1;
+                        }
                     }
                     const uint32_t m = wave_max_u32(cand);
                     if (m > best) {
@@ -441,13 +546,19 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                     }
                 }
                 rk = brk;
-                e = ld_lds(inv, rk);
                 resw = ld_lds(res, rk >> 5);
-                q = load_rec(R, e);
-                w = kth_highest(q.M, rk - q.off);
+                if constexpr (FAST) {
+                    const uint32_t q = ld_lds(inv32, rk);
+                    a = (int)(q & 63u);
+                    b2 = (int)((q >> 6) & 63u);
+                    w = (int)((q >> 12) & 63u);
+                } else {
+                    const EdgeRecV q = load_rec(R, ld_lds(inv, rk));
+                    a = q.a;
+                    b2 = q.b;
+                    w = kth_highest(q.M, rk - q.off);
+                }
             }
-            const int a = q.a, b2 = q.b;
-            const float pd = q.len;
             const uint32_t tidx = tri_id(a, b2, w);
             TDA_ACC(1, t1);
             TDA_STAMP(t2);
@@ -470,13 +581,14 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 for (int k = 0; k < K; ++k) st_lds(W, (size_t)ln * K + k, ld_lds(W, (size_t)ln * K + k) ^ x[k]);
                 ++nadds;
                 TDA_ACC(4, t2);
-            } else if (q.tie ? ((ld_lds(piv, tidx >> 5) >> (tidx & 31)) & 1u) : rk == q.off) {
+            } else if (tie ? ((ld_lds(piv, tidx >> 5) >> (tidx & 31)) & 1u) : first) {
                 // apparent pair (e, t): add the coboundary of the youngest facet e
-                cob(a, b2, pd);
+                cob(a, b2, FAST ? 0.0f : ld_lds(Dl, (size_t)a * n + b2));
                 ++nadds;
                 TDA_ACC(3, t2);
             } else {
                 // new persistence pair (column, t); R_j = W
+                const float pd = ld_lds(Dl, (size_t)a * n + b2);
                 if (pd > sdm) {
                     if (ln == 0 && ecnt < pcap) store_pair(P, ecnt, sdm, pd, (int64_t)sidx, (int64_t)tidx);
                     ++ecnt;
@@ -496,7 +608,7 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 if (ln == 0) {
                     st_lds(own, nown, (uint16_t)rk);
                     st_lds(res, rk >> 5, resw | (1u << (rk & 31)));
-                    matomic_or<false>(&pivg[tidx >> 5], 1u << (tidx & 31));  // H2 clearing reads this bitmap
+                    matomic_or<false>(&res1[tidx >> 5], 1u << (tidx & 31));  // H2 clearing reads this bitmap
                 }
                 ++nown;
                 TDA_ACC(5, t2);
@@ -524,8 +636,9 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
         st->nskip[1] = nskip;
     }
 }
-// bitmap words per lane supported by k_h1_chain instantiations
+// bitmap words per lane supported by k_h1_chain instantiations (FAST: up to 12)
 constexpr int kChainKs[] = {1, 2, 3, 4, 6, 9, 12, 16, 21};
+constexpr int kChainFastMaxK = 12;
 
 // ---------------------------------------------------------------- H2 phase 1
 // One wave per block; block (l, g) takes the layer's residual H2 columns

@@ -78,9 +78,12 @@ def test_naive_golden_pairs(gpu):
             assert res.n_all_pairs[d] == case["n_all_pairs"][str(d)]
 
 
-def test_sweep48_maxdim2_vs_oracle(gpu, oracle):
+@pytest.mark.parametrize("chain", ["auto", "general"])
+def test_sweep48_maxdim2_vs_oracle(gpu, oracle, monkeypatch, chain):
     """C2/C3 workload (32 layers x 48 points, H0-H2): every pair, its simplex
-    indices, the count and checksum of ALL pairs (incl. zero persistence)."""
+    indices, the count and checksum of ALL pairs (incl. zero persistence).
+    Both H1-chain variants (rank tables / edge records) are checked."""
+    monkeypatch.setenv("TDA_CHAIN", chain)
     X = gpu.synthetic.sweep48(32)
     res = gpu.ripser_batch(X, maxdim=2)
     orc = oracle.rips_batch_f32(X, 2)
