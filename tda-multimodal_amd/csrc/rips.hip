@@ -249,8 +249,8 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
 struct Workspace {
     int device = -1;
     bool init = false;
-    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr, evs = nullptr, evp = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr, evs = nullptr, evp = nullptr, evh = nullptr;
     char* dbuf = nullptr;
     size_t dcap = 0;
     OutPair* hout = nullptr;  // host-mapped
@@ -263,6 +263,7 @@ struct Workspace {
     std::vector<hipEvent_t> stage_ev;  // stage-time events (TDA_FLAG_STAGE_TIMES)
     std::vector<hipEvent_t> stage_ev2; // ... on the side stream
     std::vector<hipEvent_t> stage_ev3; // ... on the third stream
+    std::vector<hipEvent_t> stage_ev4; // ... on the fourth stream
     hipEvent_t evin = nullptr;         // caller's stream -> library stream
     char* hin = nullptr;               // pinned staging of host inputs (stable graph source)
     size_t hin_cap = 0;
@@ -341,6 +342,8 @@ int ws_prepare(Workspace& w, const Plan& p) {
         HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
         HIPC(hipStreamCreateWithFlags(&w.stream2, hipStreamNonBlocking));
         HIPC(hipStreamCreateWithFlags(&w.stream3, hipStreamNonBlocking));
+        HIPC(hipStreamCreateWithFlags(&w.stream4, hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&w.evh, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evs, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evp, hipEventDisableTiming));
         HIPC(hipEventCreate(&w.ev0));
@@ -498,6 +501,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     StageTimer tm{w.stage_ev, s, (a.flags & TDA_FLAG_STAGE_TIMES) != 0, {}};
     StageTimer tm2{w.stage_ev2, w.stream2, tm.on, {}};
     StageTimer tm3{w.stage_ev3, w.stream3, tm.on, {}};
+    StageTimer tm4{w.stage_ev4, w.stream4, tm.on, {}};
     GraphKey gk;
     std::memset(&gk, 0, sizeof(gk));
     gk.L = p.L;
@@ -571,15 +575,18 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(hipGetLastError());
     MARK(input_kind == 0 ? "k_distance" : "k_square_dist");
 
-    // ---- H0 on the side stream: it overlaps the apparent-pair kernels, which
+    // ---- H0 on its own stream: it overlaps the apparent-pair kernels, which
     // do not need the spanning forest (a forest edge is an H0 death, never an
-    // apparent column; k_reduce_all skips forest edges among the residuals).
+    // apparent column; the reductions skip forest edges among the residuals).
+    // The triangle ranks of the dense H1 chain go on a second side stream.
     HIPC(hipEventRecord(w.evf, s));
-    hipStream_t s2 = w.stream2;
+    hipStream_t s2 = w.stream2, s4 = w.stream4;
     HIPC(hipStreamWaitEvent(s2, w.evf, 0));
+    HIPC(hipStreamWaitEvent(s4, w.evf, 0));
     if (int rc = tm2.begin()) return rc;
+    if (int rc = tm4.begin()) return rc;
     if (n <= kSmallN) {
-        hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s2, dist, n, a.thresh, stats,
+        hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s4, dist, n, a.thresh, stats,
                            (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
     } else {
         int T = n <= 256 ? 256 : 1024;
@@ -589,11 +596,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         uint64_t ch = 1;
         while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
         size_t lds = base + ch * 8;
-        hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s2, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
+        hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
                            (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
     }
     HIPC(hipGetLastError());
-    if (int rc = tm2.mark("k_h0")) return rc;
+    if (int rc = tm4.mark("k_h0")) return rc;
+    HIPC(hipEventRecord(w.evh, s4));
     DenseBufs dnb = {};
     if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
         dnb.recs = (EdgeRec*)(B + p.o_recs);
@@ -721,7 +729,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipMemsetAsync(rb.windex, 0, (size_t)L * p.wcap_g * 2 * 8, s));
             HIPC(hipMemsetAsync(rb.wfill, 0, (size_t)L * p.wcap_g / 4 * 4, s));
         }
-        HIPC(hipStreamWaitEvent(s, w.evj, 0));  // join: forest edges (clearing of H1 columns)
+        HIPC(hipStreamWaitEvent(s, w.evh, 0));  // join: forest edges (clearing of H1 columns)
+        HIPC(hipStreamWaitEvent(s, w.evj, 0));  // join: triangle ranks
         const bool p1 = n <= 1024, p2 = n <= 256;
         Pair* pairs1 = (Pair*)(B + p.o_pairs[1]);
         Pair* pairs2 = p.maxdim >= 2 ? (Pair*)(B + p.o_pairs[2]) : pairs1;
@@ -772,6 +781,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipGetLastError());
         if (!p.dense) MARK(p.big ? "k_reduce_big" : "k_reduce_all");
     } else {
+        HIPC(hipStreamWaitEvent(s, w.evh, 0));
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
 
@@ -981,6 +991,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         (void)hipEventElapsedTime(&t, w.stage_ev2[i], w.stage_ev2[i + 1]);
         R->stage_ms.push_back(t);
         R->stage_name.push_back(tm2.names[i]);
+    }
+    for (size_t i = 0; i < tm4.names.size(); ++i) {  // fourth stream: H0
+        float t = 0.0f;
+        (void)hipEventElapsedTime(&t, w.stage_ev4[i], w.stage_ev4[i + 1]);
+        R->stage_ms.push_back(t);
+        R->stage_name.push_back(tm4.names[i]);
     }
     for (size_t i = 0; i < tm3.names.size(); ++i) {  // third stream: H2 phase 1
         float t = 0.0f;

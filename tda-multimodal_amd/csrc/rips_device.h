@@ -35,17 +35,19 @@ __host__ __device__ __forceinline__ uint64_t binom(uint64_t n64, int k) {
     return q4 * (n - 4) + (r4 * (n - 4)) / 5u;
 }
 
-// largest v in [k-1, top] with C(v, k) <= idx
+// largest v in [k-1, top] with C(v, k) <= idx.  The estimate is f32 hardware
+// math (sqrt / exp2-log2 cube root, within a vertex or two of the answer);
+// the integer walks below make the result exact.
 __device__ __forceinline__ int max_vertex(uint64_t idx, int k, int top) {
     if (k == 1) return (int)(idx < (uint64_t)top ? idx : (uint64_t)top);
-    double g;
-    double x = (double)idx;
+    float g;
+    const float x = (float)idx;
     if (k == 2)
-        g = 0.5 * (1.0 + sqrt(1.0 + 8.0 * x));
+        g = 0.5f * (1.0f + __fsqrt_rn(1.0f + 8.0f * x));
     else if (k == 3)
-        g = cbrt(6.0 * x) + 1.0;
+        g = (x > 0.0f ? __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(6.0f * x) * (1.0f / 3.0f)) : 0.0f) + 1.0f;
     else
-        g = sqrt(sqrt(24.0 * x)) + 1.5;
+        g = __fsqrt_rn(__fsqrt_rn(24.0f * x)) + 1.5f;
     int v = (int)g;
     if (v > top) v = top;
     if (v < k - 1) v = k - 1;

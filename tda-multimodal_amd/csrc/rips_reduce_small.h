@@ -296,21 +296,34 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
     uint16_t* inv = db.inv + (size_t)l * db.inv_stride;
     uint32_t* inv32 = db.inv32 + (size_t)l * db.inv_stride;
     uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
-    for (int q = wv; q < nE; q += nw) {
-        const uint64_t key = sk[q];
-        const uint32_t e = (uint32_t)(key >> 12) & 0xFFFFFu;
-        const int a = (int)((key >> 6) & 63u), b = (int)(key & 63u);
-        const uint32_t lb = (uint32_t)(key >> 32);
-        const bool tie = (q > 0 && (uint32_t)(sk[q - 1] >> 32) == lb) || (q + 1 < nE && (uint32_t)(sk[q + 1] >> 32) == lb);
-        const uint64_t M = Ms[q];
-        const uint32_t o = off[q];
-        if (!fast) {
-            const uint32_t c = (uint32_t)__popcll(M);
-            if ((uint32_t)ln < c) inv[o + ln] = (uint16_t)e;
-        } else if (ln < n && ((M >> ln) & 1ull)) {
-            const uint32_t rk = o + bits_above(M, ln);
-            st_glb(inv32, rk, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(rk == o) << 18) | ((uint32_t)tie << 19));
-            st_glb(ro, tri_id(a, b, ln), (uint16_t)rk);
+    for (int q0 = wv; q0 < nE; q0 += 4 * nw) {  // 4 edges in flight per wave
+        uint64_t key[4], M[4], kp[4], kn[4];
+        uint32_t o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int q = q0 + u * nw;
+            const bool in = q < nE;
+            key[u] = in ? sk[q] : 0;
+            M[u] = in ? Ms[q] : 0;
+            o[u] = in ? off[q] : 0;
+            kp[u] = in && q > 0 ? sk[q - 1] : kEmpty64;
+            kn[u] = in && q + 1 < nE ? sk[q + 1] : kEmpty64;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t e = (uint32_t)(key[u] >> 12) & 0xFFFFFu;
+            const int a = (int)((key[u] >> 6) & 63u), b = (int)(key[u] & 63u);
+            const uint32_t lb = (uint32_t)(key[u] >> 32);
+            const bool tie = (uint32_t)(kp[u] >> 32) == lb || (uint32_t)(kn[u] >> 32) == lb;
+            if (!fast) {
+                const uint32_t c = (uint32_t)__popcll(M[u]);
+                if ((uint32_t)ln < c) inv[o[u] + ln] = (uint16_t)e;
+            } else if (ln < n && ((M[u] >> ln) & 1ull)) {
+                const uint32_t rk = o[u] + bits_above(M[u], ln);
+                st_glb(inv32, rk, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(rk == o[u]) << 18) |
+                                      ((uint32_t)tie << 19));
+                st_glb(ro, tri_id(a, b, ln), (uint16_t)rk);
+            }
         }
     }
     if (t == 0) stats[l].ntri = s_tot;
