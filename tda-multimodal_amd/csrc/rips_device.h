@@ -188,27 +188,40 @@ __device__ __forceinline__ void matomic_or(T* p, T v) {
 // lane before the first LDS store (a single wave otherwise serialises one
 // HBM/L2 round trip per 64 elements).
 __device__ __forceinline__ void stage_to_lds(void* dst, const void* src, size_t nbytes, int t, int T) {
+    // native vector type: HIP's uint4 class defeats register promotion and
+    // sends the in-flight array through scratch
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     const size_t n16 = (((uintptr_t)src | (uintptr_t)dst) & 15) ? 0 : nbytes / 16;
-    const uint4* s4 = (const uint4*)src;
-    uint4* d4 = (uint4*)dst;
+    const TDA_GLB v4u* s4 = (const TDA_GLB v4u*)src;
+    TDA_LDS v4u* d4 = (TDA_LDS v4u*)dst;
     size_t e = t;
     for (; e + 7 * (size_t)T < n16; e += 8 * (size_t)T) {
-        uint4 r[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = s4[e + u * (size_t)T];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) d4[e + u * (size_t)T] = r[u];
+        v4u r0 = s4[e], r1 = s4[e + T], r2 = s4[e + 2 * (size_t)T], r3 = s4[e + 3 * (size_t)T];
+        v4u r4 = s4[e + 4 * (size_t)T], r5 = s4[e + 5 * (size_t)T], r6 = s4[e + 6 * (size_t)T], r7 = s4[e + 7 * (size_t)T];
+        d4[e] = r0;
+        d4[e + T] = r1;
+        d4[e + 2 * (size_t)T] = r2;
+        d4[e + 3 * (size_t)T] = r3;
+        d4[e + 4 * (size_t)T] = r4;
+        d4[e + 5 * (size_t)T] = r5;
+        d4[e + 6 * (size_t)T] = r6;
+        d4[e + 7 * (size_t)T] = r7;
     }
     for (; e < n16; e += T) d4[e] = s4[e];
-    const uint32_t* s1 = (const uint32_t*)src;
-    uint32_t* d1 = (uint32_t*)dst;
+    const TDA_GLB uint32_t* s1 = (const TDA_GLB uint32_t*)src;
+    TDA_LDS uint32_t* d1 = (TDA_LDS uint32_t*)dst;
     size_t w = n16 * 4 + t;
     for (; w + 7 * (size_t)T < nbytes / 4; w += 8 * (size_t)T) {
-        uint32_t r[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = s1[w + u * (size_t)T];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) d1[w + u * (size_t)T] = r[u];
+        uint32_t r0 = s1[w], r1 = s1[w + T], r2 = s1[w + 2 * (size_t)T], r3 = s1[w + 3 * (size_t)T];
+        uint32_t r4 = s1[w + 4 * (size_t)T], r5 = s1[w + 5 * (size_t)T], r6 = s1[w + 6 * (size_t)T], r7 = s1[w + 7 * (size_t)T];
+        d1[w] = r0;
+        d1[w + T] = r1;
+        d1[w + 2 * (size_t)T] = r2;
+        d1[w + 3 * (size_t)T] = r3;
+        d1[w + 4 * (size_t)T] = r4;
+        d1[w + 5 * (size_t)T] = r5;
+        d1[w + 6 * (size_t)T] = r6;
+        d1[w + 7 * (size_t)T] = r7;
     }
     for (; w < nbytes / 4; w += T) d1[w] = s1[w];
 }
@@ -254,6 +267,12 @@ __host__ __device__ __forceinline__ uint64_t filt_key(float diam, uint64_t idx) 
 // issues no s_barrier, so waves of one workgroup can run independent loops.
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+// compiler-only ordering of one wave's LDS traffic: LDS instructions of a
+// wave execute in program order, so no wait is needed between steps
+__device__ __forceinline__ void lds_order() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ int lane_id() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }

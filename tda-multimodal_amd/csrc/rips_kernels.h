@@ -581,14 +581,15 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                                                   DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.y;
-    const float* Dl = dist + (size_t)l * n * n;
+    const float* Dg = dist + (size_t)l * n * n;
     const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
+    float* Dsh = (float*)(smem + 16);
     if (DLDS) {  // stage this layer's distance matrix in LDS (N <= 128: <= 64 KB)
-        float* sd = (float*)(smem + 16);
-        stage_to_lds(sd, Dl, sizeof(float) * n * n, threadIdx.x, blockDim.x);
+        stage_to_lds(Dsh, Dg, sizeof(float) * n * n, threadIdx.x, blockDim.x);
         __syncthreads();
-        Dl = sd;
     }
+    // typed distance reads (LDS or HBM, never FLAT)
+    auto dat = [&](size_t i) -> float { return DLDS ? ld_lds(Dsh, i) : ld_glb(Dg, i); };
     LayerStats* st = stats + l;
     const uint32_t* cleared = b.cleared ? b.cleared + (size_t)l * b.cleared_words : nullptr;
     uint32_t* piv = b.pivbits + (size_t)l * b.piv_words;
@@ -600,9 +601,12 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
         int kind = 0;  // 0 skip, 1 apparent, 2 residual (incl. empty coboundary)
         int vs[DIM + 1];
         float sd = 0.0f;
-        if (s < b.ncand && !(cleared && ((cleared[s >> 5] >> (s & 31)) & 1u))) {
+        if (s < b.ncand && !(cleared && ((ld_glb(cleared, s >> 5) >> (s & 31)) & 1u))) {
             decode<DIM>(s, n, vs);
-            sd = simplex_diam<DIM>(Dl, n, vs);
+#pragma unroll
+            for (int i = 0; i <= DIM; ++i)
+#pragma unroll
+                for (int j = i + 1; j <= DIM; ++j) sd = fmaxf(sd, dat((size_t)vs[i] * n + vs[j]));
             if (sd <= r) {
                 // oldest cofacet, vertices descending
                 float bcd = INFINITY;
@@ -613,9 +617,8 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                     for (int i = 0; i <= DIM; ++i) mem |= (vs[i] == v);
                     if (mem) continue;
                     float cd = sd;
-                    const float* row = Dl + (size_t)v * n;
 #pragma unroll
-                    for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, row[vs[i]]);
+                    for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, dat((size_t)v * n + vs[i]));
                     if (cd <= r && cd < bcd) {
                         bcd = cd;
                         bv = v;
@@ -628,7 +631,6 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                     kind = 2;
                     if (bcd == sd) {
                         bool app = true;
-                        const float* row = Dl + (size_t)bv * n;
 #pragma unroll
                         for (int u = 0; u <= DIM; ++u) {
                             if (vs[u] < bv) continue;
@@ -637,17 +639,17 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
 #pragma unroll
                             for (int i = 0; i <= DIM; ++i) {
                                 if (i == u) continue;
-                                fd = fmaxf(fd, row[vs[i]]);
+                                fd = fmaxf(fd, dat((size_t)bv * n + vs[i]));
 #pragma unroll
                                 for (int j = i + 1; j <= DIM; ++j)
-                                    if (j != u) fd = fmaxf(fd, Dl[(size_t)vs[i] * n + vs[j]]);
+                                    if (j != u) fd = fmaxf(fd, dat((size_t)vs[i] * n + vs[j]));
                             }
                             app &= fd < sd;
                         }
                         if (app) {
                             kind = 1;
                             uint64_t tix = cofacet_index<DIM>(vs, bv);
-                            atomicOr(&piv[tix >> 5], 1u << (tix & 31));
+                            matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
                             acc_cs += pair_hash(s, tix);
                             acc_app += 1;
                         }
@@ -666,7 +668,7 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
             if (kind == 2) {
                 uint64_t pos = basepos + lanes_below(m);
                 if (pos < b.rcap)
-                    resid[pos] = col_key(sd, s);
+                    st_glb(resid, pos, col_key(sd, s));
                 else
                     atomicOr(&st->err, ERR_RESID_CAP);
             }

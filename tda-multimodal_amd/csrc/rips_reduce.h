@@ -209,6 +209,35 @@ struct KeySet {
         best = wave_min_u64(b);
         nlive = (uint32_t)wave_sum_u64(nl);
     }
+    // min live key only (wave-uniform)
+    __device__ uint64_t scan_min(int ln) const {
+        const uint32_t c = cnt;
+        uint64_t b = kEmpty64;
+        uint32_t e = 2 * ln;
+        for (; e + 384 + 1 < c; e += 512) {
+            const u64x2 a0 = mld2<LDS>(log, e), a1 = mld2<LDS>(log, e + 128);
+            const u64x2 a2 = mld2<LDS>(log, e + 256), a3 = mld2<LDS>(log, e + 384);
+            uint64_t m0 = a0.x < a0.y ? a0.x : a0.y, m1 = a1.x < a1.y ? a1.x : a1.y;
+            uint64_t m2 = a2.x < a2.y ? a2.x : a2.y, m3 = a3.x < a3.y ? a3.x : a3.y;
+            m0 = m0 < m1 ? m0 : m1;
+            m2 = m2 < m3 ? m2 : m3;
+            m0 = m0 < m2 ? m0 : m2;
+            b = m0 < b ? m0 : b;
+        }
+        for (; e < c; e += 128) {
+            const uint64_t k0 = mld<LDS>(log, e);
+            const uint64_t k1 = e + 1 < c ? mld<LDS>(log, e + 1) : kEmpty64;
+            const uint64_t m = k0 < k1 ? k0 : k1;
+            b = m < b ? m : b;
+        }
+        b = b < kDead ? b : kEmpty64;
+        return wave_min_u64(b);
+    }
+    __device__ uint32_t count_live(int ln) const {
+        uint32_t nl = 0;
+        for (uint32_t e = ln; e < cnt; e += 64) nl += mld<LDS>(log, e) < kDead;
+        return (uint32_t)wave_sum_u64(nl);
+    }
     // write the live keys to out[] (whole wave), returns how many
     template <bool OLDS = false>
     __device__ uint32_t gather_live(int ln, uint64_t* out) const {

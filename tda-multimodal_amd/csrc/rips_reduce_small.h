@@ -494,7 +494,7 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
         int a0, b0;
         edge_verts(sidx, a0, b0);
         cob(a0, b0, sdm);
-        wave_sync();
+        lds_order();
         for (uint64_t step = 0;; ++step) {
             if (step >= step_limit) {
                 if (ln == 0) printf("h1_chain: layer %d column %u step limit\n", l, j);
@@ -627,9 +627,9 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 TDA_ACC(5, t2);
                 break;
             }
-            wave_sync();
+            lds_order();
         }
-        wave_sync();
+        wave_sync();  // R_j stores reach memory before a later owner addition reads them
     }
     if (ln == 0) {
 #ifdef TDA_PROFILE
@@ -764,7 +764,7 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
 #ifdef TDA_PROFILE
             const uint64_t ts0 = clock64();
 #endif
-            W.scan(ln, pk, nlive);
+            pk = W.scan_min(ln);
 #ifdef TDA_PROFILE
             tscan += clock64() - ts0;
 #endif
@@ -775,13 +775,10 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
             if (pk == kEmpty64) break;
             const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
             int t[NV];
-            uint64_t pidx;
             if (PACKED) {
                 Lo::unpack(plo, t);
-                pidx = encode<DIM + 1>(t);
             } else {
-                pidx = plo;
-                decode_wave<DIM + 1>(pidx, n, t, ln);
+                decode_wave<DIM + 1>(plo, n, t, ln);
             }
             // youngest facet f of the pivot t (max diameter, ties -> smallest index)
             float dd[NV][NV];
@@ -825,8 +822,8 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
             const bool app = pd == fd && eq && 63 - __clzll(eq) == tv;
             if (!app) {  // not apparent: phase 1 ends here
                 out_key = pk;
-                out_idx = (uint32_t)pidx;
-                const uint32_t nl = nlive;
+                out_idx = PACKED ? (uint32_t)encode<DIM + 1>(t) : plo;
+                const uint32_t nl = W.count_live(ln);
                 unsigned long long base = 0;
                 if (ln == 0) base = atomicAdd(&sb.p1_used[l], (unsigned long long)nl);
                 base = __shfl(base, 0, 64);
@@ -853,7 +850,7 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
 #endif
             W.toggle_pass(ckey, cok, ln);
             ++adds;
-            wave_sync();
+            lds_order();
 #ifdef TDA_PROFILE
             tcob += clock64() - tc0;
 #endif
