@@ -73,11 +73,13 @@ struct Plan {
     bool fast = false;        // k_h1_chain FAST variant (rank_of + inv32 tables fit LDS)
     uint32_t chain_lds = 0;   // dynamic LDS of k_h1_chain
     uint32_t p1_lds = 0;      // dynamic LDS of k_h2_phase1
+    uint32_t n2p = 0;         // stride of the per-layer edge-class table (N * N rounded up)
+    uint32_t bm_words = 0;    // tetrahedron membership bitmap of k_h2_phase1 (words)
     uint32_t prep_lds = 0;    // dynamic LDS of k_h1_prep
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -172,8 +174,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         const uint64_t fast_lds = pre + al(2ull * p.tri_stride) + al(4ull * p.inv_stride) + tail;
         p.fast = p.dK <= kChainFastMaxK && fast_lds <= (uint64_t)kLdsMax && !getenv_is("TDA_CHAIN", "general");
         p.chain_lds = (uint32_t)(p.fast ? fast_lds : pre + al(16 * E) + al(2ull * p.inv_stride) + tail);
-        const uint64_t w = kP1WCap;
-        p.p1_lds = (uint32_t)(pre + al(8 * w) + al(16 * w) + al(4 * (2 * w / 8)) + al(16 * w));
+        p.n2p = (uint32_t)align_up(N * N, 8);
+        p.bm_words = (uint32_t)((binom(N, 4) + 31) / 32 + 1);
+        p.p1_lds = (uint32_t)(pre + al(2ull * p.n2p) + al(4ull * p.bm_words) + 2 * al(4ull * kP1LogCap));
         p.prep_lds = (uint32_t)(pre + 2048ull * 20);
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
@@ -218,6 +221,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
         if (p.dense) {
             p.o_recs = take(L * binom(N, 2) * 16);
+            p.o_cls2 = take(L * (uint64_t)p.n2p * 2);
             p.o_cls = take(L * binom(N, 2) * 4);
             p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
             if (p.fast) {
@@ -410,7 +414,7 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, true, false);
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
-    HIPC(hipFuncSetAttribute((const void*)k_h2_phase1<true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
 #define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     TDA_ATTR_CHAIN(1, false) TDA_ATTR_CHAIN(2, false) TDA_ATTR_CHAIN(3, false) TDA_ATTR_CHAIN(4, false) TDA_ATTR_CHAIN(6, false)
     TDA_ATTR_CHAIN(9, false) TDA_ATTR_CHAIN(12, false) TDA_ATTR_CHAIN(16, false) TDA_ATTR_CHAIN(21, false)
@@ -610,6 +614,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         dnb.inv32 = (uint32_t*)(B + p.o_inv32);
         dnb.rank_of = (uint16_t*)(B + p.o_rof);
         dnb.tri_stride = p.tri_stride;
+        dnb.cls2 = (uint16_t*)(B + p.o_cls2);
+        dnb.n2p = p.n2p;
         dnb.inv = (uint16_t*)(B + p.o_inv);
         dnb.E = (uint32_t)binom((uint64_t)n, 2);
         dnb.inv_stride = p.inv_stride;
@@ -707,7 +713,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             launch_sort(2, 1, w.stream3);
             HIPC(hipGetLastError());
             if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
-            hipLaunchKernelGGL(k_h2_phase1<true>, dim3(L, kP1Grid), dim3(64), p.p1_lds, w.stream3, dist, n, stats, db[2], sb,
+            HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));  // edge classes (k_h1_prep)
+            hipLaunchKernelGGL(k_h2_phase1, dim3(L, kP1Grid), dim3(64), p.p1_lds, w.stream3, dist, n, stats, db[2], sb,
+                               (const uint16_t*)dnb.cls2, p.n2p, p.bm_words, (const uint32_t*)dnb.res1, (uint32_t)p.piv_words[1],
                                step_limit());
             HIPC(hipGetLastError());
             if (int rc = tm3.mark("k_h2_phase1")) return rc;

@@ -110,6 +110,8 @@ struct DenseBufs {
     uint32_t* inv32;    // [L][inv_stride] rank -> a | b << 6 | w << 12 | first << 18 | tie << 19 (FAST path)
     uint16_t* rank_of;  // [L][tri_stride] triangle colex index -> rank, 0xFFFF above thresh (FAST path)
     uint32_t tri_stride;
+    uint16_t* cls2;     // [L][n2p] length-class rank of edge (u, v) at u * n + v; 0xFFFF above thresh (H2 phase 1)
+    uint32_t n2p;
     uint32_t* res1;     // [L][piv_words1] colex bitmap of residual H1 pivots (H2 clearing; zeroed per call)
     uint32_t E, inv_stride;
     int K;              // bitmap words per lane (W = 64 K words)
@@ -279,6 +281,9 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
         rec.len = __uint_as_float(lb);
         R[e] = rec;
         db.cls[(size_t)l * db.E + e] = off[q0] | ((off[q1] + (uint32_t)__popcll(Ms[q1])) << 16);
+        uint16_t* c2 = db.cls2 + (size_t)l * db.n2p;
+        st_glb(c2, (size_t)a * n + b, (uint16_t)q0);
+        st_glb(c2, (size_t)b * n + a, (uint16_t)q0);
     }
     for (int e = t; e < E; e += T) {  // edges above the threshold own no triangles
         int a, b;
@@ -289,6 +294,9 @@ __global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist
             rec.ab = (uint16_t)(a | (b << 6));
             rec.len = d;
             R[e] = rec;
+            uint16_t* c2 = db.cls2 + (size_t)l * db.n2p;
+            st_glb(c2, (size_t)a * n + b, (uint16_t)0xFFFFu);
+            st_glb(c2, (size_t)b * n + a, (uint16_t)0xFFFFu);
         }
     }
     __syncthreads();
@@ -655,90 +663,147 @@ constexpr int kChainFastMaxK = 12;
 
 // ---------------------------------------------------------------- H2 phase 1
 // One wave per block; block (l, g) takes the layer's residual H2 columns
-// g, g + kP1Grid, ... and reduces each with apparent columns only, in an LDS
-// toggle-set.  Thousands of independent columns fill the chip while the H1
-// chains run.  LDS: [16][D][log][index][fill][tmp].
-template <bool PACKED>
+// g, g + gridDim.y, ... and reduces each with apparent columns only.  The
+// whole step runs on 32-bit words:
+//   * a tetrahedron's key is (class << 20) | (2^20 - 1 - colex index), where
+//     class = rank of its longest edge's length among the sorted edges
+//     (cls2, k_h1_prep): key order is Ripser's (diameter asc, index desc);
+//   * membership is a bitmap over tetrahedron indices (a toggle is one
+//     returning ds_xor), the keys live in an append-only log (+ packed
+//     vertices) whose dead entries are dropped lazily by the bitmap test;
+//   * apparency is tested on the fly from the classes the coboundary step
+//     loads anyway (apparent pairs form a matching [upstream ripser.cpp
+//     get_zero_apparent_facet], so this equals k_apparent's bitmap).
+// Results go out in the u64 key format of the serial phase 2.
+// LDS: [16][D][cls2][bitmap][log][log vertices].
+constexpr uint32_t kP1LogCap = 1024;
+// Phase-1 additions per column before handing the column to the serial phase
+// 2.  The long phase-1 chains are H2 columns that turn out to be H1 deaths
+// (cleared once the H1 chain pairs them); the kept columns of the 32-layer
+// sweep need <= 44 additions in all.
+constexpr uint32_t kP1MaxAdds = 32;
+constexpr uint32_t kClsInvalid = 0xFFFFu;
+
+__device__ __forceinline__ uint32_t c4u(uint32_t x) { return x < 4 ? 0u : x * (x - 1) * (x - 2) / 6 * (x - 3) / 4; }
+__device__ __forceinline__ uint32_t c3s(uint32_t x) { return x < 3 ? 0u : x * (x - 1) * (x - 2) / 6; }
+__device__ __forceinline__ uint32_t c2s(uint32_t x) { return x < 2 ? 0u : x * (x - 1) / 2; }
+
 __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats, DimBufs b,
-                                                  SmallBufs sb, uint64_t step_limit) {
+                                                  SmallBufs sb, const uint16_t* __restrict__ cls2g, uint32_t n2p, uint32_t bm_words,
+                                                  const uint32_t* __restrict__ res1g, uint32_t res1_words, uint64_t step_limit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int DIM = 2, NV = 4;
-    using Lo = RowLo<NV>;
     const int l = blockIdx.x, ln = threadIdx.x;
     LayerStats* st = stats + l;
     uint64_t nres = (uint64_t)st->n_residual[2];
     if (nres > b.rcap) nres = b.rcap;
     if (blockIdx.y >= nres) return;
-    const float r = st->thresh;
     const uint64_t* resid = b.resid + (size_t)l * b.rcap;
-    const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
-    float* Dl = (float*)(smem + 16);
-    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, ln, 64);
-
-    const uint32_t wcap = sb.p1_wcap;
-    unsigned char* p = smem + 16 + ((4ull * n * n + 15) & ~15ull);
+    unsigned char* p = smem + 16;
     auto take = [&](size_t bytes) {
         unsigned char* q = p;
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
-    KeySet<true, true> W;
-    W.log = (uint64_t*)take(8ull * wcap);
-    W.index = (uint64_t*)take(16ull * wcap);
-    W.fill = (uint32_t*)take(4ull * (2 * wcap / 8));
-    W.tmp = (uint64_t*)take(8ull * 2 * wcap);
-    W.imask = 2 * wcap - 1;
-    W.cnt = 0;
-    for (uint32_t e = ln; e <= W.imask; e += 64) st_lds(W.index, e, (uint64_t)0);
-    for (uint32_t e = ln; e <= (W.imask >> 3); e += 64) st_lds(W.fill, e, 0u);
+    float* Dl = (float*)take(4ull * n * n);
+    uint16_t* cls = (uint16_t*)take(2ull * n2p);
+    uint32_t* bm = (uint32_t*)take(4ull * bm_words);
+    uint32_t* lk = (uint32_t*)take(4ull * kP1LogCap);
+    uint32_t* lv = (uint32_t*)take(4ull * kP1LogCap);
+    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, ln, 64);
+    stage_to_lds(cls, cls2g + (size_t)l * n2p, 2ull * n2p, ln, 64);
+    for (uint32_t i = ln; i < bm_words; i += 64) st_lds(bm, i, 0u);
     wave_sync();
-    const uint32_t wlim = (wcap >> 1) + (wcap >> 2);
 
     uint64_t* p1k = sb.p1_key + (size_t)l * b.rcap;
     uint32_t* p1i = sb.p1_info + (size_t)l * b.rcap;
     uint64_t* roff = sb.roff2 + (size_t)l * b.rcap;
     uint32_t* rlen = sb.rlen2 + (size_t)l * b.rcap;
+    auto C = [&](int u, int v) -> uint32_t { return ld_lds(cls, (size_t)u * n + v); };
+    uint32_t cnt = 0;  // log length (wave-uniform)
 
-    // coboundary entry of lane v: key, validity; returns the ballot of lanes
-    // whose cofacet has diameter sd (the oldest cofacet is its highest lane)
-    auto cob_key = [&](const int (&vs)[DIM + 1], float sd, uint64_t& key, bool& ok) -> uint64_t {
+    // coboundary of facet f (f0 > f1 > f2, class fc) in lane v: key, vertices;
+    // toggles it into the bitmap and appends new entries; returns the ballot
+    // of lanes whose cofacet has class fc (apparent test)
+    auto cob_entry = [&](int f0, int f1, int f2, uint32_t fc, uint32_t& key, uint32_t& pk, bool& ok) -> uint64_t {
         const int v = ln;
-        ok = v < n;
-#pragma unroll
-        for (int i = 0; i <= DIM; ++i) ok &= (vs[i] != v);
-        float cd = sd;
-        key = 0;
+        ok = v < n && v != f0 && v != f1 && v != f2;
+        uint32_t cc = kClsInvalid;
         if (ok) {
-#pragma unroll
-            for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, ld_lds(Dl, (size_t)vs[i] * n + v));
-            ok = cd <= r;
-            uint32_t lo;
-            if (PACKED) {
-                int t[NV];
-                int q = 0;
-                bool placed = false;
-#pragma unroll
-                for (int i = 0; i <= DIM; ++i) {
-                    if (!placed && v > vs[i]) {
-                        t[q++] = v;
-                        placed = true;
-                    }
-                    t[q++] = vs[i];
-                }
-                if (!placed) t[NV - 1] = v;
-                lo = Lo::pack(t);
-            } else {
-                lo = (uint32_t)cofacet_index<DIM>(vs, v);
-            }
-            key = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | (0xFFFFFFFFu - lo);
+            const uint32_t a0 = C(v, f0), a1 = C(v, f1), a2 = C(v, f2);
+            cc = max(fc, max(a0, max(a1, a2)));
+            ok = cc != kClsInvalid;
         }
-        return __ballot(ok && cd == sd);
+        const int x0 = max(v, f0), x1 = v > f0 ? f0 : max(v, f1), x2 = v > f1 ? f1 : max(v, f2), x3 = v > f2 ? f2 : v;
+        const uint32_t tidx = c4u(x0) + c3s(x1) + c2s(x2) + (uint32_t)x3;
+        key = (cc << 20) | (0xFFFFFu - tidx);
+        pk = (uint32_t)x0 | ((uint32_t)x1 << 6) | ((uint32_t)x2 << 12) | ((uint32_t)x3 << 18);
+        return __ballot(ok && cc == fc);
     };
-    auto cob = [&](const int (&vs)[DIM + 1], float sd) {
-        uint64_t key;
-        bool ok;
-        (void)cob_key(vs, sd, key, ok);
-        W.toggle_pass(key, ok, ln);
+    auto toggle = [&](uint32_t key, uint32_t pk, bool ok) {
+        bool ins = false;
+        if (ok) {
+            const uint32_t tidx = 0xFFFFFu - (key & 0xFFFFFu), bit = 1u << (tidx & 31);
+            const uint32_t old = __hip_atomic_fetch_xor((TDA_LDS uint32_t*)bm + (tidx >> 5), bit, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            ins = !(old & bit);
+        }
+        const uint64_t m = __ballot(ins);
+        if (ins) {
+            const uint32_t pos = cnt + lanes_below(m);
+            st_lds(lk, pos, key);
+            st_lds(lv, pos, pk);
+        }
+        cnt += (uint32_t)__popcll(m);
+    };
+    auto live = [&](uint32_t key) -> bool {
+        const uint32_t tidx = 0xFFFFFu - (key & 0xFFFFFu);
+        return (ld_lds(bm, tidx >> 5) >> (tidx & 31)) & 1u;
+    };
+    // rewrite the log with one entry per live key (in place, order kept);
+    // `emit` sees every kept (key, vertices); returns the new length
+    auto compact = [&](auto&& emit) -> uint32_t {
+        uint32_t pos = 0;
+        for (uint32_t e0 = 0; e0 < cnt; e0 += 64) {
+            const uint32_t e = e0 + ln;
+            uint32_t key = 0, pk = 0;
+            bool keep = false;
+            if (e < cnt) {
+                key = ld_lds(lk, e);
+                pk = ld_lds(lv, e);
+                const uint32_t tidx = 0xFFFFFu - (key & 0xFFFFFu), bit = 1u << (tidx & 31);
+                // first lane to clear a live bit keeps the key (duplicates drop)
+                const uint32_t old = __hip_atomic_fetch_and((TDA_LDS uint32_t*)bm + (tidx >> 5), ~bit, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+                keep = old & bit;
+            }
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const uint32_t q = pos + lanes_below(m);
+                st_lds(lk, q, key);
+                st_lds(lv, q, pk);
+                emit(q, key, pk);
+            }
+            pos += (uint32_t)__popcll(m);
+        }
+        // restore the bits of the kept keys
+        for (uint32_t e = ln; e < pos; e += 64) {
+            const uint32_t tidx = 0xFFFFFu - (ld_lds(lk, e) & 0xFFFFFu);
+            __hip_atomic_fetch_or((TDA_LDS uint32_t*)bm + (tidx >> 5), 1u << (tidx & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        lds_order();
+        return pos;
+    };
+    // packed vertices (6 bits each, descending) -> phase-2 key / diameter
+    auto diam_of = [&](uint32_t pk) -> float {
+        const int x0 = pk & 63, x1 = (pk >> 6) & 63, x2 = (pk >> 12) & 63, x3 = (pk >> 18) & 63;
+        const float* r0 = Dl + (size_t)x0 * n;
+        const float* r1 = Dl + (size_t)x1 * n;
+        float d = fmaxf(fmaxf(ld_lds(r0, x1), ld_lds(r0, x2)), fmaxf(ld_lds(r0, x3), ld_lds(r1, x2)));
+        return fmaxf(d, fmaxf(ld_lds(r1, x3), ld_lds(Dl, (size_t)x2 * n + x3)));
+    };
+    auto key64 = [&](uint32_t pk) -> uint64_t {
+        const uint32_t p8 = (pk & 63) << 24 | ((pk >> 6) & 63) << 16 | ((pk >> 12) & 63) << 8 | ((pk >> 18) & 63);
+        return ((uint64_t)__float_as_uint(diam_of(pk) + 0.0f) << 32) | (0xFFFFFFFFu - p8);
     };
 
 #ifdef TDA_PROFILE
@@ -747,113 +812,109 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
     for (uint64_t j = blockIdx.y; j < nres; j += gridDim.y) {
 #ifdef TDA_PROFILE
         const uint64_t tcol = clock64();
-        uint64_t tscan = 0, tcob = 0;
 #endif
         const uint64_t key = ld_glb(resid, j);
         const uint64_t sidx = key_idx(key);
-        const float sdm = key_diam(key);
-        int vs[DIM + 1];
-        decode_wave<DIM>(sidx, n, vs, ln);
-        cob(vs, sdm);
-        wave_sync();
+        // an H1 death found by the concurrent H1 chain is cleared: no phase 1
+        const TDA_GLB uint32_t* res1 = (const TDA_GLB uint32_t*)(res1g + (size_t)l * res1_words);
+        auto cleared = [&]() -> bool {
+            return (__hip_atomic_load(res1 + (sidx >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (sidx & 31)) & 1u;
+        };
+        if (cleared()) {
+            if (ln == 0) {
+                st_glb(p1k, j, kEmpty64);
+                st_glb(p1i, j, kP1Overflow);
+            }
+            continue;
+        }
+        int vs[3];
+        decode_wave<2>(sidx, n, vs, ln);
+        const uint32_t scls = max(C(vs[0], vs[1]), max(C(vs[0], vs[2]), C(vs[1], vs[2])));
+        {
+            uint32_t k, pk;
+            bool ok;
+            (void)cob_entry(vs[0], vs[1], vs[2], scls, k, pk, ok);
+            toggle(k, pk, ok);
+        }
+        lds_order();
         uint32_t adds = 0, flags = 0, out_idx = 0;
         uint64_t out_key = kEmpty64;
         for (uint64_t step = 0;; ++step) {
-            uint64_t pk;
-            uint32_t nlive;
-#ifdef TDA_PROFILE
-            const uint64_t ts0 = clock64();
-#endif
-            pk = W.scan_min(ln);
-#ifdef TDA_PROFILE
-            tscan += clock64() - ts0;
-#endif
-            if (step >= step_limit) {
-                flags = kP1Overflow;  // phase 2 redoes it from scratch (and enforces the limit)
+            if (step >= step_limit || adds >= kP1MaxAdds || ((step & 7) == 7 && cleared())) {
+                flags = kP1Overflow;  // phase 2 skips it if cleared, else redoes it serially
                 break;
             }
-            if (pk == kEmpty64) break;
-            const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
-            int t[NV];
-            if (PACKED) {
-                Lo::unpack(plo, t);
-            } else {
-                decode_wave<DIM + 1>(plo, n, t, ln);
-            }
-            // youngest facet f of the pivot t (max diameter, ties -> smallest index)
-            float dd[NV][NV];
+            // pivot: smallest live key (with its log position)
+            uint32_t bk = 0xFFFFFFFFu, bp = 0;
+            for (uint32_t e0 = 0; e0 < cnt; e0 += 256) {
+                uint32_t k4[4];
 #pragma unroll
-            for (int i = 0; i < NV; ++i)
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t e = e0 + (uint32_t)u * 64 + ln;
+                    k4[u] = e < cnt ? ld_lds(lk, e) : 0xFFFFFFFFu;
+                }
 #pragma unroll
-                for (int k = i + 1; k < NV; ++k) dd[i][k] = ld_lds(Dl, (size_t)t[i] * n + t[k]);
-            float fd = -1.0f;
-            int fu = 0;
-#pragma unroll
-            for (int u = 0; u < NV; ++u) {
-                float d = 0.0f;
-#pragma unroll
-                for (int i = 0; i < NV; ++i)
-#pragma unroll
-                    for (int k = i + 1; k < NV; ++k)
-                        if (i != u && k != u) d = fmaxf(d, dd[i][k]);
-                if (d > fd) {
-                    fd = d;
-                    fu = u;
+                for (int u = 0; u < 4; ++u) {
+                    const bool lv4 = k4[u] != 0xFFFFFFFFu && live(k4[u]);
+                    if (lv4 && k4[u] < bk) {
+                        bk = k4[u];
+                        bp = e0 + (uint32_t)u * 64 + ln;
+                    }
                 }
             }
-            int fv[DIM + 1];
-            int tv = t[0];
-#pragma unroll
-            for (int u = 0; u < NV; ++u) {
-                if (u != fu) continue;
-                tv = t[u];
-#pragma unroll
-                for (int i = 0, q = 0; i < NV; ++i)
-                    if (i != u) fv[q++] = t[i];
-            }
-            // (f, t) is an apparent pair iff diam t == diam f and t is the
-            // oldest cofacet of f: the highest vertex v with diam(f u v) ==
-            // diam f.  Apparent pairs form a matching [upstream ripser.cpp
-            // get_zero_apparent_facet], so this equals k_apparent's bitmap.
-            uint64_t ckey;
+            const uint32_t pk32 = wave_min_u32(bk);
+            if (pk32 == 0xFFFFFFFFu) break;  // zero column: essential
+            const int src = __builtin_ctzll(__ballot(bk == pk32));
+            const uint32_t tpk = ld_lds(lv, (uint32_t)__builtin_amdgcn_readlane((int)bp, src));
+            const uint32_t tcls = pk32 >> 20;
+            int t[4] = {(int)(tpk & 63), (int)((tpk >> 6) & 63), (int)((tpk >> 12) & 63), (int)((tpk >> 18) & 63)};
+            // youngest facet f of t: largest class, ties -> drop the larger vertex
+            const uint32_t c01 = C(t[0], t[1]), c02 = C(t[0], t[2]), c03 = C(t[0], t[3]);
+            const uint32_t c12 = C(t[1], t[2]), c13 = C(t[1], t[3]), c23 = C(t[2], t[3]);
+            const uint32_t fc0 = max(c12, max(c13, c23)), fc1 = max(c02, max(c03, c23));
+            const uint32_t fc2 = max(c01, max(c03, c13)), fc3 = max(c01, max(c02, c12));
+            int fu = 0;
+            uint32_t fc = fc0;
+            if (fc1 > fc) { fc = fc1; fu = 1; }
+            if (fc2 > fc) { fc = fc2; fu = 2; }
+            if (fc3 > fc) { fc = fc3; fu = 3; }
+            const int f0 = fu == 0 ? t[1] : t[0];
+            const int f1 = fu <= 1 ? t[2] : t[1];
+            const int f2 = fu <= 2 ? t[3] : t[2];
+            const int tv = fu == 0 ? t[0] : fu == 1 ? t[1] : fu == 2 ? t[2] : t[3];
+            uint32_t ck, cpk;
             bool cok;
-            const uint64_t eq = cob_key(fv, fd, ckey, cok);
-            const float pd = __uint_as_float((uint32_t)(pk >> 32));
-            const bool app = pd == fd && eq && 63 - __clzll(eq) == tv;
+            const uint64_t eq = cob_entry(f0, f1, f2, fc, ck, cpk, cok);
+            const bool app = tcls == fc && eq && 63 - __clzll(eq) == tv;
             if (!app) {  // not apparent: phase 1 ends here
-                out_key = pk;
-                out_idx = PACKED ? (uint32_t)encode<DIM + 1>(t) : plo;
-                const uint32_t nl = W.count_live(ln);
+                out_key = key64(tpk);
+                out_idx = 0xFFFFFu - (pk32 & 0xFFFFFu);
                 unsigned long long base = 0;
-                if (ln == 0) base = atomicAdd(&sb.p1_used[l], (unsigned long long)nl);
+                if (ln == 0) base = atomicAdd(&sb.p1_used[l], (unsigned long long)cnt);
                 base = __shfl(base, 0, 64);
-                if (base + nl > sb.rpool2_cap) {
+                if (base + cnt > sb.rpool2_cap) {
                     flags = kP1Overflow;
                     break;
                 }
-                const uint32_t wr = W.template gather_live<false>(ln, sb.rpool2 + (size_t)l * sb.rpool2_cap + base);
+                uint64_t* out = sb.rpool2 + (size_t)l * sb.rpool2_cap + base;
+                const uint32_t wr = compact([&](uint32_t q, uint32_t, uint32_t pk) { st_glb(out, q, key64(pk)); });
+                cnt = wr;
                 if (ln == 0) {
                     st_glb(roff, j, (uint64_t)base);
                     st_glb(rlen, j, wr);
                 }
                 break;
             }
-            if (W.cnt + (uint32_t)n > wlim) {
-                W.compact(ln);
-                if (W.cnt + (uint32_t)n > wlim) {
+            toggle(ck, cpk, cok);
+            ++adds;
+            if (cnt + 64 > kP1LogCap) {
+                cnt = compact([](uint32_t, uint32_t, uint32_t) {});
+                if (cnt + 64 > kP1LogCap) {
                     flags = kP1Overflow;
                     break;
                 }
             }
-#ifdef TDA_PROFILE
-            const uint64_t tc0 = clock64();
-#endif
-            W.toggle_pass(ckey, cok, ln);
-            ++adds;
             lds_order();
-#ifdef TDA_PROFILE
-            tcob += clock64() - tc0;
-#endif
         }
         if (ln == 0) {
             st_glb(p1k, j, out_key);
@@ -863,14 +924,14 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
             const uint64_t tt = clock64() - tcol;
             atomicMax((unsigned long long*)&st->prof[1][2], (unsigned long long)tt);
             atomicMax((unsigned long long*)&st->prof[1][3], (unsigned long long)((tt << 16) | (adds & 0xFFFF)));
-            atomicAdd((unsigned long long*)&st->prof[1][4], (unsigned long long)tscan);
-            atomicAdd((unsigned long long*)&st->prof[1][5], (unsigned long long)tcob);
             atomicAdd((unsigned long long*)&st->prof[1][6], (unsigned long long)tt);
             atomicAdd((unsigned long long*)&st->prof[1][7], (unsigned long long)adds);
 #endif
         }
+        // clear the bitmap words this column touched
+        for (uint32_t e = ln; e < cnt; e += 64) st_lds(bm, (0xFFFFFu - (ld_lds(lk, e) & 0xFFFFFu)) >> 5, 0u);
+        cnt = 0;
         wave_sync();
-        W.reset(ln);
     }
 #ifdef TDA_PROFILE
     if (ln == 0) atomicMax((unsigned long long*)&st->prof[1][0], (unsigned long long)(clock64() - t_p1));
