@@ -66,20 +66,21 @@ struct Plan {
     bool lds_mode = false;
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
     bool dense = false;  // N <= 64: dense-bitmap H1 chain + column-parallel H2 phase 1 (rips_reduce_small.h)
-    int E2 = 0;          // edge count rounded up to a power of two (k_h1_prep sort)
     int dK = 0;          // dense H1 bitmap words per lane (a k_h1_chain instantiation)
     uint32_t inv_stride = 0;  // rank -> edge table stride (C(N,3) rounded up)
     uint32_t tri_stride = 0;  // triangle -> rank table stride (C(N,3) rounded up)
-    bool fast = false;        // k_h1_chain FAST variant (rank_of + inv32 tables fit LDS)
+    bool fast = false;        // rank_of + inv32 tables exist (k_h1_chain FAST / TABLE)
+    int cmode = 0;            // k_h1_chain MODE: kChainGeneral / kChainFast / kChainTable
+    uint32_t cob_stride = 0;  // per-layer coboundary table (TABLE): E * N rounded up
     uint32_t chain_lds = 0;   // dynamic LDS of k_h1_chain
     uint32_t p1_lds = 0;      // dynamic LDS of k_h2_phase1
     uint32_t n2p = 0;         // stride of the per-layer edge-class table (N * N rounded up)
     uint32_t bm_words = 0;    // tetrahedron membership bitmap of k_h2_phase1 (words)
-    uint32_t prep_lds = 0;    // dynamic LDS of k_h1_prep
+    uint32_t prep_lds = 0;    // dynamic LDS of k_prep_edges
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_epos = 0, o_cobt = 0, o_eqq = 0, o_eM = 0, o_cpos = 0, o_necnt = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -156,8 +157,6 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
     }
     if (p.dense) {  // carve of rips_reduce_small.h (h1_chain / h2_phase1), mirrored here
         const uint64_t E = binom(N, 2), T3 = binom(N, 3);
-        p.E2 = 1;
-        while ((uint64_t)p.E2 < E) p.E2 <<= 1;
         const int kneed = (int)std::max<uint64_t>(1, (((T3 + 31) / 32) + 63) / 64);
         p.dK = 0;
         for (int k : kChainKs)
@@ -172,12 +171,26 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         p.tri_stride = (uint32_t)align_up(T3, 8);
         const uint64_t tail = 2 * al(4 * WP) + al(4 * p.piv_words[1]) + al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols);
         const uint64_t fast_lds = pre + al(2ull * p.tri_stride) + al(4ull * p.inv_stride) + tail;
-        p.fast = p.dK <= kChainFastMaxK && fast_lds <= (uint64_t)kLdsMax && !getenv_is("TDA_CHAIN", "general");
-        p.chain_lds = (uint32_t)(p.fast ? fast_lds : pre + al(16 * E) + al(2ull * p.inv_stride) + tail);
+        p.cob_stride = (uint32_t)align_up(E * N, 8);
+        const uint64_t table_lds = 16 + al(2ull * p.cob_stride) + al(2ull * p.inv_stride) + al(4 * WP) + al(4 * p.piv_words[1]) +
+                                   al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols);
+        // TDA_CHAIN=general|fast forces a slower variant (tests)
+        const bool want_gen = getenv_is("TDA_CHAIN", "general"), want_fast = getenv_is("TDA_CHAIN", "fast");
+        p.cmode = kChainGeneral;
+        if (!want_gen && p.dK <= kChainFastMaxK) {
+            if (!want_fast && table_lds <= (uint64_t)kLdsMax)
+                p.cmode = kChainTable;
+            else if (fast_lds <= (uint64_t)kLdsMax)
+                p.cmode = kChainFast;
+        }
+        p.fast = p.cmode != kChainGeneral;
+        p.chain_lds = (uint32_t)(p.cmode == kChainTable  ? table_lds
+                                 : p.cmode == kChainFast ? fast_lds
+                                                         : pre + al(16 * E) + al(2ull * p.inv_stride) + tail);
         p.n2p = (uint32_t)align_up(N * N, 8);
         p.bm_words = (uint32_t)((binom(N, 4) + 31) / 32 + 1);
         p.p1_lds = (uint32_t)(pre + al(2ull * p.n2p) + al(4ull * p.bm_words) + 2 * al(4ull * kP1LogCap));
-        p.prep_lds = (uint32_t)(pre + 2048ull * 20);
+        p.prep_lds = (uint32_t)(pre + al(4 * E) + 4 * 3 * 64 * 4 + 64 * 4);
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
     }
@@ -201,7 +214,10 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
     p.o_rowmax = take(L * N * 4);
     p.o_p1used = take(L * 8);
     p.o_p1next = take(L * 4);
-    if (p.dense) p.o_res1 = take(L * p.piv_words[1] * 4);
+    if (p.dense) {
+        p.o_res1 = take(L * p.piv_words[1] * 4);
+        p.o_necnt = take(L * 4);
+    }
     p.memset_hi = o;
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
     p.o_tmp = take(L * 2 * p.max_rcap * 8);
@@ -224,10 +240,15 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
             p.o_cls2 = take(L * (uint64_t)p.n2p * 2);
             p.o_cls = take(L * binom(N, 2) * 4);
             p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
+            p.o_epos = take(L * binom(N, 2) * 4);
+            p.o_eqq = take(L * binom(N, 2) * 4);
+            p.o_eM = take(L * binom(N, 2) * 8);
+            p.o_cpos = take(L * (binom(N, 2) + 8) * 4);
             if (p.fast) {
                 p.o_inv32 = take(L * (uint64_t)p.inv_stride * 4);
                 p.o_rof = take(L * (uint64_t)p.tri_stride * 2);
             }
+            if (p.cmode == kChainTable) p.o_cobt = take(L * (uint64_t)p.cob_stride * 2);
             if (p.maxdim >= 2) {
                 p.o_p1k = take(L * p.rcap[2] * 8);
                 p.o_p1i = take(L * p.rcap[2] * 4);
@@ -416,12 +437,14 @@ int set_lds_attrs(int dev) {
 #undef TDA_ATTR_RED
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
 #define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    TDA_ATTR_CHAIN(1, false) TDA_ATTR_CHAIN(2, false) TDA_ATTR_CHAIN(3, false) TDA_ATTR_CHAIN(4, false) TDA_ATTR_CHAIN(6, false)
-    TDA_ATTR_CHAIN(9, false) TDA_ATTR_CHAIN(12, false) TDA_ATTR_CHAIN(16, false) TDA_ATTR_CHAIN(21, false)
-    TDA_ATTR_CHAIN(1, true) TDA_ATTR_CHAIN(2, true) TDA_ATTR_CHAIN(3, true) TDA_ATTR_CHAIN(4, true) TDA_ATTR_CHAIN(6, true)
-    TDA_ATTR_CHAIN(9, true) TDA_ATTR_CHAIN(12, true)
+    TDA_ATTR_CHAIN(1, 0) TDA_ATTR_CHAIN(2, 0) TDA_ATTR_CHAIN(3, 0) TDA_ATTR_CHAIN(4, 0) TDA_ATTR_CHAIN(6, 0)
+    TDA_ATTR_CHAIN(9, 0) TDA_ATTR_CHAIN(12, 0) TDA_ATTR_CHAIN(16, 0) TDA_ATTR_CHAIN(21, 0)
+    TDA_ATTR_CHAIN(1, 1) TDA_ATTR_CHAIN(2, 1) TDA_ATTR_CHAIN(3, 1) TDA_ATTR_CHAIN(4, 1) TDA_ATTR_CHAIN(6, 1)
+    TDA_ATTR_CHAIN(9, 1) TDA_ATTR_CHAIN(12, 1)
+    TDA_ATTR_CHAIN(1, 2) TDA_ATTR_CHAIN(2, 2) TDA_ATTR_CHAIN(3, 2) TDA_ATTR_CHAIN(4, 2) TDA_ATTR_CHAIN(6, 2)
+    TDA_ATTR_CHAIN(9, 2) TDA_ATTR_CHAIN(12, 2)
 #undef TDA_ATTR_CHAIN
-    HIPC(hipFuncSetAttribute((const void*)k_h1_prep, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_prep_edges, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -519,7 +542,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.force_global = force_global;
     gk.scale = scale;
     gk.force_big = force_big;
-    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0);
+    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4);
     gk.thresh = a.thresh;
     gk.x = xsrc;
     gk.gen = w.gen;
@@ -578,53 +601,77 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     HIPC(hipGetLastError());
     MARK(input_kind == 0 ? "k_distance" : "k_square_dist");
+    HIPC(hipEventRecord(w.evf, s));  // fork point of the side streams
+
+    DenseBufs dnb = {};
 
     // ---- H0 on its own stream: it overlaps the apparent-pair kernels, which
     // do not need the spanning forest (a forest edge is an H0 death, never an
     // apparent column; the reductions skip forest edges among the residuals).
     // The triangle ranks of the dense H1 chain go on a second side stream.
-    HIPC(hipEventRecord(w.evf, s));
-    hipStream_t s2 = w.stream2, s4 = w.stream4;
-    HIPC(hipStreamWaitEvent(s2, w.evf, 0));
-    HIPC(hipStreamWaitEvent(s4, w.evf, 0));
-    if (int rc = tm2.begin()) return rc;
-    if (int rc = tm4.begin()) return rc;
-    if (n <= kSmallN) {
-        hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s4, dist, n, a.thresh, stats,
-                           (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
-    } else {
-        int T = n <= 256 ? 256 : 1024;
-        size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
-        base = align_up(base, 16);
-        size_t avail = kLdsMax - base;
-        uint64_t ch = 1;
-        while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
-        size_t lds = base + ch * 8;
-        hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
-                           (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
-    }
-    HIPC(hipGetLastError());
-    if (int rc = tm4.mark("k_h0")) return rc;
-    HIPC(hipEventRecord(w.evh, s4));
-    DenseBufs dnb = {};
-    if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
-        dnb.recs = (EdgeRec*)(B + p.o_recs);
-        dnb.cls = (uint32_t*)(B + p.o_cls);
-        dnb.res1 = (uint32_t*)(B + p.o_res1);
-        dnb.inv32 = (uint32_t*)(B + p.o_inv32);
-        dnb.rank_of = (uint16_t*)(B + p.o_rof);
-        dnb.tri_stride = p.tri_stride;
-        dnb.cls2 = (uint16_t*)(B + p.o_cls2);
-        dnb.n2p = p.n2p;
-        dnb.inv = (uint16_t*)(B + p.o_inv);
-        dnb.E = (uint32_t)binom((uint64_t)n, 2);
-        dnb.inv_stride = p.inv_stride;
-        dnb.K = p.dK;
-        hipLaunchKernelGGL(k_h1_prep, dim3(L), dim3(1024), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.fast ? 1 : 0, stats);
+    // Enqueued after apparent<1>, so the critical path's kernels are queued first.
+    auto launch_side = [&]() -> int {
+        hipStream_t s2 = w.stream2, s4 = w.stream4;
+        HIPC(hipStreamWaitEvent(s2, w.evf, 0));
+        HIPC(hipStreamWaitEvent(s4, w.evf, 0));
+        if (int rc = tm2.begin()) return rc;
+        if (int rc = tm4.begin()) return rc;
+        if (n <= kSmallN) {
+            hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s4, dist, n, a.thresh, stats,
+                               (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
+        } else {
+            int T = n <= 256 ? 256 : 1024;
+            size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
+            base = align_up(base, 16);
+            size_t avail = kLdsMax - base;
+            uint64_t ch = 1;
+            while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
+            size_t lds = base + ch * 8;
+            hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
+                               (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
+        }
         HIPC(hipGetLastError());
-        if (int rc = tm2.mark("k_h1_prep")) return rc;
-    }
-    HIPC(hipEventRecord(w.evj, s2));
+        if (int rc = tm4.mark("k_h0")) return rc;
+        HIPC(hipEventRecord(w.evh, s4));
+        if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
+            dnb.recs = (EdgeRec*)(B + p.o_recs);
+            dnb.cls = (uint32_t*)(B + p.o_cls);
+            dnb.res1 = (uint32_t*)(B + p.o_res1);
+            dnb.inv32 = (uint32_t*)(B + p.o_inv32);
+            dnb.rank_of = (uint16_t*)(B + p.o_rof);
+            dnb.tri_stride = p.tri_stride;
+            dnb.cls2 = (uint16_t*)(B + p.o_cls2);
+            dnb.n2p = p.n2p;
+            dnb.inv = (uint16_t*)(B + p.o_inv);
+            dnb.E = (uint32_t)binom((uint64_t)n, 2);
+            dnb.inv_stride = p.inv_stride;
+            dnb.K = p.dK;
+            dnb.epos = (uint32_t*)(B + p.o_epos);
+            dnb.eqq = (uint32_t*)(B + p.o_eqq);
+            dnb.eM = (uint64_t*)(B + p.o_eM);
+            dnb.cpos = (uint32_t*)(B + p.o_cpos);
+            dnb.necnt = (uint32_t*)(B + p.o_necnt);
+            const dim3 pg((unsigned)L, (unsigned)((dnb.E + kPrepEdges - 1) / kPrepEdges));
+            hipLaunchKernelGGL(k_prep_edges, pg, dim3(256), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.fast ? 1 : 0);
+            HIPC(hipGetLastError());
+            if (int rc = tm2.mark("k_prep_edges")) return rc;
+            hipLaunchKernelGGL(k_prep_scan, dim3(L), dim3(256), 0, s2, dnb, stats);
+            HIPC(hipGetLastError());
+            if (int rc = tm2.mark("k_prep_scan")) return rc;
+            hipLaunchKernelGGL(k_prep_tables, pg, dim3(256), 0, s2, dist, n, dnb, p.fast ? 1 : 0);
+            HIPC(hipGetLastError());
+            if (int rc = tm2.mark("k_prep_tables")) return rc;
+            if (p.cmode == kChainTable) {
+                dnb.cobt = (uint16_t*)(B + p.o_cobt);
+                dnb.cob_stride = p.cob_stride;
+                hipLaunchKernelGGL(k_prep_cob, pg, dim3(256), 0, s2, n, dnb);
+                HIPC(hipGetLastError());
+                if (int rc = tm2.mark("k_prep_cob")) return rc;
+            }
+        }
+        HIPC(hipEventRecord(w.evj, s2));
+        return 0;
+    };
 
     // ---- H1 .. Hmaxdim: apparent pairs (parallel), residual sort, serial reduction
     DimBufs db[3] = {};
@@ -699,10 +746,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // on a third stream beside the H1 chain; they only need apparent<1>'s
     // pivot bitmap, and the chain records its residual pivots separately
     const bool split2 = p.dense && p.maxdim >= 2;
+    if (p.maxdim < 1)
+        if (int rc = launch_side()) return rc;
     if (p.maxdim >= 1) {
         launch_apparent(1, s);
         HIPC(hipGetLastError());
         MARK("k_apparent<1>");
+        if (int rc = launch_side()) return rc;
         if (split2) {
             HIPC(hipEventRecord(w.evs, s));
             HIPC(hipStreamWaitEvent(w.stream3, w.evs, 0));
@@ -713,7 +763,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             launch_sort(2, 1, w.stream3);
             HIPC(hipGetLastError());
             if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
-            HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));  // edge classes (k_h1_prep)
+            HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));  // edge classes (k_prep_*)
             hipLaunchKernelGGL(k_h2_phase1, dim3(L, kP1Grid), dim3(64), p.p1_lds, w.stream3, dist, n, stats, db[2], sb,
                                (const uint16_t*)dnb.cls2, p.n2p, p.bm_words, (const uint32_t*)dnb.res1, (uint32_t)p.piv_words[1],
                                step_limit());
@@ -747,15 +797,16 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     hipLaunchKernelGGL((k_reduce_all<LW, P1, P2>), dim3(L), dim3(64), rc.bytes, s, dist, n, p.maxdim, stats, db[1], db[2], rb, rc, \
                        pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
         if (p.dense) {
-            switch (p.dK * 2 + (p.fast ? 1 : 0)) {
+            switch (p.dK * 3 + p.cmode) {
 #define TDA_CHAIN(K, F)                                                                                                          \
-    case K * 2 + F:                                                                                                              \
+    case K * 3 + F:                                                                                                              \
         hipLaunchKernelGGL((k_h1_chain<K, F>), dim3(L), dim3(kChainT), p.chain_lds, s, dist, n, stats, db[1], rb, dnb, step_limit(), \
                            pairs1, p.pcap[1]);                                                                                   \
         break;
                 TDA_CHAIN(1, 0) TDA_CHAIN(2, 0) TDA_CHAIN(3, 0) TDA_CHAIN(4, 0) TDA_CHAIN(6, 0) TDA_CHAIN(9, 0) TDA_CHAIN(12, 0)
                 TDA_CHAIN(16, 0) TDA_CHAIN(21, 0)
                 TDA_CHAIN(1, 1) TDA_CHAIN(2, 1) TDA_CHAIN(3, 1) TDA_CHAIN(4, 1) TDA_CHAIN(6, 1) TDA_CHAIN(9, 1) TDA_CHAIN(12, 1)
+                TDA_CHAIN(1, 2) TDA_CHAIN(2, 2) TDA_CHAIN(3, 2) TDA_CHAIN(4, 2) TDA_CHAIN(6, 2) TDA_CHAIN(9, 2) TDA_CHAIN(12, 2)
 #undef TDA_CHAIN
                 default:
                     return fail(TDA_E_INVALID, "no k_h1_chain instantiation for this N");
@@ -902,10 +953,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 mxa = w.hstats[l].prof[1][3] & 0xFFFF;
             }
         }
-        const uint64_t* pp = w.hstats[0].prof[3];
-        fprintf(stderr, "[tda-prof] k_h1_prep layer 0: keys %llu sort %llu masks %llu scan %llu recs %llu inv %llu cycles\n",
-                (unsigned long long)pp[1], (unsigned long long)pp[2], (unsigned long long)pp[3], (unsigned long long)pp[4],
-                (unsigned long long)pp[5], (unsigned long long)pp[6]);
         fprintf(stderr, "[tda-prof] H2 phase 1: all columns %llu cycles (scan %llu cob %llu), %llu adds; slowest column %llu cycles (%llu adds)\n",
                 (unsigned long long)tt, (unsigned long long)sc, (unsigned long long)cb, (unsigned long long)ad, (unsigned long long)mx,
                 (unsigned long long)mxa);

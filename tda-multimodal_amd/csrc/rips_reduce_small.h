@@ -5,7 +5,7 @@
 //     apparent additions in a row (layer 25: 168 of the layer's 173).  That
 //     chain is the critical path of the whole batch, so its per-addition cost
 //     is what matters.  The working column W is a dense LDS bitmap over the
-//     triangles in FILTRATION order (k_h1_prep ranks them), so the pivot is
+//     triangles in FILTRATION order (k_prep_* rank them), so the pivot is
 //     simply the first set bit: every lane tests its 32*K-bit slice, one
 //     ballot picks the first non-empty slice.  A toggle is one fire-and-forget
 //     ds_xor at the triangle's rank, a stored reduced column R_j is a copy of
@@ -25,7 +25,7 @@
 // pivot owned by an apparent column is never a residual pivot), so the
 // result is bit-identical to the serial order.
 //
-// Triangle ranks (k_h1_prep).  Every triangle t <= thresh is assigned to its
+// Triangle ranks (k_prep_*).  Every triangle t <= thresh is assigned to its
 // youngest facet e(t) (longest edge, ties -> smallest edge index); that is the
 // facet an apparent pair would pair it with.  Edges are sorted by length and
 // edge e owns the rank block [off_e, off_e + |M_e|), M_e = bitmask of third
@@ -42,7 +42,7 @@
 namespace tda {
 
 constexpr int kDenseMaxN = 64;
-constexpr int kChainT = 256;              // threads per k_h1_chain block (staging; the chain is wave 0)
+constexpr int kChainT = 1024;             // threads per k_h1_chain block (staging; the chain is wave 0)
 constexpr int kP1Grid = 96;               // k_h2_phase1 blocks per layer (one wave each, strided columns)
 constexpr uint32_t kP1WCap = 512;         // phase-1 toggle-set capacity
 constexpr int kChainMaxCols = 512;        // non-cleared H1 residual columns / stored R_j per layer
@@ -106,256 +106,267 @@ __device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) {
 struct DenseBufs {
     EdgeRec* recs;      // [L][E]
     uint32_t* cls;      // [L][E] rank range of the edge's length class: cs | ce << 16 (tie path)
-    uint16_t* inv;      // [L][inv_stride] rank -> edge (general path)
+    uint16_t* inv;      // [L][inv_stride] rank -> edge | kInvFirst | kInvTie (kInvRes set by the TABLE chain in LDS)
     uint32_t* inv32;    // [L][inv_stride] rank -> a | b << 6 | w << 12 | first << 18 | tie << 19 (FAST path)
     uint16_t* rank_of;  // [L][tri_stride] triangle colex index -> rank, 0xFFFF above thresh (FAST path)
     uint32_t tri_stride;
     uint16_t* cls2;     // [L][n2p] length-class rank of edge (u, v) at u * n + v; 0xFFFF above thresh (H2 phase 1)
     uint32_t n2p;
     uint32_t* res1;     // [L][piv_words1] colex bitmap of residual H1 pivots (H2 clearing; zeroed per call)
+    uint32_t* epos;     // [L][E] rank of the edge among edges <= thresh (kNoRank above)
+    uint32_t* eqq;      // [L][E] length class of the edge in rank positions: q0 | q1 << 16
+    uint64_t* eM;       // [L][E] block masks
+    uint32_t* cpos;     // [L][E + 8] block sizes by rank, then their exclusive scan
+    uint32_t* necnt;    // [L] edges <= thresh (zeroed per call)
+    uint16_t* cobt;     // [L][cob_stride] TABLE chain: rank of {a, b, v} at e * n + v
+    uint32_t cob_stride;
     uint32_t E, inv_stride;
     int K;              // bitmap words per lane (W = 64 K words)
 };
 
 // ---------------------------------------------------------------- ranks
-// 2048 u64 keys in one 1024-thread block, ascending: two keys per thread in
-// registers; compare-exchange distances below 128 are in-wave shuffles, only
-// the 10 stages with distance >= 128 go through LDS (sk).
-__device__ __forceinline__ void sort2048(uint64_t& k0, uint64_t& k1, uint64_t* sk) {
-    const int t = threadIdx.x;
-    for (int k = 2; k <= 2048; k <<= 1) {
-        const bool up = ((2 * t) & k) == 0;
-        int j = k >> 1;
-        if (j >= 128) {
-            sk[2 * t] = k0;
-            sk[2 * t + 1] = k1;
-            __syncthreads();
-            for (; j >= 128; j >>= 1) {
-                // element pairs (i, i ^ j) with i < i ^ j: one per thread
-                const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-                const uint64_t x = sk[i], y = sk[i ^ j];
-                const bool u = (i & k) == 0;
-                if ((x > y) == u) {
-                    sk[i] = y;
-                    sk[i ^ j] = x;
-                }
-                __syncthreads();
-            }
-            k0 = sk[2 * t];
-            k1 = sk[2 * t + 1];
-            __syncthreads();
-        }
-        for (; j >= 2; j >>= 1) {
-            const int m = j >> 1;  // partner thread t ^ m (same wave: m < 64)
-            const uint64_t p0 = shfl_xor_u64(k0, m), p1 = shfl_xor_u64(k1, m);
-            const bool lower = (t & m) == 0;
-            const bool keep_min = lower == up;
-            k0 = keep_min ? (k0 < p0 ? k0 : p0) : (k0 > p0 ? k0 : p0);
-            k1 = keep_min ? (k1 < p1 ? k1 : p1) : (k1 > p1 ? k1 : p1);
-        }
-        {  // j == 1: inside the thread
-            const uint64_t lo = k0 < k1 ? k0 : k1, hi = k0 < k1 ? k1 : k0;
-            k0 = up ? lo : hi;
-            k1 = up ? hi : lo;
-        }
-    }
-}
+// Triangle ranks in three launches, spread over kPrepEdges-edge blocks so a
+// layer's edge work is not serialised on one CU:
+//   k_prep_edges   rank of each edge <= thresh in (length, index) order by
+//                  counting, its length class [q0, q1], its block mask M_e
+//   k_prep_scan    exclusive scan of the block sizes in rank order
+//   k_prep_tables  recs / cls / cls2 and the rank tables:
+//                  rank_of[triangle] (0xFFFF above thresh), inv32[rank] = a |
+//                  b << 6 | w << 12 | first << 18 | tie << 19   (FAST path)
+//                  inv16[rank] = edge                           (general path)
+constexpr int kPrepEdges = 64;   // edges per block (counting: 4 slices of the edge list per edge)
+constexpr uint32_t kNoRank = 0xFFFFFFFFu;
+// inv16[rank] = edge | flags (edge < 2048 for N <= 64)
+constexpr uint32_t kInvEdge = 0x7FFu, kInvFirst = 1u << 11, kInvTie = 1u << 12, kInvRes = 1u << 13;
 
-// One 1024-thread block per layer: sort the edges <= thresh by length, build
-// each edge's block mask, the exclusive scan of block sizes (= ranks), the
-// class ranges and the rank tables:
-//   recs[e], inv16[rank] = e           (general path)
-//   rank_of[triangle] (0xFFFF: above thresh), inv32[rank] = a | b << 6 |
-//   w << 12 | first-of-block << 18 | tie << 19      (FAST path, N <= ~51)
-// Keys are (length bits << 32 | e << 12 | a << 6 | b): no index decode after
-// the sort.  LDS: [16][D][keys 2048][counts 2048][masks 2048].
-__global__ __launch_bounds__(1024) void k_h1_prep(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
-                                                  float user_thresh, DenseBufs db, int fast, LayerStats* __restrict__ stats) {
+__global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
+                                                    float user_thresh, DenseBufs db, int fast) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, t = threadIdx.x, T = blockDim.x, ln = t & 63, wv = t >> 6, nw = T >> 6;
-#ifdef TDA_PROFILE
-    uint64_t tp[8];
-    tp[0] = clock64();
-#define TDA_PREP_STAMP(i) tp[i] = clock64()
-#else
-#define TDA_PREP_STAMP(i)
-#endif
+    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    const int e0 = blockIdx.y * kPrepEdges;
+    const int E = n * (n - 1) / 2;
     const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
     float* D = (float*)(smem + 16);
-    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, T);
-    uint64_t* sk = (uint64_t*)(smem + 16 + ((4ull * n * n + 15) & ~15ull));
-    uint32_t* off = (uint32_t*)(sk + 2048);
-    uint64_t* Ms = (uint64_t*)(off + 2048);
-    uint32_t& s_ne = *(uint32_t*)(smem + 4);
-    uint32_t& s_tot = *(uint32_t*)(smem + 8);
-    const int E = n * (n - 1) / 2;
-    if (t == 0) s_ne = 0;
-    if (fast) {  // every triangle starts "above the threshold"
+    float* lens = D + ((n * n + 3) & ~3);
+    uint32_t* part = (uint32_t*)(lens + ((E + 3) & ~3));  // [4 slices][3][64]
+    uint32_t* rk_sh = part + 4 * 3 * 64;                   // [64]
+    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, 256);
+    if (fast) {  // this block's share of "every triangle above the threshold"
         uint32_t* ro = (uint32_t*)(db.rank_of + (size_t)l * db.tri_stride);
-        for (uint32_t i = t; i < db.tri_stride / 2; i += T) st_glb(ro, i, 0xFFFFFFFFu);
+        const uint32_t words = db.tri_stride / 2, per = (words + gridDim.y - 1) / gridDim.y;
+        const uint32_t w0 = blockIdx.y * per, w1 = min(words, w0 + per);
+        for (uint32_t i = w0 + t; i < w1; i += 256) st_glb(ro, i, 0xFFFFFFFFu);
     }
     __syncthreads();
-    uint64_t k0 = kEmpty64, k1 = kEmpty64;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const int q = 2 * t + c;
-        uint64_t k = kEmpty64;
-        if (q < E) {
-            int a, b;
-            edge_verts((uint32_t)q, a, b);
-            const float d = D[a * n + b];
-            if (d <= r) k = ((uint64_t)__float_as_uint(d + 0.0f) << 32) | ((uint32_t)q << 12) | ((uint32_t)a << 6) | (uint32_t)b;
+    for (int e = t; e < E; e += 256) {
+        int a, b;
+        edge_verts((uint32_t)e, a, b);
+        const float d = D[a * n + b];
+        lens[e] = d <= r ? d : INFINITY;
+    }
+    __syncthreads();
+    // rank = #{shorter} + #{same length, smaller index}; class = [#{shorter}, #{shorter} + #{same} - 1]
+    {
+        const int e = e0 + ln, sl = wv;
+        const float le = e < E ? lens[e] : INFINITY;
+        const int c0 = (E * sl) / 4, c1 = (E * (sl + 1)) / 4;
+        uint32_t nless = 0, neq = 0, neqlo = 0;
+        for (int q = c0; q < c1; ++q) {
+            const float x = lens[q];
+            nless += x < le;
+            neq += x == le;
+            neqlo += (x == le) & (q < e);
         }
-        (c == 0 ? k0 : k1) = k;
+        part[(sl * 3 + 0) * 64 + ln] = nless;
+        part[(sl * 3 + 1) * 64 + ln] = neq;
+        part[(sl * 3 + 2) * 64 + ln] = neqlo;
     }
-    TDA_PREP_STAMP(1);
-    sort2048(k0, k1, sk);
-    sk[2 * t] = k0;
-    sk[2 * t + 1] = k1;
     __syncthreads();
-    // the thread holding the last real key publishes the edge count
-    if (k0 != kEmpty64 && k1 == kEmpty64) s_ne = (uint32_t)(2 * t + 1);
-    if (k1 != kEmpty64 && (t == T - 1 || sk[2 * t + 2] == kEmpty64)) s_ne = (uint32_t)(2 * t + 2);
+    if (t < 64) {
+        const int e = e0 + t;
+        uint32_t rank = kNoRank;
+        if (e < E && lens[e] != INFINITY) {
+            uint32_t nless = 0, neq = 0, neqlo = 0;
+#pragma unroll
+            for (int sl = 0; sl < 4; ++sl) {
+                nless += part[(sl * 3 + 0) * 64 + t];
+                neq += part[(sl * 3 + 1) * 64 + t];
+                neqlo += part[(sl * 3 + 2) * 64 + t];
+            }
+            rank = nless + neqlo;
+            st_glb(db.eqq + (size_t)l * db.E, (size_t)e, nless | ((nless + neq - 1) << 16));
+        }
+        if (e < E) st_glb(db.epos + (size_t)l * db.E, (size_t)e, rank);
+        rk_sh[t] = rank;
+        const uint64_t m = __ballot(rank != kNoRank);
+        if (t == 0 && m) atomicAdd(&db.necnt[l], (uint32_t)__popcll(m));
+    }
     __syncthreads();
-    TDA_PREP_STAMP(2);
-    const int nE = (int)s_ne;
-    // block masks: one wave per edge (4 edges in flight), lane = third vertex
-    for (int q0 = wv; q0 < nE; q0 += 4 * nw) {
-        uint64_t kk[4];
-        float dav[4], dbv[4];
+    // block masks: wave per edge (4 in flight), lane = third vertex
+    for (int i0 = 0; i0 < kPrepEdges / 4; i0 += 4) {
+        float dav[4], dbv[4], lev[4];
+        int av[4], bv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int q = q0 + u * nw;
-            kk[u] = q < nE ? sk[q] : kEmpty64;
-            const int a = (int)((kk[u] >> 6) & 63u), b = (int)(kk[u] & 63u);
+            const int e = e0 + wv * (kPrepEdges / 4) + i0 + u;
+            int a = 0, b = 0;
+            if (e < E) edge_verts((uint32_t)e, a, b);
+            av[u] = a;
+            bv[u] = b;
+            lev[u] = e < E ? lens[e] : INFINITY;
             dav[u] = ln < n ? D[a * n + ln] : 0.0f;
             dbv[u] = ln < n ? D[b * n + ln] : 0.0f;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int q = q0 + u * nw;
-            const uint32_t e = (uint32_t)(kk[u] >> 12) & 0xFFFFFu;
-            const int a = (int)((kk[u] >> 6) & 63u), b = (int)(kk[u] & 63u), v = ln;
-            const float le = __uint_as_float((uint32_t)(kk[u] >> 32));
-            bool ok = q < nE && v < n && v != a && v != b && dav[u] <= le && dbv[u] <= le;
-            if (ok && dav[u] == le && edge_id(a, v) < e) ok = false;  // (a, v) is the younger facet
-            if (ok && dbv[u] == le && edge_id(b, v) < e) ok = false;
+            const int li = wv * (kPrepEdges / 4) + i0 + u, e = e0 + li;
+            const int a = av[u], b = bv[u], v = ln;
+            const float le = lev[u];
+            bool ok = e < E && le != INFINITY && v < n && v != a && v != b && dav[u] <= le && dbv[u] <= le;
+            if (ok && dav[u] == le && edge_id(a, v) < (uint32_t)e) ok = false;  // (a, v) is the younger facet
+            if (ok && dbv[u] == le && edge_id(b, v) < (uint32_t)e) ok = false;
             const uint64_t m = __ballot(ok);
-            if (ln == 0 && q < nE) {
-                Ms[q] = m;
-                off[q] = (uint32_t)__popcll(m);
+            if (ln == 0 && e < E) {
+                st_glb(db.eM + (size_t)l * db.E, (size_t)e, m);
+                const uint32_t rk = rk_sh[li];
+                if (rk != kNoRank) st_glb(db.cpos + (size_t)l * (db.E + 8), (size_t)rk, (uint32_t)__popcll(m));
             }
         }
     }
-    __syncthreads();
-    TDA_PREP_STAMP(3);
-    if (wv == 0) {  // exclusive scan of the block sizes
-        uint32_t carry = 0;
-        for (int q0 = 0; q0 < nE; q0 += 64) {
-            const int q = q0 + ln;
-            const uint32_t c = q < nE ? off[q] : 0u;
-            uint32_t x = c;
-            for (int s = 1; s < 64; s <<= 1) {
-                const uint32_t y = __shfl_up(x, s, 64);
-                if (ln >= s) x += y;
-            }
-            if (q < nE) off[q] = carry + x - c;
-            carry += __shfl(x, 63, 64);
-        }
-        if (ln == 0) s_tot = carry;
+}
+
+// exclusive scan of the block sizes in rank order (one block per layer)
+__global__ __launch_bounds__(256) void k_prep_scan(DenseBufs db, LayerStats* __restrict__ stats) {
+    __shared__ uint32_t wsum[4];
+    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    const uint32_t nE = db.necnt[l];
+    uint32_t* c = db.cpos + (size_t)l * (db.E + 8);
+    const uint32_t per = (nE + 255) / 256, q0 = t * per;
+    uint32_t loc = 0;
+    for (uint32_t q = q0; q < min(nE, q0 + per); ++q) loc += ld_glb(c, q);
+    uint32_t x = loc;  // inclusive wave scan
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t y = __shfl_up(x, s, 64);
+        if (ln >= s) x += y;
     }
+    if (ln == 63) wsum[wv] = x;
     __syncthreads();
-    TDA_PREP_STAMP(4);
+    uint32_t base = 0;
+    for (int w = 0; w < wv; ++w) base += wsum[w];
+    uint32_t run = base + x - loc;  // exclusive prefix of this thread's chunk
+    for (uint32_t q = q0; q < min(nE, q0 + per); ++q) {
+        const uint32_t v = ld_glb(c, q);
+        st_glb(c, q, run);
+        run += v;
+    }
+    if (t == 255) {
+        const uint32_t tot = base + x;
+        st_glb(c, nE, tot);
+        stats[l].ntri = tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_prep_tables(const float* __restrict__ dist, int n, DenseBufs db, int fast) {
+    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    const int E = n * (n - 1) / 2;
+    const float* Dg = dist + (size_t)l * n * n;
+    const uint32_t* c = db.cpos + (size_t)l * (db.E + 8);
     EdgeRec* R = db.recs + (size_t)l * db.E;
-    for (int q = t; q < nE; q += T) {
-        const uint32_t lb = (uint32_t)(sk[q] >> 32);
-        int q0 = q, q1 = q;
-        while (q0 > 0 && (uint32_t)(sk[q0 - 1] >> 32) == lb) --q0;
-        while (q1 + 1 < nE && (uint32_t)(sk[q1 + 1] >> 32) == lb) ++q1;
-        const uint32_t e = (uint32_t)(sk[q] >> 12) & 0xFFFFFu;
-        const int a = (int)((sk[q] >> 6) & 63u), b = (int)(sk[q] & 63u);
-        EdgeRec rec;
-        rec.M = Ms[q];
-        rec.off = (uint16_t)off[q];
-        rec.ab = (uint16_t)(a | (b << 6) | ((q0 != q1) << 12));
-        rec.len = __uint_as_float(lb);
-        R[e] = rec;
-        db.cls[(size_t)l * db.E + e] = off[q0] | ((off[q1] + (uint32_t)__popcll(Ms[q1])) << 16);
-        uint16_t* c2 = db.cls2 + (size_t)l * db.n2p;
-        st_glb(c2, (size_t)a * n + b, (uint16_t)q0);
-        st_glb(c2, (size_t)b * n + a, (uint16_t)q0);
-    }
-    for (int e = t; e < E; e += T) {  // edges above the threshold own no triangles
-        int a, b;
-        edge_verts((uint32_t)e, a, b);
-        const float d = D[a * n + b];
-        if (!(d <= r)) {
-            EdgeRec rec = {};
-            rec.ab = (uint16_t)(a | (b << 6));
-            rec.len = d;
-            R[e] = rec;
-            uint16_t* c2 = db.cls2 + (size_t)l * db.n2p;
-            st_glb(c2, (size_t)a * n + b, (uint16_t)0xFFFFu);
-            st_glb(c2, (size_t)b * n + a, (uint16_t)0xFFFFu);
-        }
-    }
-    __syncthreads();
-    TDA_PREP_STAMP(5);
+    uint16_t* c2 = db.cls2 + (size_t)l * db.n2p;
     uint16_t* inv = db.inv + (size_t)l * db.inv_stride;
     uint32_t* inv32 = db.inv32 + (size_t)l * db.inv_stride;
     uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
-    for (int q0 = wv; q0 < nE; q0 += 4 * nw) {  // 4 edges in flight per wave
-        uint64_t key[4], M[4], kp[4], kn[4];
-        uint32_t o[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int q = q0 + u * nw;
-            const bool in = q < nE;
-            key[u] = in ? sk[q] : 0;
-            M[u] = in ? Ms[q] : 0;
-            o[u] = in ? off[q] : 0;
-            kp[u] = in && q > 0 ? sk[q - 1] : kEmpty64;
-            kn[u] = in && q + 1 < nE ? sk[q + 1] : kEmpty64;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t e = (uint32_t)(key[u] >> 12) & 0xFFFFFu;
-            const int a = (int)((key[u] >> 6) & 63u), b = (int)(key[u] & 63u);
-            const uint32_t lb = (uint32_t)(key[u] >> 32);
-            const bool tie = (uint32_t)(kp[u] >> 32) == lb || (uint32_t)(kn[u] >> 32) == lb;
-            if (!fast) {
-                const uint32_t c = (uint32_t)__popcll(M[u]);
-                if ((uint32_t)ln < c) inv[o[u] + ln] = (uint16_t)e;
-            } else if (ln < n && ((M[u] >> ln) & 1ull)) {
-                const uint32_t rk = o[u] + bits_above(M[u], ln);
-                st_glb(inv32, rk, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(rk == o[u]) << 18) |
-                                      ((uint32_t)tie << 19));
-                st_glb(ro, tri_id(a, b, ln), (uint16_t)rk);
+    for (int i = 0; i < kPrepEdges / 4; ++i) {
+        const int e = blockIdx.y * kPrepEdges + wv * (kPrepEdges / 4) + i;
+        if (e >= E) break;
+        int a, b;
+        edge_verts((uint32_t)e, a, b);
+        const uint32_t rk = ld_glb(db.epos + (size_t)l * db.E, (size_t)e);
+        const float len = ld_glb(Dg, (size_t)a * n + b);
+        if (rk == kNoRank) {  // above the threshold: owns no triangles
+            if (ln == 0) {
+                EdgeRec rec = {};
+                rec.ab = (uint16_t)(a | (b << 6));
+                rec.len = len;
+                R[e] = rec;
+                st_glb(c2, (size_t)a * n + b, (uint16_t)0xFFFFu);
+                st_glb(c2, (size_t)b * n + a, (uint16_t)0xFFFFu);
             }
+            continue;
+        }
+        const uint32_t qq = ld_glb(db.eqq + (size_t)l * db.E, (size_t)e), q0 = qq & 0xFFFFu, q1 = qq >> 16;
+        const uint64_t M = ld_glb(db.eM + (size_t)l * db.E, (size_t)e);
+        const uint32_t off = ld_glb(c, rk);
+        const bool tie = q1 > q0;
+        if (ln == 0) {
+            EdgeRec rec;
+            rec.M = M;
+            rec.off = (uint16_t)off;
+            rec.ab = (uint16_t)(a | (b << 6) | ((uint32_t)tie << 12));
+            rec.len = len;
+            R[e] = rec;
+            st_glb(db.cls + (size_t)l * db.E, (size_t)e, ld_glb(c, q0) | (ld_glb(c, q1 + 1) << 16));
+            st_glb(c2, (size_t)a * n + b, (uint16_t)q0);
+            st_glb(c2, (size_t)b * n + a, (uint16_t)q0);
+        }
+        if ((uint32_t)ln < (uint32_t)__popcll(M))
+            st_glb(inv, off + ln, (uint16_t)(e | (ln == 0 ? kInvFirst : 0u) | (tie ? kInvTie : 0u)));
+        if (fast && ln < n && ((M >> ln) & 1ull)) {
+            const uint32_t q = off + bits_above(M, ln);
+            st_glb(inv32, q, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(q == off) << 18) | ((uint32_t)tie << 19));
+            st_glb(ro, tri_id(a, b, ln), (uint16_t)q);
         }
     }
-    if (t == 0) stats[l].ntri = s_tot;
-#ifdef TDA_PROFILE
-    TDA_PREP_STAMP(6);
-    if (t == 0)
-        for (int i = 1; i < 7; ++i) stats[l].prof[3][i] = tp[i] - tp[i - 1];
-#endif
-#undef TDA_PREP_STAMP
+}
+
+// coboundary table of the TABLE chain: cobt[e * n + v] = rank of {a, b, v}
+// (0xFFFF: v in {a, b} or above thresh); one wave per edge, 4 edges in flight
+__global__ __launch_bounds__(256) void k_prep_cob(int n, DenseBufs db) {
+    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    const int E = n * (n - 1) / 2;
+    const uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
+    uint16_t* ct = db.cobt + (size_t)l * db.cob_stride;
+    for (int i0 = 0; i0 < kPrepEdges / 4; i0 += 4) {
+        uint16_t v16[4];
+        int ev[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = blockIdx.y * kPrepEdges + wv * (kPrepEdges / 4) + i0 + u;
+            ev[u] = e;
+            v16[u] = 0xFFFFu;
+            if (e < E && ln < n) {
+                int a, b;
+                edge_verts((uint32_t)e, a, b);
+                if (ln != a && ln != b) v16[u] = ld_glb(ro, tri_id(a, b, ln));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (ev[u] < E && ln < n) st_glb(ct, (size_t)ev[u] * n + ln, v16[u]);
+    }
 }
 
 // ---------------------------------------------------------------- H1 chain
 // H1 of one layer.  All kChainT threads stage the layer's tables and filter
 // the residual columns; then wave 0 alone runs the serial reduction (waves
-// 1..3 leave; no s_barrier is issued after that point).  K = bitmap words per
-// lane (compile time: the pivot scan is K independent loads and a min tree).
-// FAST (N <= ~51): a toggle is rank_of[triangle] -> ds_xor and the pivot's
-// vertices are one inv32 load; otherwise edge records (recs, inv16).
-// LDS: [16][D][recs E | rank_of][inv16 | inv32][W 64K][res 64K][piv][cols][own].
-template <int K, bool FAST>
+// 1..15 leave; no s_barrier is issued after that point).  K = bitmap words per
+// lane; the bitmap is word-major (word i = k * 64 + lane holds ranks
+// [32 i, 32 i + 32)), so the pivot is the first lane of the first non-empty
+// ballot over k.  MODE picks how a step finds the triangles:
+//   kChainTable (N <= 48): cobt[e][v] is the coboundary of edge e by rank and
+//     inv16[rank] carries edge | first | tie | residual, so an apparent step is
+//     three dependent LDS reads (bitmap, inv16, cobt) and a ds_xor; the
+//     rare new-pair / tie steps decode through inv32 in global memory.
+//   kChainFast (N <= ~51): rank_of[triangle] + inv32 in LDS.
+//   kChainGeneral: edge records (youngest facet, block mask) + inv16.
+// LDS: [16][D][recs E | rank_of | cobt][inv16 | inv32][W 64K][res 64K][piv][cols][own].
+constexpr int kChainGeneral = 0, kChainFast = 1, kChainTable = 2;
+template <int K, int MODE>
 __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
                                                       DimBufs b, Reduce2Bufs rb, DenseBufs db, uint64_t step_limit,
                                                       Pair* __restrict__ pairs, uint64_t pcap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool FAST = MODE == kChainFast, TABLE = MODE == kChainTable, GEN = MODE == kChainGeneral;
     constexpr uint32_t WP = 64u * K;
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
     LayerStats* st = stats + l;
@@ -366,25 +377,28 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
         p += (bytes + 15) & ~(size_t)15;
         return q;
     };
-    float* Dl = (float*)take(4ull * n * n);
-    EdgeRec* R = FAST ? nullptr : (EdgeRec*)take(16ull * E);
-    uint16_t* inv = FAST ? nullptr : (uint16_t*)take(2ull * db.inv_stride);
+    float* Dl = TABLE ? nullptr : (float*)take(4ull * n * n);
+    EdgeRec* R = GEN ? (EdgeRec*)take(16ull * E) : nullptr;
     uint16_t* rof = FAST ? (uint16_t*)take(2ull * db.tri_stride) : nullptr;
+    uint16_t* cobt = TABLE ? (uint16_t*)take(2ull * db.cob_stride) : nullptr;
+    uint16_t* inv = FAST ? nullptr : (uint16_t*)take(2ull * db.inv_stride);
     uint32_t* inv32 = FAST ? (uint32_t*)take(4ull * db.inv_stride) : nullptr;
     uint32_t* W = (uint32_t*)take(4ull * WP);
-    uint32_t* res = (uint32_t*)take(4ull * WP);  // ranks that are residual pivots
+    uint32_t* res = TABLE ? nullptr : (uint32_t*)take(4ull * WP);  // ranks that are residual pivots
     uint32_t* piv = (uint32_t*)take(4ull * b.piv_words);  // colex bitmap of apparent pivots (tie classes)
     uint64_t* cols = (uint64_t*)take(8ull * kChainMaxCols);
     uint16_t* own = (uint16_t*)take(2ull * kChainMaxCols);
-    uint32_t* hdr = (uint32_t*)smem;
 
     const uint32_t ntri = (uint32_t)st->ntri;
-    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, t, kChainT);
+    const float* Dg = dist + (size_t)l * n * n;
+    const uint32_t* inv32g = db.inv32 + (size_t)l * db.inv_stride;
+    if constexpr (!TABLE) stage_to_lds(Dl, Dg, 4ull * n * n, t, kChainT);
     if constexpr (FAST) {
         stage_to_lds(rof, db.rank_of + (size_t)l * db.tri_stride, 2ull * db.tri_stride, t, kChainT);
-        stage_to_lds(inv32, db.inv32 + (size_t)l * db.inv_stride, 4ull * ntri, t, kChainT);
+        stage_to_lds(inv32, inv32g, 4ull * ntri, t, kChainT);
     } else {
-        stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kChainT);
+        if constexpr (GEN) stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kChainT);
+        if constexpr (TABLE) stage_to_lds(cobt, db.cobt + (size_t)l * db.cob_stride, 2ull * db.cob_stride, t, kChainT);  // whole words
         stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kChainT);
     }
     const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
@@ -392,16 +406,19 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
     stage_to_lds(piv, pivg, 4ull * b.piv_words, t, kChainT);
     for (uint32_t i = t; i < WP; i += kChainT) {
         st_lds(W, i, 0u);
-        st_lds(res, i, 0u);
+        if constexpr (!TABLE) st_lds(res, i, 0u);
     }
     uint64_t nres = (uint64_t)st->n_residual[1];
     if (nres > b.rcap) nres = b.rcap;
-    if (wv == 0) {  // drop H0 deaths (spanning-forest edges: cleared columns), keep column order
+    // drop H0 deaths (spanning-forest edges: cleared columns), keep column
+    // order: ordered compaction over the whole block, kChainT columns a round
+    uint32_t* wcnt = (uint32_t*)own;  // per-wave counts (own is unused until the chain)
+    uint32_t nc = 0, nskip = 0;
+    {
         const uint64_t* resid = b.resid + (size_t)l * b.rcap;
         const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
-        uint32_t nc = 0, nskip = 0;
-        for (uint64_t j0 = 0; j0 < nres; j0 += 64) {
-            const uint64_t j = j0 + ln;
+        for (uint64_t j0 = 0; j0 < nres; j0 += kChainT) {
+            const uint64_t j = j0 + t;
             uint64_t key = 0;
             bool keep = false;
             if (j < nres) {
@@ -410,21 +427,26 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 keep = !((ld_glb(mst, s >> 5) >> (s & 31)) & 1u);
             }
             const uint64_t m = __ballot(keep);
-            const uint32_t pos = nc + lanes_below(m);
+            if (ln == 0) wcnt[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t below = 0, tot = 0;
+            for (int q = 0; q < kChainT / 64; ++q) {
+                const uint32_t c = wcnt[q];
+                below += q < wv ? c : 0u;
+                tot += c;
+            }
+            const uint32_t pos = nc + below + lanes_below(m);
             if (keep && pos < (uint32_t)kChainMaxCols) st_lds(cols, pos, key);
-            nc += (uint32_t)__popcll(m);
-            nskip += (uint32_t)__popcll(__ballot(j < nres)) - (uint32_t)__popcll(m);
-        }
-        if (ln == 0) {
-            hdr[0] = nc;
-            hdr[1] = nskip;
+            const uint32_t valid = (uint32_t)min<uint64_t>(kChainT, nres - j0);
+            nc += tot;
+            nskip += valid - tot;
+            __syncthreads();
         }
     }
-    __syncthreads();
+    __syncthreads();  // staging done (also when there are no columns)
     if (wv != 0) return;
 
     const float r = st->thresh;
-    const uint32_t nc = hdr[0], nskip = hdr[1];
     Pair* P = pairs + (size_t)l * pcap;
     uint32_t* pool = (uint32_t*)(rb.rpool + (size_t)l * rb.rpool_cap);
     const uint64_t pool_words = 2ull * rb.rpool_cap;
@@ -441,6 +463,13 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
     // toggle the coboundary of edge (a, b) (length le <= r): lane v -> {a, b, v}
     auto cob = [&](int a, int b, float le) {
         const int v = ln;
+        if constexpr (TABLE) {
+            if (v < n) {
+                const uint32_t rk = ld_lds(cobt, (size_t)edge_id(a, b) * n + v);
+                if (rk != 0xFFFFu) lds_xor(&W[rk >> 5], 1u << (rk & 31));
+            }
+            return;
+        }
         if constexpr (FAST) {
             if (v < n && v != a && v != b) {
                 const uint32_t rk = ld_lds(rof, tri_id(a, b, v));
@@ -476,33 +505,87 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
             lds_xor(&W[rk >> 5], 1u << (rk & 31));
         }
     };
-    // first set bit of W (wave-uniform), false if W is empty
-    auto first_bit = [&](uint32_t& rk) -> bool {
+    // the TABLE coboundary of edge e
+    auto cob_e = [&](uint32_t e) {
+        if (ln < n) {
+            const uint32_t rk = ld_lds(cobt, (size_t)e * n + ln);
+            if (rk != 0xFFFFu) lds_xor(&W[rk >> 5], 1u << (rk & 31));
+        }
+    };
+    // first set bit of W (wave-uniform), false if W is empty; TABLE: also
+    // inv16 of it, loaded per lane for the lane's own first bit while the
+    // ballots run
+    auto first_bit = [&](uint32_t& rk, uint32_t& qv) -> bool {
         uint32_t w[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) w[k] = ld_lds(W, (size_t)ln * K + k);
-        uint32_t pos[K];
+        for (int k = 0; k < K; ++k) w[k] = ld_lds(W, (size_t)k * 64 + ln);
+        uint32_t ws = 0, kk = 0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) pos[k] = w[k] ? (uint32_t)k * 32u + (uint32_t)__builtin_ctz(w[k]) : 0xFFFFu;
+        for (int k = K - 1; k >= 0; --k)
+            if (w[k]) {
+                ws = w[k];
+                kk = (uint32_t)k;
+            }
+        const uint32_t rl = ((kk * 64u + (uint32_t)ln) << 5) + (uint32_t)__builtin_ctz(ws | 0x80000000u);
+        uint32_t ql = 0;
+        if constexpr (TABLE) ql = ld_lds(inv, ws ? rl : 0u);
+        uint64_t m = 0;
 #pragma unroll
-        for (int s = 1; s < K; s <<= 1)
-#pragma unroll
-            for (int k = 0; k + s < K; k += 2 * s) pos[k] = min(pos[k], pos[k + s]);
-        const uint64_t m = __ballot(pos[0] != 0xFFFFu);
+        for (int k = 0; k < K; ++k) {
+            m = __ballot(w[k] != 0u);
+            if (m) break;
+        }
         if (!m) return false;
         const int f = __builtin_ctzll(m);
-        rk = (uint32_t)f * (32u * K) + (uint32_t)__builtin_amdgcn_readlane((int)pos[0], f);
+        rk = (uint32_t)__builtin_amdgcn_readlane((int)rl, f);
+        if constexpr (TABLE) qv = (uint32_t)__builtin_amdgcn_readlane((int)ql, f);
         return true;
+    };
+    // first set bit at rank >= lo, where every bit below lo is known to be
+    // clear: one read of the 64 words from lo on (a column's pivot only moves
+    // forward, and usually not far), the full scan when those are empty
+    auto first_bit_from = [&](uint32_t lo, uint32_t& rk, uint32_t& qv) -> bool {
+        const uint32_t wi = (lo >> 5) + (uint32_t)ln;
+        uint32_t x = wi < WP ? ld_lds(W, wi) : 0u;
+        if (ln == 0) x &= ~0u << (lo & 31);
+        const uint32_t rl = (wi << 5) + (uint32_t)__builtin_ctz(x | 0x80000000u);
+        uint32_t ql = 0;
+        if constexpr (TABLE) ql = ld_lds(inv, x ? rl : 0u);
+        const uint64_t m = __ballot(x != 0u);
+        if (!m) return first_bit(rk, qv);
+        const int f = __builtin_ctzll(m);
+        rk = (uint32_t)__builtin_amdgcn_readlane((int)rl, f);
+        if constexpr (TABLE) qv = (uint32_t)__builtin_amdgcn_readlane((int)ql, f);
+        return true;
+    };
+    // vertices of the triangle at rank rk (a > b: its youngest facet, w: third vertex)
+    auto decode = [&](uint32_t rk, int& a, int& b2, int& w) {
+        if constexpr (GEN) {
+            const EdgeRecV q = load_rec(R, ld_lds(inv, rk) & kInvEdge);
+            a = q.a;
+            b2 = q.b;
+            w = kth_highest(q.M, rk - q.off);
+        } else {
+            const uint32_t q = FAST ? ld_lds(inv32, rk) : ld_glb(inv32g, rk);
+            a = (int)(q & 63u);
+            b2 = (int)((q >> 6) & 63u);
+            w = (int)((q >> 12) & 63u);
+        }
     };
 
     for (uint32_t j = 0; j < nc && !err; ++j) {
         const uint64_t key = ld_lds(cols, j);
         const uint32_t sidx = (uint32_t)key_idx(key);
         const float sdm = key_diam(key);
-        int a0, b0;
-        edge_verts(sidx, a0, b0);
-        cob(a0, b0, sdm);
+        if constexpr (TABLE) {
+            cob_e(sidx);
+        } else {
+            int a0, b0;
+            edge_verts(sidx, a0, b0);
+            cob(a0, b0, sdm);
+        }
         lds_order();
+        uint32_t lo = 0;  // every bit of W below rank lo is clear
         for (uint64_t step = 0;; ++step) {
             if (step >= step_limit) {
                 if (ln == 0) printf("h1_chain: layer %d column %u step limit\n", l, j);
@@ -510,8 +593,8 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 break;
             }
             TDA_STAMP(t1);
-            uint32_t rk;
-            const bool found = first_bit(rk);
+            uint32_t rk, qv = 0;
+            const bool found = first_bit_from(lo, rk, qv);
 #ifdef TDA_PROFILE
             prof[7] += 1;
 #endif
@@ -521,44 +604,63 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 TDA_ACC(1, t1);
                 break;
             }
-            uint32_t resw = ld_lds(res, rk >> 5);
-            int a, b2, w;
-            bool tie, first;
-            if constexpr (FAST) {
-                const uint32_t q = ld_lds(inv32, rk);
-                a = (int)(q & 63u);
-                b2 = (int)((q >> 6) & 63u);
-                w = (int)((q >> 12) & 63u);
-                first = (q >> 18) & 1u;
-                tie = (q >> 19) & 1u;
+            if constexpr (TABLE) {
+                if ((qv & (kInvFirst | kInvTie | kInvRes)) == kInvFirst) {
+                    // apparent pair (e, t): add the coboundary of the youngest facet e
+                    TDA_ACC(1, t1);
+                    TDA_STAMP(t2);
+                    lo = rk + 1;  // the added column starts at rk, which cancels
+                    cob_e(qv & kInvEdge);
+                    ++nadds;
+                    TDA_ACC(3, t2);
+                    lds_order();
+                    continue;
+                }
+            }
+            bool isres, tie, first;
+            int a = 0, b2 = 0, w = 0;
+            uint32_t lo_next = rk + 1;
+            if constexpr (TABLE) {
+                isres = (qv & kInvRes) != 0;
+                tie = (qv & kInvTie) != 0;
+                first = (qv & kInvFirst) != 0;
+                if (!isres && !tie) decode(rk, a, b2, w);
             } else {
-                const EdgeRecV q = load_rec(R, ld_lds(inv, rk));
-                a = q.a;
-                b2 = q.b;
-                tie = q.tie;
-                first = rk == q.off;
-                const uint32_t k = rk - q.off;
-                const int v = ln;
-                w = __builtin_ctzll(__ballot(((q.M >> v) & 1ull) && bits_above(q.M, v) == k));
+                isres = (ld_lds(res, rk >> 5) >> (rk & 31)) & 1u;
+                if constexpr (FAST) {
+                    const uint32_t q = ld_lds(inv32, rk);
+                    a = (int)(q & 63u);
+                    b2 = (int)((q >> 6) & 63u);
+                    w = (int)((q >> 12) & 63u);
+                    first = (q >> 18) & 1u;
+                    tie = (q >> 19) & 1u;
+                } else {
+                    const uint32_t qi = ld_lds(inv, rk);
+                    const EdgeRecV q = load_rec(R, qi & kInvEdge);
+                    a = q.a;
+                    b2 = q.b;
+                    tie = q.tie;
+                    first = rk == q.off;
+                    const uint32_t k = rk - q.off;
+                    const int v = ln;
+                    w = __builtin_ctzll(__ballot(((q.M >> v) & 1ull) && bits_above(q.M, v) == k));
+                }
             }
             if (tie) {
                 // tie class: the pivot is the set triangle of [cs, ce) with the largest index
 #ifdef TDA_PROFILE
                 ++ties;
 #endif
-                const uint32_t cc = ld_glb(clsg, edge_id(a, b2)), c0 = cc & 0xFFFFu, c1 = cc >> 16;
+                const uint32_t cc = ld_glb(clsg, TABLE ? (qv & kInvEdge) : edge_id(a, b2)), c0 = cc & 0xFFFFu, c1 = cc >> 16;
+                lo_next = c0;  // inside the class rank order is not filtration order
                 uint32_t best = 0, brk = rk;
                 for (uint32_t base = c0; base < c1; base += 64) {
                     const uint32_t rho = base + ln;
                     uint32_t cand = 0;
                     if (rho < c1 && ((ld_lds(W, rho >> 5) >> (rho & 31)) & 1u)) {
-                        if constexpr (FAST) {
-                            const uint32_t q2 = ld_lds(inv32, rho);
-                            cand = tri_id((int)(q2 & 63u), (int)((q2 >> 6) & 63u), (int)((q2 >> 12) & 63u)) + 1;
-                        } else {
-                            const EdgeRecV q2 = load_rec(R, ld_lds(inv, rho));
-                            cand = tri_id(q2.a, q2.b, kth_highest(q2.M, rho - q2.off)) + 1;
-                        }
+                        int x, y, z;
+                        decode(rho, x, y, z);
+                        cand = tri_id(x, y, z) + 1;
                     }
                     const uint32_t m = wave_max_u32(cand);
                     if (m > best) {
@@ -567,23 +669,17 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                     }
                 }
                 rk = brk;
-                resw = ld_lds(res, rk >> 5);
-                if constexpr (FAST) {
-                    const uint32_t q = ld_lds(inv32, rk);
-                    a = (int)(q & 63u);
-                    b2 = (int)((q >> 6) & 63u);
-                    w = (int)((q >> 12) & 63u);
+                if constexpr (TABLE) {
+                    qv = ld_lds(inv, rk);
+                    isres = (qv & kInvRes) != 0;
                 } else {
-                    const EdgeRecV q = load_rec(R, ld_lds(inv, rk));
-                    a = q.a;
-                    b2 = q.b;
-                    w = kth_highest(q.M, rk - q.off);
+                    isres = (ld_lds(res, rk >> 5) >> (rk & 31)) & 1u;
                 }
+                decode(rk, a, b2, w);
             }
-            const uint32_t tidx = tri_id(a, b2, w);
             TDA_ACC(1, t1);
             TDA_STAMP(t2);
-            if ((resw >> (rk & 31)) & 1u) {
+            if (isres) {
                 // add the stored reduced column of the residual column that owns rk
                 uint32_t s = 0;
                 for (uint32_t s0 = 0; s0 < nown; s0 += 64) {
@@ -599,17 +695,26 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
 #pragma unroll
                 for (int k = 0; k < K; ++k) x[k] = ld_glb(src, (size_t)k * 64 + ln);
 #pragma unroll
-                for (int k = 0; k < K; ++k) st_lds(W, (size_t)ln * K + k, ld_lds(W, (size_t)ln * K + k) ^ x[k]);
+                for (int k = 0; k < K; ++k) st_lds(W, (size_t)k * 64 + ln, ld_lds(W, (size_t)k * 64 + ln) ^ x[k]);
                 ++nadds;
                 TDA_ACC(4, t2);
-            } else if (tie ? ((ld_lds(piv, tidx >> 5) >> (tidx & 31)) & 1u) : first) {
+                lo = lo_next;
+                lds_order();
+                continue;
+            }
+            const uint32_t tidx = tri_id(a, b2, w);
+            if (tie ? ((ld_lds(piv, tidx >> 5) >> (tidx & 31)) & 1u) : first) {
                 // apparent pair (e, t): add the coboundary of the youngest facet e
-                cob(a, b2, FAST ? 0.0f : ld_lds(Dl, (size_t)a * n + b2));
+                if constexpr (TABLE)
+                    cob_e(edge_id(a, b2));
+                else
+                    cob(a, b2, FAST ? 0.0f : ld_lds(Dl, (size_t)a * n + b2));
                 ++nadds;
+                lo = lo_next;
                 TDA_ACC(3, t2);
             } else {
                 // new persistence pair (column, t); R_j = W
-                const float pd = ld_lds(Dl, (size_t)a * n + b2);
+                const float pd = TABLE ? ld_glb(Dg, (size_t)a * n + b2) : ld_lds(Dl, (size_t)a * n + b2);
                 if (pd > sdm) {
                     if (ln == 0 && ecnt < pcap) store_pair(P, ecnt, sdm, pd, (int64_t)sidx, (int64_t)tidx);
                     ++ecnt;
@@ -623,12 +728,15 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 uint32_t* dst = pool + (size_t)nown * WP;
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    st_glb(dst, (size_t)k * 64 + ln, ld_lds(W, (size_t)ln * K + k));
-                    st_lds(W, (size_t)ln * K + k, 0u);
+                    st_glb(dst, (size_t)k * 64 + ln, ld_lds(W, (size_t)k * 64 + ln));
+                    st_lds(W, (size_t)k * 64 + ln, 0u);
                 }
                 if (ln == 0) {
                     st_lds(own, nown, (uint16_t)rk);
-                    st_lds(res, rk >> 5, resw | (1u << (rk & 31)));
+                    if constexpr (TABLE)
+                        st_lds(inv, rk, (uint16_t)(ld_lds(inv, rk) | kInvRes));
+                    else
+                        st_lds(res, rk >> 5, ld_lds(res, rk >> 5) | (1u << (rk & 31)));
                     matomic_or<false>(&res1[tidx >> 5], 1u << (tidx & 31));  // H2 clearing reads this bitmap
                 }
                 ++nown;
@@ -657,7 +765,7 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
         st->nskip[1] = nskip;
     }
 }
-// bitmap words per lane supported by k_h1_chain instantiations (FAST: up to 12)
+// bitmap words per lane supported by k_h1_chain instantiations (FAST / TABLE: up to 12)
 constexpr int kChainKs[] = {1, 2, 3, 4, 6, 9, 12, 16, 21};
 constexpr int kChainFastMaxK = 12;
 
@@ -667,7 +775,7 @@ constexpr int kChainFastMaxK = 12;
 // whole step runs on 32-bit words:
 //   * a tetrahedron's key is (class << 20) | (2^20 - 1 - colex index), where
 //     class = rank of its longest edge's length among the sorted edges
-//     (cls2, k_h1_prep): key order is Ripser's (diameter asc, index desc);
+//     (cls2, k_prep_tables): key order is Ripser's (diameter asc, index desc);
 //   * membership is a bitmap over tetrahedron indices (a toggle is one
 //     returning ds_xor), the keys live in an append-only log (+ packed
 //     vertices) whose dead entries are dropped lazily by the bitmap test;

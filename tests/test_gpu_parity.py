@@ -78,11 +78,12 @@ def test_naive_golden_pairs(gpu):
             assert res.n_all_pairs[d] == case["n_all_pairs"][str(d)]
 
 
-@pytest.mark.parametrize("chain", ["auto", "general"])
+@pytest.mark.parametrize("chain", ["auto", "fast", "general"])
 def test_sweep48_maxdim2_vs_oracle(gpu, oracle, monkeypatch, chain):
     """C2/C3 workload (32 layers x 48 points, H0-H2): every pair, its simplex
     indices, the count and checksum of ALL pairs (incl. zero persistence).
-    Both H1-chain variants (rank tables / edge records) are checked."""
+    All three H1-chain variants (coboundary table / rank tables / edge
+    records) are checked."""
     monkeypatch.setenv("TDA_CHAIN", chain)
     X = gpu.synthetic.sweep48(32)
     res = gpu.ripser_batch(X, maxdim=2)
@@ -198,6 +199,26 @@ def test_torch_device_input(gpu, oracle):
     res = gpu.ripser_batch(t, maxdim=2)
     for l in range(4):
         assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, f"torch{l}")
+
+
+@pytest.mark.parametrize("chain", ["auto", "fast", "general"])
+def test_dense_chain_ties_vs_oracle(gpu, oracle, monkeypatch, chain):
+    """N <= 64 clouds with many equal edge lengths (integer grids, small
+    integer coordinates): the tie-class pivot path of every H1-chain variant."""
+    monkeypatch.setenv("TDA_CHAIN", chain)
+    rng = np.random.default_rng(5)
+    g2 = np.array([(i, j) for i in range(6) for j in range(8)], np.float32)
+    g3 = np.array([(i, j, k) for i in range(3) for j in range(4) for k in range(4)], np.float32)
+    clouds = [
+        np.stack([g2, g2[rng.permutation(len(g2))]]),
+        np.stack([g3, g3[rng.permutation(len(g3))]]),
+        rng.integers(0, 4, (2, 40, 3)).astype(np.float32),
+        rng.integers(0, 3, (2, 64, 4)).astype(np.float32),
+    ]
+    for X in clouds:
+        res = gpu.ripser_batch(X, maxdim=2)
+        for l in range(len(X)):
+            assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, f"tie n{X.shape[1]} l{l}")
 
 
 def test_random_clouds_vs_oracle(gpu, oracle):
