@@ -88,6 +88,11 @@ typedef struct tda_rips_result {
     const int64_t *n_residual;/* [L][maxdim+1] columns needing reduction        */
     const int64_t *n_adds;    /* [L][maxdim+1] column additions (serial part)   */
     const float *dist;        /* [L][N][N] when want_dist, else NULL            */
+    /* Layout guarantee (lets a binding copy them in three reads): count,
+     * offset, checksum, n_all_pairs, n_columns, n_residual and n_adds are
+     * consecutive [L][maxdim+1] blocks of one allocation, in that order
+     * (count + k * L * (maxdim+1) is the k-th); death = birth + total and
+     * death_idx = birth_idx + total. */
     double device_ms;         /* device time of the call (HIP events)           */
     /* per-stage device times, filled when args.flags & TDA_FLAG_STAGE_TIMES:
      * stage_ms[i] is the time between consecutive stream events bracketing

@@ -80,7 +80,7 @@ struct Plan {
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_epos = 0, o_cobt = 0, o_eqq = 0, o_eM = 0, o_cpos = 0, o_necnt = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_epos = 0, o_cobt = 0, o_lenr = 0, o_clsr = 0, o_q0t = 0, o_eM = 0, o_cpos = 0, o_necnt = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -190,7 +190,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         p.n2p = (uint32_t)align_up(N * N, 8);
         p.bm_words = (uint32_t)((binom(N, 4) + 31) / 32 + 1);
         p.p1_lds = (uint32_t)(pre + al(2ull * p.n2p) + al(4ull * p.bm_words) + 2 * al(4ull * kP1LogCap));
-        p.prep_lds = (uint32_t)(pre + al(4 * E) + 4 * 3 * 64 * 4 + 64 * 4);
+        p.prep_lds = (uint32_t)(pre + al(8 * ((E + 1) & ~1ull)) + 4 * 64 * 4 + 64 * 4);
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
     }
@@ -241,7 +241,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
             p.o_cls = take(L * binom(N, 2) * 4);
             p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
             p.o_epos = take(L * binom(N, 2) * 4);
-            p.o_eqq = take(L * binom(N, 2) * 4);
+            p.o_lenr = take(L * (binom(N, 2) + 8) * 4);
+            p.o_clsr = take(L * (binom(N, 2) + 8) * 4);
+            p.o_q0t = take(L * (binom(N, 2) + 8) * 4);
             p.o_eM = take(L * binom(N, 2) * 8);
             p.o_cpos = take(L * (binom(N, 2) + 8) * 4);
             if (p.fast) {
@@ -281,7 +283,9 @@ struct Workspace {
     OutPair* hout = nullptr;  // host-mapped
     OutPair* hout_dev = nullptr;
     size_t hout_cap = 0;      // in pairs
-    LayerStats* hstats = nullptr;  // pinned
+    LayerStats* hstats = nullptr;  // host-mapped: k_compact writes it
+    LayerStats* hstats_dev = nullptr;
+    int64_t* houtoff_dev = nullptr;
     size_t hstats_cap = 0;
     int64_t* houtoff = nullptr;
     size_t houtoff_cap = 0;
@@ -389,13 +393,15 @@ int ws_prepare(Workspace& w, const Plan& p) {
     if (w.hstats_cap < (size_t)p.L) {
         drop_graphs(w);
         if (w.hstats) HIPC(hipHostFree(w.hstats));
-        HIPC(hipHostMalloc((void**)&w.hstats, sizeof(LayerStats) * p.L, hipHostMallocDefault));
+        HIPC(hipHostMalloc((void**)&w.hstats, sizeof(LayerStats) * p.L, hipHostMallocMapped));
+        HIPC(hipHostGetDevicePointer((void**)&w.hstats_dev, w.hstats, 0));
         w.hstats_cap = p.L;
     }
     if (w.houtoff_cap < (size_t)p.L * 4) {
         drop_graphs(w);
         if (w.houtoff) HIPC(hipHostFree(w.houtoff));
-        HIPC(hipHostMalloc((void**)&w.houtoff, sizeof(int64_t) * p.L * 4, hipHostMallocDefault));
+        HIPC(hipHostMalloc((void**)&w.houtoff, sizeof(int64_t) * p.L * 4, hipHostMallocMapped));
+        HIPC(hipHostGetDevicePointer((void**)&w.houtoff_dev, w.houtoff, 0));
         w.houtoff_cap = p.L * 4;
     }
     size_t want = std::max<size_t>(1 << 16, (size_t)p.L * 256);
@@ -455,12 +461,14 @@ int set_lds_attrs(int dev) {
 }
 
 // result owned by the library
+// The per-(layer, dim) arrays are one allocation, in the order count,
+// offset, checksum, n_all_pairs, n_columns, n_residual, n_adds; birth/death
+// and birth_idx/death_idx are each one allocation too (tda_rips.h).
 struct ResultImpl {
     tda_rips_result pub;
-    std::vector<int64_t> count, offset, num_edges, n_all, n_cols, n_res, n_add, bidx, didx;
-    std::vector<float> birth, death, thresh, dist, stage_ms;
+    std::vector<int64_t> meta, num_edges, idx;
+    std::vector<float> bd, thresh, dist, stage_ms;
     std::vector<const char*> stage_name;
-    std::vector<uint64_t> checksum;
 };
 
 std::string err_flags(int e) {
@@ -647,27 +655,25 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             dnb.inv_stride = p.inv_stride;
             dnb.K = p.dK;
             dnb.epos = (uint32_t*)(B + p.o_epos);
-            dnb.eqq = (uint32_t*)(B + p.o_eqq);
+            dnb.lenr = (uint32_t*)(B + p.o_lenr);
+            dnb.clsr = (uint32_t*)(B + p.o_clsr);
+            dnb.q0t = (uint32_t*)(B + p.o_q0t);
+            dnb.cobt = (uint16_t*)(B + p.o_cobt);
+            dnb.cob_stride = p.cob_stride;
             dnb.eM = (uint64_t*)(B + p.o_eM);
             dnb.cpos = (uint32_t*)(B + p.o_cpos);
             dnb.necnt = (uint32_t*)(B + p.o_necnt);
             const dim3 pg((unsigned)L, (unsigned)((dnb.E + kPrepEdges - 1) / kPrepEdges));
-            hipLaunchKernelGGL(k_prep_edges, pg, dim3(256), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.fast ? 1 : 0);
+            hipLaunchKernelGGL(k_prep_edges, pg, dim3(256), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_edges")) return rc;
             hipLaunchKernelGGL(k_prep_scan, dim3(L), dim3(256), 0, s2, dnb, stats);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_scan")) return rc;
-            hipLaunchKernelGGL(k_prep_tables, pg, dim3(256), 0, s2, dist, n, dnb, p.fast ? 1 : 0);
+            hipLaunchKernelGGL(k_prep_tables, pg, dim3(256), 16 + align_up(4ull * n * n, 16), s2, dist, n, rowmax, a.thresh, dnb,
+                               p.cmode);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_tables")) return rc;
-            if (p.cmode == kChainTable) {
-                dnb.cobt = (uint16_t*)(B + p.o_cobt);
-                dnb.cob_stride = p.cob_stride;
-                hipLaunchKernelGGL(k_prep_cob, pg, dim3(256), 0, s2, n, dnb);
-                HIPC(hipGetLastError());
-                if (int rc = tm2.mark("k_prep_cob")) return rc;
-            }
         }
         HIPC(hipEventRecord(w.evj, s2));
         return 0;
@@ -852,13 +858,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         MARK("k_finalize");
     }
     const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, (int64_t*)(B + p.o_outoff), w.hout_dev,
-                       (uint64_t)w.hout_cap);
+    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, w.houtoff_dev, w.hout_dev,
+                       (uint64_t)w.hout_cap, w.hstats_dev);
     HIPC(hipGetLastError());
     MARK("k_compact");
-    HIPC(hipMemcpyAsync(w.hstats, stats, sizeof(LayerStats) * L, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(w.houtoff, B + p.o_outoff, sizeof(int64_t) * L * (p.maxdim + 1), hipMemcpyDeviceToHost, s));
-    MARK("d2h_stats");
     HIPC(rec_t(w.ev1));
     return 0;
     };  // enqueue
@@ -901,11 +904,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         for (int l = 0; l < L; ++l) w.hstats[l].err = 0;
         HIPC(hipMemcpyAsync(stats, w.hstats, sizeof(LayerStats) * L, hipMemcpyHostToDevice, s));
         const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
-        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, (int64_t*)(B + p.o_outoff), w.hout_dev,
-                           (uint64_t)w.hout_cap);
+        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, w.houtoff_dev, w.hout_dev,
+                           (uint64_t)w.hout_cap, w.hstats_dev);
         HIPC(hipGetLastError());
-        HIPC(hipMemcpyAsync(w.hstats, stats, sizeof(LayerStats) * L, hipMemcpyDeviceToHost, s));
-        HIPC(hipMemcpyAsync(w.houtoff, B + p.o_outoff, sizeof(int64_t) * L * (p.maxdim + 1), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
         errs = 0;
         for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
@@ -974,13 +975,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // ---- result
     auto* R = new ResultImpl();
     const int nd = p.maxdim + 1;
-    R->count.resize((size_t)L * nd);
-    R->offset.resize((size_t)L * nd);
-    R->checksum.resize((size_t)L * nd);
-    R->n_all.resize((size_t)L * nd);
-    R->n_cols.resize((size_t)L * nd);
-    R->n_res.resize((size_t)L * nd);
-    R->n_add.resize((size_t)L * nd);
+    const size_t S = (size_t)L * nd;
+    R->meta.resize(7 * S);
+    int64_t* m_count = R->meta.data();
+    int64_t* m_off = m_count + S;
+    uint64_t* m_cs = (uint64_t*)(m_count + 2 * S);
+    int64_t* m_all = m_count + 3 * S;
+    int64_t* m_cols = m_count + 4 * S;
+    int64_t* m_res = m_count + 5 * S;
+    int64_t* m_add = m_count + 6 * S;
     R->thresh.resize(L);
     R->num_edges.resize(L);
     size_t total = 0;
@@ -990,25 +993,24 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         R->num_edges[l] = st.num_edges;
         for (int d = 0; d < nd; ++d) {
             int64_t c = std::min<int64_t>(st.count[d], (int64_t)p.pcap[d]);
-            R->count[l * nd + d] = c;
-            R->offset[l * nd + d] = w.houtoff[l * nd + d];
-            R->checksum[l * nd + d] = st.checksum[d];
-            R->n_all[l * nd + d] = st.all_pairs[d];
-            R->n_cols[l * nd + d] = st.n_columns[d];
-            R->n_res[l * nd + d] = st.n_residual[d] - st.nskip[d];
-            R->n_add[l * nd + d] = st.n_adds[d];
+            m_count[l * nd + d] = c;
+            m_off[l * nd + d] = w.houtoff[l * nd + d];
+            m_cs[l * nd + d] = st.checksum[d];
+            m_all[l * nd + d] = st.all_pairs[d];
+            m_cols[l * nd + d] = st.n_columns[d];
+            m_res[l * nd + d] = st.n_residual[d] - st.nskip[d];
+            m_add[l * nd + d] = st.n_adds[d];
             total += (size_t)c;
         }
     }
-    R->birth.resize(total);
-    R->death.resize(total);
-    R->bidx.resize(total);
-    R->didx.resize(total);
+    R->bd.resize(2 * total);
+    R->idx.resize(2 * total);
     for (size_t e = 0; e < total; ++e) {
-        R->birth[e] = w.hout[e].birth;
-        R->death[e] = w.hout[e].death;
-        R->bidx[e] = w.hout[e].birth_idx;
-        R->didx[e] = w.hout[e].death_idx;
+        const OutPair q = w.hout[e];
+        R->bd[e] = q.birth;
+        R->bd[total + e] = q.death;
+        R->idx[e] = q.birth_idx;
+        R->idx[total + e] = q.death_idx;
     }
     if (a.want_dist) {
         R->dist.resize((size_t)L * n * n);
@@ -1020,19 +1022,19 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     o.L = L;
     o.maxdim = p.maxdim;
     o.N = n;
-    o.count = R->count.data();
-    o.offset = R->offset.data();
-    o.birth = R->birth.data();
-    o.death = R->death.data();
-    o.birth_idx = R->bidx.data();
-    o.death_idx = R->didx.data();
+    o.count = m_count;
+    o.offset = m_off;
+    o.birth = R->bd.data();
+    o.death = R->bd.data() + total;
+    o.birth_idx = R->idx.data();
+    o.death_idx = R->idx.data() + total;
     o.thresh = R->thresh.data();
     o.num_edges = R->num_edges.data();
-    o.checksum = R->checksum.data();
-    o.n_all_pairs = R->n_all.data();
-    o.n_columns = R->n_cols.data();
-    o.n_residual = R->n_res.data();
-    o.n_adds = R->n_add.data();
+    o.checksum = m_cs;
+    o.n_all_pairs = m_all;
+    o.n_columns = m_cols;
+    o.n_residual = m_res;
+    o.n_adds = m_add;
     o.dist = a.want_dist ? R->dist.data() : nullptr;
     o.device_ms = ms;
     for (size_t i = 0; i < tm.names.size(); ++i) {

@@ -755,8 +755,10 @@ struct OutPair {
     float birth, death;
     int64_t birth_idx, death_idx;
 };
+// The layer stats and segment offsets also go straight to host-mapped memory
+// (no copy kernels after this one).
 __global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats, int L, int maxdim, PairSet ps, int64_t* __restrict__ out_off,
-                                                  OutPair* __restrict__ out, uint64_t out_cap) {
+                                                  OutPair* __restrict__ out, uint64_t out_cap, LayerStats* __restrict__ stats_host) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int64_t* off = (int64_t*)smem;  // L*nd + 1
     const int nd = maxdim + 1, S = L * nd, t = threadIdx.x;
@@ -775,6 +777,13 @@ __global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats
     }
     __syncthreads();
     for (int i = t; i < S; i += blockDim.x) out_off[i] = off[i];
+    {
+        static_assert(sizeof(LayerStats) % 8 == 0, "LayerStats copies as u64 words");
+        const uint64_t* src = (const uint64_t*)stats;
+        uint64_t* dst = (uint64_t*)stats_host;
+        const int nw8 = L * (int)(sizeof(LayerStats) / 8);
+        for (int i = t; i < nw8; i += blockDim.x) dst[i] = src[i];
+    }
     if ((uint64_t)off[S] > out_cap) return;
     const int w = t >> 6, ln = t & 63, nw = blockDim.x >> 6;
     for (int i = w; i < S; i += nw) {

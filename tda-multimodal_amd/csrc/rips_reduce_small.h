@@ -114,7 +114,9 @@ struct DenseBufs {
     uint32_t n2p;
     uint32_t* res1;     // [L][piv_words1] colex bitmap of residual H1 pivots (H2 clearing; zeroed per call)
     uint32_t* epos;     // [L][E] rank of the edge among edges <= thresh (kNoRank above)
-    uint32_t* eqq;      // [L][E] length class of the edge in rank positions: q0 | q1 << 16
+    uint32_t* lenr;     // [L][E + 8] length bits by rank
+    uint32_t* clsr;     // [L][E + 8] by rank: the class's triangle ranks: cs | ce << 16
+    uint32_t* q0t;      // [L][E + 8] by rank: first edge rank of the class | tie << 16
     uint64_t* eM;       // [L][E] block masks
     uint32_t* cpos;     // [L][E + 8] block sizes by rank, then their exclusive scan
     uint32_t* necnt;    // [L] edges <= thresh (zeroed per call)
@@ -128,30 +130,35 @@ struct DenseBufs {
 // Triangle ranks in three launches, spread over kPrepEdges-edge blocks so a
 // layer's edge work is not serialised on one CU:
 //   k_prep_edges   rank of each edge <= thresh in (length, index) order by
-//                  counting, its length class [q0, q1], its block mask M_e
-//   k_prep_scan    exclusive scan of the block sizes in rank order
-//   k_prep_tables  recs / cls / cls2 and the rank tables:
-//                  rank_of[triangle] (0xFFFF above thresh), inv32[rank] = a |
-//                  b << 6 | w << 12 | first << 18 | tie << 19   (FAST path)
-//                  inv16[rank] = edge                           (general path)
+//                  counting smaller 64-bit keys; its block mask M_e; by rank:
+//                  the block size and the length bits
+//   k_prep_scan    per layer: exclusive scan of the block sizes in rank
+//                  order, and each rank's length class [q0, q1]
+//   k_prep_tables  recs / cls / cls2 and the rank tables: inv16[rank] = edge
+//                  | first | tie; FAST and TABLE: inv32[rank] = a | b << 6 |
+//                  w << 12 | first << 18 | tie << 19; FAST: rank_of[triangle]
+//                  (0xFFFF above thresh); TABLE: cobt[e][v] = rank of
+//                  {a, b, v} from its youngest facet's block
 constexpr int kPrepEdges = 64;   // edges per block (counting: 4 slices of the edge list per edge)
 constexpr uint32_t kNoRank = 0xFFFFFFFFu;
 // inv16[rank] = edge | flags (edge < 2048 for N <= 64)
 constexpr uint32_t kInvEdge = 0x7FFu, kInvFirst = 1u << 11, kInvTie = 1u << 12, kInvRes = 1u << 13;
+// k_h1_chain variants (template MODE)
+constexpr int kChainGeneral = 0, kChainFast = 1, kChainTable = 2;
 
 __global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
-                                                    float user_thresh, DenseBufs db, int fast) {
+                                                    float user_thresh, DenseBufs db, int cmode) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
     const int e0 = blockIdx.y * kPrepEdges;
     const int E = n * (n - 1) / 2;
     const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
     float* D = (float*)(smem + 16);
-    float* lens = D + ((n * n + 3) & ~3);
-    uint32_t* part = (uint32_t*)(lens + ((E + 3) & ~3));  // [4 slices][3][64]
-    uint32_t* rk_sh = part + 4 * 3 * 64;                   // [64]
+    uint64_t* keys = (uint64_t*)(D + ((n * n + 3) & ~3));   // [E rounded to 2] (length bits, edge)
+    uint32_t* part = (uint32_t*)(keys + ((E + 1) & ~1));   // [4 slices][64]
+    uint32_t* rk_sh = part + 4 * 64;                        // [64]
     stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, 256);
-    if (fast) {  // this block's share of "every triangle above the threshold"
+    if (cmode == kChainFast) {  // this block's share of "every triangle above the threshold"
         uint32_t* ro = (uint32_t*)(db.rank_of + (size_t)l * db.tri_stride);
         const uint32_t words = db.tri_stride / 2, per = (words + gridDim.y - 1) / gridDim.y;
         const uint32_t w0 = blockIdx.y * per, w1 = min(words, w0 + per);
@@ -161,40 +168,35 @@ __global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ di
     for (int e = t; e < E; e += 256) {
         int a, b;
         edge_verts((uint32_t)e, a, b);
-        const float d = D[a * n + b];
-        lens[e] = d <= r ? d : INFINITY;
+        keys[e] = ((uint64_t)__float_as_uint(D[a * n + b]) << 32) | (uint32_t)e;
     }
+    if (t == 0 && (E & 1)) keys[E] = ~0ull;
     __syncthreads();
-    // rank = #{shorter} + #{same length, smaller index}; class = [#{shorter}, #{shorter} + #{same} - 1]
+    // rank = #{keys below}: edges above thresh have larger keys than any edge
+    // <= thresh, so counting over all edges is exact for the edges that rank
     {
         const int e = e0 + ln, sl = wv;
-        const float le = e < E ? lens[e] : INFINITY;
-        const int c0 = (E * sl) / 4, c1 = (E * (sl + 1)) / 4;
-        uint32_t nless = 0, neq = 0, neqlo = 0;
+        const uint64_t ke = e < E ? keys[e] : ~0ull;
+        const int np = (E + 1) >> 1;  // key pairs
+        const int c0 = (np * sl) / 4, c1 = (np * (sl + 1)) / 4;
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        const TDA_LDS u64x2* kp = (const TDA_LDS u64x2*)keys;
+        uint32_t cnt = 0;
+#pragma unroll 4
         for (int q = c0; q < c1; ++q) {
-            const float x = lens[q];
-            nless += x < le;
-            neq += x == le;
-            neqlo += (x == le) & (q < e);
+            const u64x2 x = kp[q];
+            cnt += (uint64_t)x.x < ke;
+            cnt += (uint64_t)x.y < ke;
         }
-        part[(sl * 3 + 0) * 64 + ln] = nless;
-        part[(sl * 3 + 1) * 64 + ln] = neq;
-        part[(sl * 3 + 2) * 64 + ln] = neqlo;
+        part[sl * 64 + ln] = cnt;
     }
     __syncthreads();
     if (t < 64) {
         const int e = e0 + t;
         uint32_t rank = kNoRank;
-        if (e < E && lens[e] != INFINITY) {
-            uint32_t nless = 0, neq = 0, neqlo = 0;
-#pragma unroll
-            for (int sl = 0; sl < 4; ++sl) {
-                nless += part[(sl * 3 + 0) * 64 + t];
-                neq += part[(sl * 3 + 1) * 64 + t];
-                neqlo += part[(sl * 3 + 2) * 64 + t];
-            }
-            rank = nless + neqlo;
-            st_glb(db.eqq + (size_t)l * db.E, (size_t)e, nless | ((nless + neq - 1) << 16));
+        if (e < E && __uint_as_float((uint32_t)(keys[e] >> 32)) <= r) {
+            rank = part[t] + part[64 + t] + part[128 + t] + part[192 + t];
+            st_glb(db.lenr + (size_t)l * (db.E + 8), (size_t)rank, (uint32_t)(keys[e] >> 32));
         }
         if (e < E) st_glb(db.epos + (size_t)l * db.E, (size_t)e, rank);
         rk_sh[t] = rank;
@@ -213,7 +215,7 @@ __global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ di
             if (e < E) edge_verts((uint32_t)e, a, b);
             av[u] = a;
             bv[u] = b;
-            lev[u] = e < E ? lens[e] : INFINITY;
+            lev[u] = e < E ? D[a * n + b] : INFINITY;
             dav[u] = ln < n ? D[a * n + ln] : 0.0f;
             dbv[u] = ln < n ? D[b * n + ln] : 0.0f;
         }
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ di
             const int li = wv * (kPrepEdges / 4) + i0 + u, e = e0 + li;
             const int a = av[u], b = bv[u], v = ln;
             const float le = lev[u];
-            bool ok = e < E && le != INFINITY && v < n && v != a && v != b && dav[u] <= le && dbv[u] <= le;
+            bool ok = e < E && le <= r && v < n && v != a && v != b && dav[u] <= le && dbv[u] <= le;
             if (ok && dav[u] == le && edge_id(a, v) < (uint32_t)e) ok = false;  // (a, v) is the younger facet
             if (ok && dbv[u] == le && edge_id(b, v) < (uint32_t)e) ok = false;
             const uint64_t m = __ballot(ok);
@@ -235,12 +237,19 @@ __global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ di
     }
 }
 
-// exclusive scan of the block sizes in rank order (one block per layer)
+// per layer: exclusive scan of the block sizes in rank order (cpos, in
+// place) and the length class of each rank: clsr[q] = first rank of the
+// class's triangles | end << 16, q0t[q] = first edge rank of the class |
+// tie << 16 (the class holds more than one edge)
 __global__ __launch_bounds__(256) void k_prep_scan(DenseBufs db, LayerStats* __restrict__ stats) {
     __shared__ uint32_t wsum[4];
+    __shared__ uint32_t offs[2048 + 8];
+    __shared__ uint32_t lens[2048 + 8];
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
     const uint32_t nE = db.necnt[l];
     uint32_t* c = db.cpos + (size_t)l * (db.E + 8);
+    const uint32_t* lr = db.lenr + (size_t)l * (db.E + 8);
+    for (uint32_t q = t; q < nE; q += 256) lens[q] = ld_glb(lr, q);
     const uint32_t per = (nE + 255) / 256, q0 = t * per;
     uint32_t loc = 0;
     for (uint32_t q = q0; q < min(nE, q0 + per); ++q) loc += ld_glb(c, q);
@@ -256,34 +265,69 @@ __global__ __launch_bounds__(256) void k_prep_scan(DenseBufs db, LayerStats* __r
     uint32_t run = base + x - loc;  // exclusive prefix of this thread's chunk
     for (uint32_t q = q0; q < min(nE, q0 + per); ++q) {
         const uint32_t v = ld_glb(c, q);
+        offs[q] = run;
         st_glb(c, q, run);
         run += v;
     }
     if (t == 255) {
         const uint32_t tot = base + x;
+        offs[nE] = tot;
         st_glb(c, nE, tot);
         stats[l].ntri = tot;
     }
+    __syncthreads();
+    for (uint32_t q = t; q < nE; q += 256) {
+        const uint32_t len = lens[q];
+        uint32_t a = q, b = q;  // classes are short except on lattice-like inputs
+        while (a > 0 && lens[a - 1] == len) --a;
+        while (b + 1 < nE && lens[b + 1] == len) ++b;
+        st_glb(db.clsr + (size_t)l * (db.E + 8), (size_t)q, offs[a] | (offs[b + 1] << 16));
+        st_glb(db.q0t + (size_t)l * (db.E + 8), (size_t)q, a | ((uint32_t)(b > a) << 16));
+    }
 }
 
-__global__ __launch_bounds__(256) void k_prep_tables(const float* __restrict__ dist, int n, DenseBufs db, int fast) {
+// tables: one wave per edge; the per-edge words of a wave's 16 edges are
+// loaded at once by lanes 0..15 and broadcast
+__global__ __launch_bounds__(256) void k_prep_tables(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
+                                                     float user_thresh, DenseBufs db, int cmode) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
     const int E = n * (n - 1) / 2;
-    const float* Dg = dist + (size_t)l * n * n;
-    const uint32_t* c = db.cpos + (size_t)l * (db.E + 8);
+    const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
+    float* D = (float*)(smem + 16);
+    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, 256);
+    const size_t ls = (size_t)l * (db.E + 8);
+    const uint32_t* c = db.cpos + ls;
+    const uint32_t* epos = db.epos + (size_t)l * db.E;
+    const uint64_t* eM = db.eM + (size_t)l * db.E;
     EdgeRec* R = db.recs + (size_t)l * db.E;
     uint16_t* c2 = db.cls2 + (size_t)l * db.n2p;
     uint16_t* inv = db.inv + (size_t)l * db.inv_stride;
     uint32_t* inv32 = db.inv32 + (size_t)l * db.inv_stride;
     uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
+    uint16_t* ct = db.cobt + (size_t)l * db.cob_stride;
+    const int eb = blockIdx.y * kPrepEdges + wv * (kPrepEdges / 4);
+    // lanes 0..15: this wave's edges
+    uint32_t rk = kNoRank, off = 0, cl = 0, qt = 0;
+    uint64_t M = 0;
+    if (ln < kPrepEdges / 4 && eb + ln < E) {
+        rk = ld_glb(epos, (size_t)(eb + ln));
+        M = ld_glb(eM, (size_t)(eb + ln));
+        if (rk != kNoRank) {
+            off = ld_glb(c, rk);
+            cl = ld_glb(db.clsr + ls, rk);
+            qt = ld_glb(db.q0t + ls, rk);
+        }
+    }
+    __syncthreads();  // D staged
     for (int i = 0; i < kPrepEdges / 4; ++i) {
-        const int e = blockIdx.y * kPrepEdges + wv * (kPrepEdges / 4) + i;
+        const int e = eb + i;
         if (e >= E) break;
         int a, b;
         edge_verts((uint32_t)e, a, b);
-        const uint32_t rk = ld_glb(db.epos + (size_t)l * db.E, (size_t)e);
-        const float len = ld_glb(Dg, (size_t)a * n + b);
-        if (rk == kNoRank) {  // above the threshold: owns no triangles
+        const uint32_t rki = (uint32_t)__builtin_amdgcn_readlane((int)rk, i);
+        const float len = D[a * n + b];
+        if (rki == kNoRank) {  // above the threshold: owns no triangles, no coboundary
             if (ln == 0) {
                 EdgeRec rec = {};
                 rec.ab = (uint16_t)(a | (b << 6));
@@ -292,57 +336,82 @@ __global__ __launch_bounds__(256) void k_prep_tables(const float* __restrict__ d
                 st_glb(c2, (size_t)a * n + b, (uint16_t)0xFFFFu);
                 st_glb(c2, (size_t)b * n + a, (uint16_t)0xFFFFu);
             }
+            if (cmode == kChainTable && ln < n) st_glb(ct, (size_t)e * n + ln, (uint16_t)0xFFFFu);
             continue;
         }
-        const uint32_t qq = ld_glb(db.eqq + (size_t)l * db.E, (size_t)e), q0 = qq & 0xFFFFu, q1 = qq >> 16;
-        const uint64_t M = ld_glb(db.eM + (size_t)l * db.E, (size_t)e);
-        const uint32_t off = ld_glb(c, rk);
-        const bool tie = q1 > q0;
+        const uint32_t offi = (uint32_t)__builtin_amdgcn_readlane((int)off, i);
+        const uint32_t cli = (uint32_t)__builtin_amdgcn_readlane((int)cl, i);
+        const uint32_t qti = (uint32_t)__builtin_amdgcn_readlane((int)qt, i);
+        const uint64_t Mi = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)M, i) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(M >> 32), i) << 32);
+        const bool tie = (qti >> 16) & 1u;
         if (ln == 0) {
             EdgeRec rec;
-            rec.M = M;
-            rec.off = (uint16_t)off;
+            rec.M = Mi;
+            rec.off = (uint16_t)offi;
             rec.ab = (uint16_t)(a | (b << 6) | ((uint32_t)tie << 12));
             rec.len = len;
             R[e] = rec;
-            st_glb(db.cls + (size_t)l * db.E, (size_t)e, ld_glb(c, q0) | (ld_glb(c, q1 + 1) << 16));
-            st_glb(c2, (size_t)a * n + b, (uint16_t)q0);
-            st_glb(c2, (size_t)b * n + a, (uint16_t)q0);
+            st_glb(db.cls + (size_t)l * db.E, (size_t)e, cli);
+            st_glb(c2, (size_t)a * n + b, (uint16_t)(qti & 0xFFFFu));
+            st_glb(c2, (size_t)b * n + a, (uint16_t)(qti & 0xFFFFu));
         }
-        if ((uint32_t)ln < (uint32_t)__popcll(M))
-            st_glb(inv, off + ln, (uint16_t)(e | (ln == 0 ? kInvFirst : 0u) | (tie ? kInvTie : 0u)));
-        if (fast && ln < n && ((M >> ln) & 1ull)) {
-            const uint32_t q = off + bits_above(M, ln);
-            st_glb(inv32, q, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(q == off) << 18) | ((uint32_t)tie << 19));
-            st_glb(ro, tri_id(a, b, ln), (uint16_t)q);
+        if ((uint32_t)ln < (uint32_t)__popcll(Mi))
+            st_glb(inv, offi + ln, (uint16_t)(e | (ln == 0 ? kInvFirst : 0u) | (tie ? kInvTie : 0u)));
+        if (cmode != kChainGeneral && ln < n && ((Mi >> ln) & 1ull)) {
+            const uint32_t q = offi + bits_above(Mi, ln);
+            st_glb(inv32, q, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(q == offi) << 18) | ((uint32_t)tie << 19));
+            if (cmode == kChainFast) st_glb(ro, tri_id(a, b, ln), (uint16_t)q);
         }
     }
-}
-
-// coboundary table of the TABLE chain: cobt[e * n + v] = rank of {a, b, v}
-// (0xFFFF: v in {a, b} or above thresh); one wave per edge, 4 edges in flight
-__global__ __launch_bounds__(256) void k_prep_cob(int n, DenseBufs db) {
-    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
-    const int E = n * (n - 1) / 2;
-    const uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
-    uint16_t* ct = db.cobt + (size_t)l * db.cob_stride;
-    for (int i0 = 0; i0 < kPrepEdges / 4; i0 += 4) {
-        uint16_t v16[4];
-        int ev[4];
+    if (cmode != kChainTable) return;
+    // coboundary rows: lane v of edge (a, b) -> rank of {a, b, v} = off(e') +
+    // bits_above(M_e', third), e' its youngest facet (longest edge, ties ->
+    // smallest index); two dependent gathers, 8 edges in flight
+    for (int i0 = 0; i0 < kPrepEdges / 4; i0 += 8) {
+        uint32_t pe[8], th[8];
+        uint64_t pm[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e = blockIdx.y * kPrepEdges + wv * (kPrepEdges / 4) + i0 + u;
-            ev[u] = e;
-            v16[u] = 0xFFFFu;
+        for (int u = 0; u < 8; ++u) {
+            const int e = eb + i0 + u;
+            pe[u] = kNoRank;
+            th[u] = 0;
+            pm[u] = 0;
             if (e < E && ln < n) {
                 int a, b;
                 edge_verts((uint32_t)e, a, b);
-                if (ln != a && ln != b) v16[u] = ld_glb(ro, tri_id(a, b, ln));
+                const int v = ln;
+                const float le = D[a * n + b], dav = D[a * n + v], dbv = D[b * n + v];
+                if (v != a && v != b && fmaxf(le, fmaxf(dav, dbv)) <= r) {
+                    float bl = le;
+                    uint32_t be = (uint32_t)e;
+                    int third = v;
+                    const uint32_t eav = edge_id(a, v), ebv = edge_id(b, v);
+                    if (dav > bl || (dav == bl && eav < be)) {
+                        bl = dav;
+                        be = eav;
+                        third = b;
+                    }
+                    if (dbv > bl || (dbv == bl && ebv < be)) {
+                        bl = dbv;
+                        be = ebv;
+                        third = a;
+                    }
+                    pe[u] = ld_glb(epos, (size_t)be);
+                    pm[u] = ld_glb(eM, (size_t)be);
+                    th[u] = (uint32_t)third;
+                }
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (ev[u] < E && ln < n) st_glb(ct, (size_t)ev[u] * n + ln, v16[u]);
+        for (int u = 0; u < 8; ++u) pe[u] = pe[u] != kNoRank ? ld_glb(c, pe[u]) : kNoRank;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int e = eb + i0 + u;
+            if (e < E && ln < n)
+                st_glb(ct, (size_t)e * n + ln,
+                       (uint16_t)(pe[u] != kNoRank ? pe[u] + bits_above(pm[u], (int)th[u]) : 0xFFFFu));
+        }
     }
 }
 
@@ -360,7 +429,6 @@ __global__ __launch_bounds__(256) void k_prep_cob(int n, DenseBufs db) {
 //   kChainFast (N <= ~51): rank_of[triangle] + inv32 in LDS.
 //   kChainGeneral: edge records (youngest facet, block mask) + inv16.
 // LDS: [16][D][recs E | rank_of | cobt][inv16 | inv32][W 64K][res 64K][piv][cols][own].
-constexpr int kChainGeneral = 0, kChainFast = 1, kChainTable = 2;
 template <int K, int MODE>
 __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
                                                       DimBufs b, Reduce2Bufs rb, DenseBufs db, uint64_t step_limit,

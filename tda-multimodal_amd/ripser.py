@@ -26,26 +26,33 @@ from . import _lib
 class _Batch:
     """Host copies of one batched call's outputs; LayerResults are views into it."""
 
-    __slots__ = ("L", "nd", "N", "pairs", "bounds", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist")
+    __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist")
 
 
 class LayerResult:
     """Persistence of one layer (all arrays on the host).
 
-    ``dgms`` (list of (n_k, 2) float64 arrays, ripser's emission order) is
-    built eagerly; the remaining fields are views into the batch's shared
-    arrays, materialised on access.
+    ``dgms`` (list of (n_k, 2) float64 arrays, ripser's emission order) and
+    the other fields are views into the batch's shared arrays, made on first
+    access.
     """
 
-    __slots__ = ("dgms", "_b", "_l")
+    __slots__ = ("_dgms", "_b", "_l")
 
-    def __init__(self, dgms, batch, layer):
-        self.dgms = dgms
+    def __init__(self, batch, layer):
+        self._dgms = None
         self._b = batch
         self._l = layer
 
     def _seg(self, arr):
-        return [arr[a:e] for a, e in self._b.bounds[self._l]]
+        b = self._b
+        return [arr[o:o + c] for o, c in zip(b.off[self._l].tolist(), b.cnt[self._l].tolist())]
+
+    @property
+    def dgms(self) -> list:
+        if self._dgms is None:
+            self._dgms = self._seg(self._b.pairs)
+        return self._dgms
 
     @property
     def birth_idx(self):
@@ -99,28 +106,27 @@ def _unpack(res_p, want_dist: bool) -> tuple[list, dict]:
     r = res_p.contents
     L, md, N = int(r.L), int(r.maxdim), int(r.N)
     nd = md + 1
+    S = L * nd
     b = _Batch()
     b.L, b.nd, b.N = L, nd, N
-    cnt = _arr(r.count, L * nd, np.int64)
-    off = _arr(r.offset, L * nd, np.int64)
-    total = int(cnt.sum())
-    # one (total, 2) float64 block; every diagram is a view into it
+    # count .. n_adds: seven consecutive [L][nd] blocks (tda_rips.h layout guarantee)
+    meta = _arr(r.count, 7 * S, np.int64).reshape(7, L, nd)
+    b.cnt, b.off = meta[0], meta[1]
+    b.cs = meta[2].view(np.uint64)
+    b.na, b.nc, b.nr, b.nadd = meta[3], meta[4], meta[5], meta[6]
+    total = int(b.cnt.sum())
+    # birth | death -> one (total, 2) float64 block; every diagram is a view into it
+    bd = _arr(r.birth, 2 * total, np.float32)
     pairs = np.empty((total, 2), dtype=np.float64)
-    pairs[:, 0] = _arr(r.birth, total, np.float32)
-    pairs[:, 1] = _arr(r.death, total, np.float32)
+    pairs[:, 0] = bd[:total]
+    pairs[:, 1] = bd[total:]
     b.pairs = pairs
-    b.bidx = _arr(r.birth_idx, total, np.int64)
-    b.didx = _arr(r.death_idx, total, np.int64)
+    idx = _arr(r.birth_idx, 2 * total, np.int64)
+    b.bidx, b.didx = idx[:total], idx[total:]
     b.thr = _arr(r.thresh, L, np.float32)
     b.ne = _arr(r.num_edges, L, np.int64)
-    b.cs = _arr(r.checksum, L * nd, np.uint64).reshape(L, nd)
-    b.na = _arr(r.n_all_pairs, L * nd, np.int64).reshape(L, nd)
-    b.nc = _arr(r.n_columns, L * nd, np.int64).reshape(L, nd)
-    b.nr = _arr(r.n_residual, L * nd, np.int64).reshape(L, nd)
-    b.nadd = _arr(r.n_adds, L * nd, np.int64).reshape(L, nd)
     b.dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N) if want_dist and bool(r.dist) else None
-    b.bounds = np.stack([off, off + cnt], axis=1).reshape(L, nd, 2).tolist()
-    out = [LayerResult([pairs[a:e] for a, e in bl], b, l) for l, bl in enumerate(b.bounds)]
+    out = [LayerResult(b, l) for l in range(L)]
     stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(int(r.n_stages))]
     return out, {"device_ms": float(r.device_ms), "stages": stages}
 
