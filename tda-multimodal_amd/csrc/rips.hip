@@ -431,7 +431,7 @@ int set_lds_attrs(int dev) {
     if (dev < 64 && g_attr_done[dev]) return 0;
     HIPC(hipFuncSetAttribute((const void*)k_h0, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_sort_resid, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    HIPC(hipFuncSetAttribute((const void*)k_finalize, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds));
 #define TDA_ATTR_RED(LW, P1, P2) \
     HIPC(hipFuncSetAttribute((const void*)k_reduce_all<LW, P1, P2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax))
     TDA_ATTR_RED(true, true, true);
@@ -625,7 +625,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         if (int rc = tm2.begin()) return rc;
         if (int rc = tm4.begin()) return rc;
         if (n <= kSmallN) {
-            hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s4, dist, n, a.thresh, stats,
+            hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s4, dist, n, rowmax, a.thresh, stats,
                                (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
         } else {
             int T = n <= 256 ? 256 : 1024;
@@ -692,7 +692,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     auto launch_apparent = [&](int d, hipStream_t st) {
         uint64_t blocks = (p.ncand[d] + 255) / 256;
-        unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, 4096 / L)));
+        // total blocks over all layers: measured (r01, sweep48) 1024 beats 4096,
+        // whose grid holds every CU while the critical small kernels wait
+        static const uint64_t app_total = getenv("TDA_APP_GRID") ? strtoull(getenv("TDA_APP_GRID"), nullptr, 10) : 1024;
+        unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, app_total / L)));
         const bool dl = n <= kAppLdsMaxN;
         const size_t alds = 16 + (dl ? (size_t)n * n * 4 : 0);
         if (d == 1) {
@@ -850,18 +853,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
 
-    // ---- emission order + compaction into host-mapped memory
-    if (p.maxdim >= 1) {
-        hipLaunchKernelGGL(k_finalize, dim3(L), dim3(1024), 8192 * 12, s, stats, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
-                           (uint32_t*)(B + p.o_fv), p.sstride, 13);
-        HIPC(hipGetLastError());
-        MARK("k_finalize");
-    }
-    const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
-    hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, w.houtoff_dev, w.hout_dev,
-                       (uint64_t)w.hout_cap, w.hstats_dev);
+    // ---- emission order, straight into host-mapped memory
+    hipLaunchKernelGGL(k_emit, dim3(L), dim3(1024), kEmitLds, s, stats, L, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
+                       (uint32_t*)(B + p.o_fv), p.sstride, w.houtoff_dev, w.hout_dev, (uint64_t)w.hout_cap, w.hstats_dev);
     HIPC(hipGetLastError());
-    MARK("k_compact");
+    MARK("k_emit");
     HIPC(rec_t(w.ev1));
     return 0;
     };  // enqueue
@@ -903,9 +899,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         if (int rc = grow_hout(w, need + 16)) return rc;
         for (int l = 0; l < L; ++l) w.hstats[l].err = 0;
         HIPC(hipMemcpyAsync(stats, w.hstats, sizeof(LayerStats) * L, hipMemcpyHostToDevice, s));
-        const size_t clds = align_up(((size_t)L * (p.maxdim + 1) + 1) * 8, 16);
-        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), clds, s, stats, L, p.maxdim, ps, w.houtoff_dev, w.hout_dev,
-                           (uint64_t)w.hout_cap, w.hstats_dev);
+        hipLaunchKernelGGL(k_emit, dim3(L), dim3(1024), kEmitLds, s, stats, L, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
+                           (uint32_t*)(B + p.o_fv), p.sstride, w.houtoff_dev, w.hout_dev, (uint64_t)w.hout_cap, w.hstats_dev);
         HIPC(hipGetLastError());
         HIPC(hipStreamSynchronize(s));
         errs = 0;
@@ -953,6 +948,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 mx = w.hstats[l].prof[1][2];
                 mxa = w.hstats[l].prof[1][3] & 0xFFFF;
             }
+        }
+        {
+            const uint64_t* h = w.hstats[0].prof[3];
+            fprintf(stderr, "[tda-prof] k_h0_wave layer 0 (cycles from entry): thresh %llu prim %llu sort %llu unionfind %llu end %llu; chain staging (slowest layer) %llu\n",
+                    (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4],
+                    (unsigned long long)h[5], (unsigned long long)q[6]);
         }
         fprintf(stderr, "[tda-prof] H2 phase 1: all columns %llu cycles (scan %llu cob %llu), %llu adds; slowest column %llu cycles (%llu adds)\n",
                 (unsigned long long)tt, (unsigned long long)sc, (unsigned long long)cb, (unsigned long long)ad, (unsigned long long)mx,

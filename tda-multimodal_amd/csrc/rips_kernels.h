@@ -464,29 +464,44 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
 // owns vertex v; Prim's frontier keys live in registers, the arg-min vertex is
 // found by ballot (no index decode); the <= 63 forest edges are sorted with an
 // in-register bitonic network.  Same results as k_h0.
-__global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, int n, float user_thresh,
-                                                LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
+__global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
+                                                float user_thresh, LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
                                                 uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, v = threadIdx.x;
+    // enclosing radius = min over rows of the row maxima k_distance folded in
+    const uint32_t rmv = v < n ? ld_glb(rowmax + (size_t)l * n, (size_t)v) : 0xFFFFFFFFu;
     float* D = (float*)smem;              // n*n
     const float* Dg = dist + (size_t)l * n * n;
     stage_to_lds(D, Dg, sizeof(float) * n * n, v, 64);
     __syncthreads();
     LayerStats* st = stats + l;
     const bool real = v < n;
+#ifdef TDA_PROFILE
+    const uint64_t tp0 = clock64();
+#define TDA_H0_MARK(i) \
+    if (v == 0) st->prof[3][i] = clock64() - tp0;
+#else
+#define TDA_H0_MARK(i)
+#endif
+    TDA_H0_MARK(0)
     float thr = user_thresh;
-    if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) {
-        float rm = real ? 0.0f : INFINITY;
-        if (real)
-            for (int j = 0; j < n; ++j) rm = fmaxf(rm, D[v * n + j]);
-        for (int m = 32; m >= 1; m >>= 1) rm = fminf(rm, __shfl_xor(rm, m, 64));
-        thr = rm;
-    }
+    if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) thr = n == 1 ? 0.0f : __uint_as_float(wave_min_u32(rmv));
+    // D is symmetric: lane v counts column v below the diagonal, 8 loads in flight
     uint64_t ne = 0;
     if (real)
-        for (int j = v + 1; j < n; ++j) ne += D[v * n + j] <= thr;
+        for (int j0 = v + 1; j0 < n; j0 += 8) {
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = j0 + u < n ? D[(j0 + u) * n + v] : INFINITY;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) ne += x[u] <= thr;
+        }
     ne = wave_sum_u64(ne);
+    TDA_H0_MARK(1)
+    // Prim: lane v keeps its best tree edge as a filtration key (diam, then
+    // index desc); the arg-min is a 32-bit min over the diameter bits, and a
+    // second one over the index word only when diameters tie
     bool intree = v == 0;
     uint64_t best = kEmpty64;
     int cur = 0;
@@ -494,26 +509,35 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
     int nmst = 0;
     for (int it = 1; it < n; ++it) {
         if (real && !intree) {
-            float d = D[cur * n + v];
+            const float d = D[cur * n + v];
             if (d <= thr) {
-                int a = cur > v ? cur : v, bb = cur > v ? v : cur;
-                uint64_t k = filt_key(d, binom((uint64_t)a, 2) + bb);
+                const uint32_t a = (uint32_t)max(cur, v), bb = (uint32_t)min(cur, v);
+                const uint64_t k = filt_key(d, (uint64_t)(a * (a - 1) / 2 + bb));
                 best = k < best ? k : best;
             }
         }
-        uint64_t cand = (real && !intree) ? best : kEmpty64;
-        uint64_t m = wave_min_u64(cand);
+        const bool live = real && !intree;
+        const uint32_t hi = live ? (uint32_t)(best >> 32) : 0xFFFFFFFFu;
+        const uint32_t mh = wave_min_u32(hi);
         int nv;
-        if (m == kEmpty64) {
-            nv = __builtin_ctzll(__ballot(real && !intree));  // new component
+        if (mh == 0xFFFFFFFFu) {
+            nv = __builtin_ctzll(__ballot(live));  // new component
         } else {
-            nv = __builtin_ctzll(__ballot(real && !intree && cand == m));
+            uint64_t cm = __ballot(live && hi == mh);
+            if (__popcll(cm) > 1) {  // equal diameters: smallest index word = largest edge index
+                const uint32_t lo = (live && hi == mh) ? (uint32_t)best : 0xFFFFFFFFu;
+                const uint32_t ml = wave_min_u32(lo);
+                cm = __ballot(live && hi == mh && (uint32_t)best == ml);
+            }
+            nv = __builtin_ctzll(cm);
+            const uint64_t m = ((uint64_t)mh << 32) | (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)best, nv);
             if (v == nmst) mykey = m;
             ++nmst;
         }
         if (v == nv) intree = true;
         cur = nv;
     }
+    TDA_H0_MARK(2)
     // bitonic sort of the forest keys (one per lane, EMPTY padding)
     uint64_t k = mykey;
 #pragma unroll
@@ -527,6 +551,7 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
             k = (lower == up) ? lo : hi;
         }
     }
+    TDA_H0_MARK(3)
     // lane e now holds the e-th forest edge in Kruskal order (diam asc, idx desc)
     const bool has = v < nmst;
     const uint64_t eidx = has ? 0xFFFFFFFFull - (k & 0xFFFFFFFFull) : 0;
@@ -548,6 +573,7 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
         if (label == young) label = old;
         if (v == e) young_e = young;
     }
+    TDA_H0_MARK(4)
     // emission: finite bars (d > 0) in Kruskal order, then [0, inf) per root
     Pair* P = pairs0 + (size_t)l * pcap0;
     const uint64_t posm = __ballot(has && d > 0.0f);
@@ -564,6 +590,8 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
         st->all_pairs[0] = nmst;
         st->n_columns[0] = n;
     }
+    TDA_H0_MARK(5)
+#undef TDA_H0_MARK
 }
 
 // ------------------------------------------------------------------ apparent
@@ -793,6 +821,82 @@ __global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats
         OutPair* o = out + off[i];
         for (int64_t e = ln; e < c; e += 64) o[e] = OutPair{P[e].birth, P[e].death, P[e].birth_idx, P[e].death_idx};
     }
+}
+
+// ------------------------------------------------------------------ emit
+// k_finalize + k_compact in one launch: block l sorts its layer's dims >= 1
+// into emission order and writes every segment straight into the host-mapped
+// output at its global offset (a prefix over the stats' counts, recomputed
+// per block), then its LayerStats.  LDS: the sort chunk (8 KiB keys * 12 B)
+// and 16 x 2 words of reduction scratch behind it.
+constexpr int kEmitSortLog2 = 13;
+constexpr size_t kEmitLds = (size_t(12) << kEmitSortLog2) + 16 * 2 * 8;
+__global__ __launch_bounds__(1024) void k_emit(LayerStats* __restrict__ stats, int L, int maxdim, PairSet ps, uint64_t* __restrict__ skeys,
+                                               uint32_t* __restrict__ svals, uint64_t sstride, int64_t* __restrict__ out_off,
+                                               OutPair* __restrict__ out, uint64_t out_cap, LayerStats* __restrict__ stats_host) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, t = threadIdx.x, nd = maxdim + 1;
+    constexpr uint64_t CH = 1ull << kEmitSortLog2;
+    uint64_t* sk = (uint64_t*)smem;
+    uint32_t* sv = (uint32_t*)(sk + CH);
+    uint64_t* red = (uint64_t*)(smem + CH * 12);  // [16][2]
+    auto cnt_of = [&](int ll, int d) -> uint64_t {
+        const uint64_t c = (uint64_t)stats[ll].count[d];
+        return c > ps.cap[d] ? ps.cap[d] : c;
+    };
+    uint64_t before = 0, total = 0;
+    for (int i = t; i < L * nd; i += blockDim.x) {
+        const uint64_t c = cnt_of(i / nd, i % nd);
+        total += c;
+        before += i < l * nd ? c : 0;
+    }
+    before = wave_sum_u64(before);
+    total = wave_sum_u64(total);
+    if ((t & 63) == 0) {
+        red[(t >> 6) * 2] = before;
+        red[(t >> 6) * 2 + 1] = total;
+    }
+    __syncthreads();
+    before = 0;
+    total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        before += red[w * 2];
+        total += red[w * 2 + 1];
+    }
+    const bool over = total > out_cap;
+    uint64_t o = before;
+    for (int d = 0; d < nd; ++d) {
+        const uint64_t cnt = cnt_of(l, d);
+        if (t == 0) out_off[l * nd + d] = (int64_t)o;
+        if (!over) {
+            const Pair* P = ps.p[d] + (size_t)l * ps.cap[d];
+            OutPair* dst = out + o;
+            if (d == 0 || cnt < 2) {
+                for (uint64_t e = t; e < cnt; e += blockDim.x) dst[e] = OutPair{P[e].birth, P[e].death, P[e].birth_idx, P[e].death_idx};
+            } else {
+                uint64_t* k = skeys + (size_t)l * sstride * 2;
+                uint32_t* v = svals + (size_t)l * sstride * 2;
+                for (uint64_t e = t; e < cnt; e += blockDim.x) {
+                    k[e] = col_key(P[e].birth, (uint64_t)P[e].birth_idx);
+                    v[e] = (uint32_t)e;
+                }
+                __syncthreads();
+                block_sort<true>(k, v, cnt, k + sstride, v + sstride, sk, sv, kEmitSortLog2);
+                for (uint64_t e = t; e < cnt; e += blockDim.x) {
+                    const Pair q = P[v[e]];
+                    dst[e] = OutPair{q.birth, q.death, q.birth_idx, q.death_idx};
+                }
+                __syncthreads();  // k / v are reused by the next dim
+            }
+        }
+        o += cnt;
+    }
+    if (over && t == 0) stats[l].err |= ERR_OUT_CAP;
+    __syncthreads();
+    static_assert(sizeof(LayerStats) % 8 == 0, "LayerStats copies as u64 words");
+    const uint64_t* src = (const uint64_t*)(stats + l);
+    uint64_t* dstS = (uint64_t*)(stats_host + l);
+    for (int i = t; i < (int)(sizeof(LayerStats) / 8); i += blockDim.x) dstS[i] = src[i];
 }
 
 }  // namespace tda

@@ -436,6 +436,9 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool FAST = MODE == kChainFast, TABLE = MODE == kChainTable, GEN = MODE == kChainGeneral;
     constexpr uint32_t WP = 64u * K;
+#ifdef TDA_PROFILE
+    const uint64_t t_entry = clock64();
+#endif
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
     LayerStats* st = stats + l;
     const int E = n * (n - 1) / 2;
@@ -819,6 +822,7 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
 #ifdef TDA_PROFILE
         prof[0] = clock64() - t_all;
         prof[2] = ties;
+        prof[6] = t_all - t_entry;  // staging + column filter
         for (int i = 0; i < 8; ++i) st->prof[0][i] = prof[i];
 #endif
         if (err == 1) atomicOr(&st->err, ERR_LDS_SPILL);
