@@ -755,16 +755,28 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // on a third stream beside the H1 chain; they only need apparent<1>'s
     // pivot bitmap, and the chain records its residual pivots separately
     const bool split2 = p.dense && p.maxdim >= 2;
-    if (p.maxdim < 1)
+    // capture order of the launches (the graph executor dispatches in it):
+    // TDA_ORDER=0 apparent<1> first; 1 side streams first; 2 side streams
+    // first and the H2 branch after the triangle ranks; 3 side streams first,
+    // sort<1> enqueued before the H2 branch
+    static const int order = getenv("TDA_ORDER") ? atoi(getenv("TDA_ORDER")) : 3;  // 3: measured best (r01)
+    if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
     if (p.maxdim >= 1) {
         launch_apparent(1, s);
         HIPC(hipGetLastError());
         MARK("k_apparent<1>");
-        if (int rc = launch_side()) return rc;
+        if (order == 0)
+            if (int rc = launch_side()) return rc;
         if (split2) {
             HIPC(hipEventRecord(w.evs, s));
+            if (order == 3) {
+                launch_sort(1, 1, s);
+                HIPC(hipGetLastError());
+                MARK("k_sort_resid<1>");
+            }
             HIPC(hipStreamWaitEvent(w.stream3, w.evs, 0));
+            if (order == 2) HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));
             if (int rc = tm3.begin()) return rc;
             launch_apparent(2, w.stream3);
             HIPC(hipGetLastError());
@@ -779,9 +791,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipGetLastError());
             if (int rc = tm3.mark("k_h2_phase1")) return rc;
             HIPC(hipEventRecord(w.evp, w.stream3));
-            launch_sort(1, 1, s);
-            HIPC(hipGetLastError());
-            MARK("k_sort_resid<1>");
+            if (order != 3) {
+                launch_sort(1, 1, s);
+                HIPC(hipGetLastError());
+                MARK("k_sort_resid<1>");
+            }
         } else {
             for (int d = 2; d <= p.maxdim; ++d) {
                 launch_apparent(d, s);

@@ -664,8 +664,42 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
                 break;
             }
             TDA_STAMP(t1);
-            uint32_t rk, qv = 0;
-            const bool found = first_bit_from(lo, rk, qv);
+            uint32_t rk = 0, qv = 0;
+            bool found;
+            if constexpr (TABLE) {
+                // apparent run: window pivot -> inv16 -> coboundary row, for
+                // as long as the pivot is the first triangle of a non-tie,
+                // non-residual block (one ballot, two scalar reads per step)
+                found = false;
+                bool win = true;
+                while (step < step_limit) {
+                    const uint32_t w0 = lo >> 5, wi = w0 + (uint32_t)ln;
+                    uint32_t x = wi < WP ? ld_lds(W, wi) : 0u;
+                    if (ln == 0) x &= ~0u << (lo & 31);
+                    const uint64_t m = __ballot(x != 0u);
+                    if (!m) {
+                        win = false;
+                        break;
+                    }
+                    const int f = __builtin_ctzll(m);
+                    const uint32_t wd = (uint32_t)__builtin_amdgcn_readlane((int)x, f);
+                    rk = ((w0 + (uint32_t)f) << 5) + (uint32_t)__builtin_ctz(wd);
+                    qv = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_lds(inv, rk));
+                    if ((qv & (kInvFirst | kInvTie | kInvRes)) != kInvFirst) {
+                        found = true;
+                        break;
+                    }
+                    lo = rk + 1;  // the added column starts at rk, which cancels
+                    cob_e(qv & kInvEdge);
+                    ++nadds;
+                    ++step;
+                    lds_order();
+                }
+                if (step >= step_limit) continue;  // the loop head reports it
+                if (!win) found = first_bit(rk, qv);
+            } else {
+                found = first_bit_from(lo, rk, qv);
+            }
 #ifdef TDA_PROFILE
             prof[7] += 1;
 #endif
