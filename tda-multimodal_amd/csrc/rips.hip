@@ -451,6 +451,7 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_CHAIN(9, 2) TDA_ATTR_CHAIN(12, 2)
 #undef TDA_ATTR_CHAIN
     HIPC(hipFuncSetAttribute((const void*)k_prep_edges, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_prep_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)prep_tables_lds(kDenseMaxN)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -670,8 +671,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             hipLaunchKernelGGL(k_prep_scan, dim3(L), dim3(256), 0, s2, dnb, stats);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_scan")) return rc;
-            hipLaunchKernelGGL(k_prep_tables, pg, dim3(256), 16 + align_up(4ull * n * n, 16), s2, dist, n, rowmax, a.thresh, dnb,
-                               p.cmode);
+            hipLaunchKernelGGL(k_prep_tables, dim3(L, kPrepTabBlocks), dim3(kPrepTabT), prep_tables_lds(n), s2, dist, n, dnb, p.cmode);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_tables")) return rc;
         }

@@ -286,48 +286,51 @@ __global__ __launch_bounds__(256) void k_prep_scan(DenseBufs db, LayerStats* __r
     }
 }
 
-// tables: one wave per edge; the per-edge words of a wave's 16 edges are
-// loaded at once by lanes 0..15 and broadcast
-__global__ __launch_bounds__(256) void k_prep_tables(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
-                                                     float user_thresh, DenseBufs db, int cmode) {
+// tables: kPrepTabBlocks blocks of 1024 threads per layer.  Every block
+// stages the layer's per-edge words (rank, block mask) and per-rank words
+// (first triangle rank, class range, class start) in LDS, so the
+// coboundary rows' youngest-facet lookups are LDS gathers; then one wave per
+// edge writes its record, class words and rank-table entries, and (TABLE)
+// its coboundary row, lane v -> rank of {a, b, v}.
+constexpr int kPrepTabBlocks = 4;
+constexpr int kPrepTabT = 1024;
+__host__ __device__ constexpr size_t prep_tables_lds(int n) {
+    return 16 + (((size_t)4 * n * n + 15) & ~(size_t)15) + (size_t)(n * (n - 1) / 2 + 8) * (8 + 4 + 4 + 4 + 4);
+}
+__global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restrict__ dist, int n, DenseBufs db, int cmode) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    constexpr int NW = kPrepTabT / 64;
     const int E = n * (n - 1) / 2;
-    const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
+    const int ES = E + 8;
     float* D = (float*)(smem + 16);
-    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, 256);
-    const size_t ls = (size_t)l * (db.E + 8);
-    const uint32_t* c = db.cpos + ls;
-    const uint32_t* epos = db.epos + (size_t)l * db.E;
-    const uint64_t* eM = db.eM + (size_t)l * db.E;
-    EdgeRec* R = db.recs + (size_t)l * db.E;
+    uint64_t* Ms = (uint64_t*)(smem + 16 + (((size_t)4 * n * n + 15) & ~(size_t)15));  // [E] by edge
+    uint32_t* ep = (uint32_t*)(Ms + ES);                                             // [E] edge -> rank
+    uint32_t* fr = ep + ES;                                                          // [nE + 1] rank -> first triangle rank
+    uint32_t* cl = fr + ES;                                                          // [nE] rank -> class triangle range
+    uint32_t* qt = cl + ES;                                                          // [nE] rank -> class start | tie << 16
+    const size_t lE = (size_t)l * db.E, lS = (size_t)l * (db.E + 8);
+    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, kPrepTabT);
+    for (int e = t; e < E; e += kPrepTabT) {
+        Ms[e] = ld_glb(db.eM + lE, (size_t)e);
+        ep[e] = ld_glb(db.epos + lE, (size_t)e);
+        fr[e] = ld_glb(db.cpos + lS, (size_t)e);
+        cl[e] = ld_glb(db.clsr + lS, (size_t)e);
+        qt[e] = ld_glb(db.q0t + lS, (size_t)e);
+    }
+    __syncthreads();
+    EdgeRec* R = db.recs + lE;
     uint16_t* c2 = db.cls2 + (size_t)l * db.n2p;
     uint16_t* inv = db.inv + (size_t)l * db.inv_stride;
     uint32_t* inv32 = db.inv32 + (size_t)l * db.inv_stride;
     uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
     uint16_t* ct = db.cobt + (size_t)l * db.cob_stride;
-    const int eb = blockIdx.y * kPrepEdges + wv * (kPrepEdges / 4);
-    // lanes 0..15: this wave's edges
-    uint32_t rk = kNoRank, off = 0, cl = 0, qt = 0;
-    uint64_t M = 0;
-    if (ln < kPrepEdges / 4 && eb + ln < E) {
-        rk = ld_glb(epos, (size_t)(eb + ln));
-        M = ld_glb(eM, (size_t)(eb + ln));
-        if (rk != kNoRank) {
-            off = ld_glb(c, rk);
-            cl = ld_glb(db.clsr + ls, rk);
-            qt = ld_glb(db.q0t + ls, rk);
-        }
-    }
-    __syncthreads();  // D staged
-    for (int i = 0; i < kPrepEdges / 4; ++i) {
-        const int e = eb + i;
-        if (e >= E) break;
+    for (int e = blockIdx.y * NW + wv; e < E; e += kPrepTabBlocks * NW) {
         int a, b;
         edge_verts((uint32_t)e, a, b);
-        const uint32_t rki = (uint32_t)__builtin_amdgcn_readlane((int)rk, i);
+        const uint32_t rk = ep[e];
         const float len = D[a * n + b];
-        if (rki == kNoRank) {  // above the threshold: owns no triangles, no coboundary
+        if (rk == kNoRank) {  // above the threshold: owns no triangles, no coboundary
             if (ln == 0) {
                 EdgeRec rec = {};
                 rec.ab = (uint16_t)(a | (b << 6));
@@ -339,78 +342,52 @@ __global__ __launch_bounds__(256) void k_prep_tables(const float* __restrict__ d
             if (cmode == kChainTable && ln < n) st_glb(ct, (size_t)e * n + ln, (uint16_t)0xFFFFu);
             continue;
         }
-        const uint32_t offi = (uint32_t)__builtin_amdgcn_readlane((int)off, i);
-        const uint32_t cli = (uint32_t)__builtin_amdgcn_readlane((int)cl, i);
-        const uint32_t qti = (uint32_t)__builtin_amdgcn_readlane((int)qt, i);
-        const uint64_t Mi = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)M, i) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(M >> 32), i) << 32);
-        const bool tie = (qti >> 16) & 1u;
+        const uint64_t M = Ms[e];
+        const uint32_t off = fr[rk], q = qt[rk];
+        const bool tie = (q >> 16) & 1u;
         if (ln == 0) {
             EdgeRec rec;
-            rec.M = Mi;
-            rec.off = (uint16_t)offi;
+            rec.M = M;
+            rec.off = (uint16_t)off;
             rec.ab = (uint16_t)(a | (b << 6) | ((uint32_t)tie << 12));
             rec.len = len;
             R[e] = rec;
-            st_glb(db.cls + (size_t)l * db.E, (size_t)e, cli);
-            st_glb(c2, (size_t)a * n + b, (uint16_t)(qti & 0xFFFFu));
-            st_glb(c2, (size_t)b * n + a, (uint16_t)(qti & 0xFFFFu));
+            st_glb(db.cls + lE, (size_t)e, cl[rk]);
+            st_glb(c2, (size_t)a * n + b, (uint16_t)(q & 0xFFFFu));
+            st_glb(c2, (size_t)b * n + a, (uint16_t)(q & 0xFFFFu));
         }
-        if ((uint32_t)ln < (uint32_t)__popcll(Mi))
-            st_glb(inv, offi + ln, (uint16_t)(e | (ln == 0 ? kInvFirst : 0u) | (tie ? kInvTie : 0u)));
-        if (cmode != kChainGeneral && ln < n && ((Mi >> ln) & 1ull)) {
-            const uint32_t q = offi + bits_above(Mi, ln);
-            st_glb(inv32, q, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(q == offi) << 18) | ((uint32_t)tie << 19));
-            if (cmode == kChainFast) st_glb(ro, tri_id(a, b, ln), (uint16_t)q);
+        if ((uint32_t)ln < (uint32_t)__popcll(M))
+            st_glb(inv, off + ln, (uint16_t)(e | (ln == 0 ? kInvFirst : 0u) | (tie ? kInvTie : 0u)));
+        if (cmode != kChainGeneral && ln < n && ((M >> ln) & 1ull)) {
+            const uint32_t r2 = off + bits_above(M, ln);
+            st_glb(inv32, r2, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(r2 == off) << 18) | ((uint32_t)tie << 19));
+            if (cmode == kChainFast) st_glb(ro, tri_id(a, b, ln), (uint16_t)r2);
         }
-    }
-    if (cmode != kChainTable) return;
-    // coboundary rows: lane v of edge (a, b) -> rank of {a, b, v} = off(e') +
-    // bits_above(M_e', third), e' its youngest facet (longest edge, ties ->
-    // smallest index); two dependent gathers, 8 edges in flight
-    for (int i0 = 0; i0 < kPrepEdges / 4; i0 += 8) {
-        uint32_t pe[8], th[8];
-        uint64_t pm[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = eb + i0 + u;
-            pe[u] = kNoRank;
-            th[u] = 0;
-            pm[u] = 0;
-            if (e < E && ln < n) {
-                int a, b;
-                edge_verts((uint32_t)e, a, b);
-                const int v = ln;
-                const float le = D[a * n + b], dav = D[a * n + v], dbv = D[b * n + v];
-                if (v != a && v != b && fmaxf(le, fmaxf(dav, dbv)) <= r) {
-                    float bl = le;
-                    uint32_t be = (uint32_t)e;
-                    int third = v;
-                    const uint32_t eav = edge_id(a, v), ebv = edge_id(b, v);
-                    if (dav > bl || (dav == bl && eav < be)) {
-                        bl = dav;
-                        be = eav;
-                        third = b;
-                    }
-                    if (dbv > bl || (dbv == bl && ebv < be)) {
-                        bl = dbv;
-                        be = ebv;
-                        third = a;
-                    }
-                    pe[u] = ld_glb(epos, (size_t)be);
-                    pm[u] = ld_glb(eM, (size_t)be);
-                    th[u] = (uint32_t)third;
+        if (cmode == kChainTable && ln < n) {
+            // lane v: youngest facet e' of {a, b, v} (longest edge, ties ->
+            // smallest index); the triangle is <= thresh iff e' is
+            const int v = ln;
+            uint16_t out = 0xFFFFu;
+            if (v != a && v != b) {
+                const float dav = D[a * n + v], dbv = D[b * n + v];
+                float bl = len;
+                uint32_t be = (uint32_t)e;
+                int third = v;
+                const uint32_t eav = edge_id(a, v), ebv = edge_id(b, v);
+                if (dav > bl || (dav == bl && eav < be)) {
+                    bl = dav;
+                    be = eav;
+                    third = b;
                 }
+                if (dbv > bl || (dbv == bl && ebv < be)) {
+                    bl = dbv;
+                    be = ebv;
+                    third = a;
+                }
+                const uint32_t rb = ep[be];
+                if (rb != kNoRank) out = (uint16_t)(fr[rb] + bits_above(Ms[be], third));
             }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) pe[u] = pe[u] != kNoRank ? ld_glb(c, pe[u]) : kNoRank;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int e = eb + i0 + u;
-            if (e < E && ln < n)
-                st_glb(ct, (size_t)e * n + ln,
-                       (uint16_t)(pe[u] != kNoRank ? pe[u] + bits_above(pm[u], (int)th[u]) : 0xFFFFu));
+            st_glb(ct, (size_t)e * n + v, out);
         }
     }
 }
