@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TDA_RIPS_ABI_VERSION 1
+#define TDA_RIPS_ABI_VERSION 2
 
 /* error codes */
 #define TDA_OK 0
@@ -65,6 +65,14 @@ typedef struct tda_rips_args {
     void *stream;       /* hipStream_t or NULL (library stream)                 */
     int32_t want_dist;  /* 1: also return the (L, N, N) f32 distance matrices   */
     int32_t flags;      /* TDA_FLAG_* bits (0 = none)                           */
+    /* optional silhouette scores on the same distance matrices (ABI >= 2):
+     * sklearn.metrics.silhouette_score(cloud, labels), called by the reference
+     * beside ripser at debug_tda_pipeline.py:117-118 (shape / color labels) and
+     * analyze_adversarial_tda.py:108-111.  `labels` is host memory [n_label_sets][N]
+     * of LabelEncoder codes 0..K-1 (every code present, 2 <= K <= min(N-1, 32)),
+     * shared by all L layers.  NULL / 0 = none. */
+    const int32_t *labels;
+    int32_t n_label_sets;
 } tda_rips_args;
 
 /* per (layer, dim) emitted persistence pairs, in the reference's emission
@@ -100,6 +108,8 @@ typedef struct tda_rips_result {
     int32_t n_stages;
     const char *const *stage_name;
     const float *stage_ms;
+    /* [L][n_label_sets] silhouette scores when args.labels was given, else NULL */
+    const double *silhouette;
 } tda_rips_result;
 
 #define TDA_FLAG_STAGE_TIMES 1

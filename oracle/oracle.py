@@ -163,3 +163,30 @@ def rips_batch_f32(X: np.ndarray, maxdim: int, thresh: float = np.inf) -> list:
         out.append(_unpack(res[l], maxdim))
         lib().oracle_free(ctypes.byref(res[l]))
     return out
+
+
+def silhouette(D: np.ndarray, labels) -> float:
+    """CPU restatement of sklearn.metrics.silhouette_score(X, labels) on the
+    f32 distance matrix D of X (the reference's call at
+    debug_tda_pipeline.py:117-118), following sklearn 1.7.2
+    metrics/cluster/_unsupervised.py: _silhouette_reduce (per-cluster distance
+    sums: np.bincount in f64 added into an f32 array) and silhouette_samples
+    (in-place f32 divisions by the int64 cluster sizes, s = (b - a) /
+    max(a, b), nan_to_num).  The mean is taken in f64.  Checker for
+    k_silhouette; pinned by tests/golden/silhouette.json."""
+    D = np.asarray(D, dtype=np.float32)
+    _, lab = np.unique(np.asarray(labels), return_inverse=True)
+    n = D.shape[0]
+    freq = np.bincount(lab)
+    sums = np.zeros((n, len(freq)), dtype=np.float32)
+    for i in range(n):
+        sums[i] += np.bincount(lab, weights=D[i], minlength=len(freq))
+    intra = sums[np.arange(n), lab].copy()
+    sums[np.arange(n), lab] = np.inf
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sums /= freq
+        inter = sums.min(axis=1)
+        intra /= (freq - 1)[lab]
+        s = inter - intra
+        s /= np.maximum(intra, inter)
+    return float(np.mean(np.nan_to_num(s).astype(np.float64)))

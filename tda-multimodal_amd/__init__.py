@@ -9,8 +9,8 @@ import sys as _sys
 
 from . import distributed, synthetic  # noqa: F401
 from ._lib import EXPORTS, LIB_PATH, build, lib  # noqa: F401
-from .pipeline import get_max_persistence, get_persistence, layer_record, run_sweep  # noqa: F401
-from .ripser import LayerResult, persistence_pairs, ripser, ripser_batch, rips_dm  # noqa: F401
+from .pipeline import get_max_persistence, get_persistence, layer_record, peak_layer, run_sweep, write_summary_stats  # noqa: F401
+from .ripser import LayerResult, persistence_pairs, ripser, ripser_batch, rips_dm, silhouette_score  # noqa: F401
 
 _sys.modules.setdefault("tda_multimodal_amd", _sys.modules[__name__])
 
@@ -24,6 +24,9 @@ __all__ = [
     "get_max_persistence",
     "layer_record",
     "run_sweep",
+    "write_summary_stats",
+    "peak_layer",
+    "silhouette_score",
     "build",
     "lib",
 ]

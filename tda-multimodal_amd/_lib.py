@@ -37,6 +37,8 @@ class RipsArgs(ctypes.Structure):
         ("stream", ctypes.c_void_p),
         ("want_dist", ctypes.c_int32),
         ("flags", ctypes.c_int32),
+        ("labels", ctypes.c_void_p),
+        ("n_label_sets", ctypes.c_int32),
     ]
 
 
@@ -67,6 +69,7 @@ class RipsResult(ctypes.Structure):
         ("n_stages", ctypes.c_int32),
         ("stage_name", ctypes.POINTER(ctypes.c_char_p)),
         ("stage_ms", _f32p),
+        ("silhouette", ctypes.POINTER(ctypes.c_double)),
     ]
 
 

@@ -277,13 +277,16 @@ struct Workspace {
     int device = -1;
     bool init = false;
     hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr, evs = nullptr, evp = nullptr, evh = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr, evs = nullptr, evp = nullptr, evh = nullptr, evsil = nullptr;
     char* dbuf = nullptr;
     size_t dcap = 0;
     OutPair* hout = nullptr;  // host-mapped
     OutPair* hout_dev = nullptr;
     size_t hout_cap = 0;      // in pairs
     LayerStats* hstats = nullptr;  // host-mapped: k_compact writes it
+    char* hsil = nullptr;          // host-mapped: silhouette labels [S][N] i32, then scores [L][S] f64
+    char* hsil_dev = nullptr;
+    size_t hsil_cap = 0;
     LayerStats* hstats_dev = nullptr;
     int64_t* houtoff_dev = nullptr;
     size_t hstats_cap = 0;
@@ -305,7 +308,7 @@ struct Workspace {
 // a single hipGraphLaunch when the same plan, input address and flags recur
 struct GraphKey {
     int64_t L, N, D;
-    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant;
+    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets;
     float thresh;
     const void* x;
     uint64_t gen;
@@ -375,6 +378,7 @@ int ws_prepare(Workspace& w, const Plan& p) {
         HIPC(hipEventCreateWithFlags(&w.evh, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evs, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evp, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&w.evsil, hipEventDisableTiming));
         HIPC(hipEventCreate(&w.ev0));
         HIPC(hipEventCreate(&w.ev1));
         HIPC(hipEventCreateWithFlags(&w.evf, hipEventDisableTiming));
@@ -442,6 +446,7 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
 #define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     TDA_ATTR_CHAIN(1, 0) TDA_ATTR_CHAIN(2, 0) TDA_ATTR_CHAIN(3, 0) TDA_ATTR_CHAIN(4, 0) TDA_ATTR_CHAIN(6, 0)
     TDA_ATTR_CHAIN(9, 0) TDA_ATTR_CHAIN(12, 0) TDA_ATTR_CHAIN(16, 0) TDA_ATTR_CHAIN(21, 0)
@@ -469,6 +474,7 @@ struct ResultImpl {
     tda_rips_result pub;
     std::vector<int64_t> meta, num_edges, idx;
     std::vector<float> bd, thresh, dist, stage_ms;
+    std::vector<double> sil;
     std::vector<const char*> stage_name;
 };
 
@@ -534,6 +540,39 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         xsrc = w.hin;
     }
 
+    // silhouette labels -> host-mapped buffer (stable address: a graph source)
+    const int nls = (a.labels && a.n_label_sets > 0) ? (int)a.n_label_sets : 0;
+    int sil_K = 0;
+    size_t sil_out_off = 0;
+    if (nls) {
+        for (int q = 0; q < nls; ++q) {
+            int K = 0;
+            std::vector<int> f(kSilMaxK, 0);
+            for (int i = 0; i < n; ++i) {
+                const int32_t c = a.labels[(size_t)q * n + i];
+                if (c < 0 || c >= kSilMaxK) return fail(TDA_E_INVALID, "silhouette labels must be codes 0..K-1 with K <= 32");
+                ++f[c];
+                K = std::max(K, c + 1);
+            }
+            for (int c = 0; c < K; ++c)
+                if (!f[c]) return fail(TDA_E_INVALID, "silhouette labels must be contiguous codes 0..K-1 (LabelEncoder)");
+            if (K < 2 || K > n - 1)
+                return fail(TDA_E_INVALID, "Number of labels is " + std::to_string(K) + ". Valid values are 2 to n_samples - 1 (inclusive)");
+            sil_K = std::max(sil_K, K);
+        }
+        sil_out_off = align_up((size_t)nls * n * 4, 16);
+        const size_t need = sil_out_off + (size_t)L * nls * 8;
+        if (w.hsil_cap < need) {
+            drop_graphs(w);
+            if (w.hsil) HIPC(hipHostFree(w.hsil));
+            w.hsil = nullptr;
+            HIPC(hipHostMalloc((void**)&w.hsil, std::max<size_t>(need, 1 << 12), hipHostMallocMapped));
+            HIPC(hipHostGetDevicePointer((void**)&w.hsil_dev, w.hsil, 0));
+            w.hsil_cap = std::max<size_t>(need, 1 << 12);
+        }
+        std::memcpy(w.hsil, a.labels, (size_t)nls * n * 4);
+    }
+
     StageTimer tm{w.stage_ev, s, (a.flags & TDA_FLAG_STAGE_TIMES) != 0, {}};
     StageTimer tm2{w.stage_ev2, w.stream2, tm.on, {}};
     StageTimer tm3{w.stage_ev3, w.stream3, tm.on, {}};
@@ -553,6 +592,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.force_big = force_big;
     gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4);
     gk.thresh = a.thresh;
+    gk.n_label_sets = nls;
     gk.x = xsrc;
     gk.gen = w.gen;
     GraphEntry* ge = nullptr;
@@ -642,6 +682,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipGetLastError());
         if (int rc = tm4.mark("k_h0")) return rc;
         HIPC(hipEventRecord(w.evh, s4));
+        if (nls) {  // silhouette scores on the same distance matrices (sklearn semantics), after the H0 join
+            const size_t lds = (size_t)sil_K * kSilT * 8 + (size_t)n * 4;
+            hipLaunchKernelGGL(k_silhouette, dim3(L, nls), dim3(kSilT), lds, s4, dist, n, (const int32_t*)w.hsil_dev, sil_K,
+                               (double*)(w.hsil_dev + sil_out_off));
+            HIPC(hipGetLastError());
+            if (int rc = tm4.mark("k_silhouette")) return rc;
+            HIPC(hipEventRecord(w.evsil, s4));
+        }
         if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
             dnb.recs = (EdgeRec*)(B + p.o_recs);
             dnb.cls = (uint32_t*)(B + p.o_cls);
@@ -812,6 +860,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         }
         HIPC(hipStreamWaitEvent(s, w.evh, 0));  // join: forest edges (clearing of H1 columns)
         HIPC(hipStreamWaitEvent(s, w.evj, 0));  // join: triangle ranks
+        MARK("wait:join");  // keeps the side streams' time out of the next kernel's stage
         const bool p1 = n <= 1024, p2 = n <= 256;
         Pair* pairs1 = (Pair*)(B + p.o_pairs[1]);
         Pair* pairs2 = p.maxdim >= 2 ? (Pair*)(B + p.o_pairs[2]) : pairs1;
@@ -838,6 +887,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             MARK("k_h1_chain");
             if (p.maxdim >= 2) {
                 HIPC(hipStreamWaitEvent(s, w.evp, 0));  // phase-1 results
+                MARK("wait:phase1");
                 hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[1], db[2], rb, rc, sb,
                                    (const uint32_t*)dnb.res1, pairs2, p.pcap[2]);
                 HIPC(hipGetLastError());
@@ -867,6 +917,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
 
+    if (nls) HIPC(hipStreamWaitEvent(s, w.evsil, 0));  // join: silhouette scores
     // ---- emission order, straight into host-mapped memory
     hipLaunchKernelGGL(k_emit, dim3(L), dim3(1024), kEmitLds, s, stats, L, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
                        (uint32_t*)(B + p.o_fv), p.sstride, w.houtoff_dev, w.hout_dev, (uint64_t)w.hout_cap, w.hstats_dev);
@@ -1051,6 +1102,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     o.n_residual = m_res;
     o.n_adds = m_add;
     o.dist = a.want_dist ? R->dist.data() : nullptr;
+    if (nls) {
+        R->sil.assign((const double*)(w.hsil + sil_out_off), (const double*)(w.hsil + sil_out_off) + (size_t)L * nls);
+        o.silhouette = R->sil.data();
+    } else {
+        o.silhouette = nullptr;
+    }
     o.device_ms = ms;
     for (size_t i = 0; i < tm.names.size(); ++i) {
         float t = 0.0f;

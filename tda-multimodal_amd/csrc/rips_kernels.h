@@ -899,4 +899,71 @@ __global__ __launch_bounds__(1024) void k_emit(LayerStats* __restrict__ stats, i
     for (int i = t; i < (int)(sizeof(LayerStats) / 8); i += blockDim.x) dstS[i] = src[i];
 }
 
+// ---------------------------------------------------------------- silhouette
+// Silhouette coefficient of each label set on the layer's f32 distance matrix:
+// sklearn.metrics.silhouette_score(X, labels) (metric='euclidean'), which the
+// reference calls next to ripser on the same cloud (debug_tda_pipeline.py:117-118,
+// analyze_adversarial_tda.py:108-111).  Follows sklearn's _silhouette_reduce /
+// silhouette_samples arithmetic: per-(point, cluster) distance sums in f64
+// rounded to f32, intra / (|C|-1) and inter = min_k sum_k / |C_k| computed in
+// f64 and rounded to f32, s = (b - a) / max(a, b) in f32, NaN (singleton
+// cluster) -> 0; the mean is accumulated in f64.
+// One block per (layer, label set); thread per point i, j-major loop over
+// column i of the symmetric matrix (D[j][i]), so a wave's loads are coalesced.
+// labels: [S][N] codes 0..K-1, every code present (checked on the host).
+constexpr int kSilT = 256;
+constexpr int kSilMaxK = 32;
+__global__ __launch_bounds__(kSilT) void k_silhouette(const float* __restrict__ dist, int n, const int32_t* __restrict__ labels,
+                                                      int K, double* __restrict__ out) {
+    extern __shared__ __align__(16) unsigned char sil_lds[];
+    const int l = blockIdx.x, s = blockIdx.y, S = gridDim.y, t = threadIdx.x;
+    double* acc = (double*)sil_lds;                        // [K][kSilT]
+    int32_t* lab = (int32_t*)(acc + (size_t)K * kSilT);    // [n]
+    __shared__ int32_t freq[kSilMaxK];
+    __shared__ double part[kSilT / 64];
+    const float* D = dist + (size_t)l * n * n;
+    if (t < kSilMaxK) freq[t] = 0;
+    __syncthreads();
+    for (int j = t; j < n; j += kSilT) {
+        const int32_t c = labels[(size_t)s * n + j];
+        lab[j] = c;
+        atomicAdd(&freq[c], 1);
+    }
+    __syncthreads();
+    double tot = 0.0;
+    for (int i0 = 0; i0 < n; i0 += kSilT) {
+        const int i = i0 + t;
+        const bool on = i < n;
+        for (int k = 0; k < K; ++k) acc[k * kSilT + t] = 0.0;
+        if (on)
+            for (int j = 0; j < n; ++j) acc[lab[j] * kSilT + t] += (double)D[(size_t)j * n + i];
+        if (on) {
+            const int li = lab[i];
+            float inter = INFINITY;
+            for (int k = 0; k < K; ++k) {
+                if (k == li) continue;
+                const float c = (float)((double)(float)acc[k * kSilT + t] / (double)freq[k]);
+                inter = c < inter ? c : inter;
+            }
+            const int den = freq[li] - 1;
+            float sv = 0.0f;
+            if (den > 0) {
+                const float a = (float)((double)(float)acc[li * kSilT + t] / (double)den);
+                const float m = fmaxf(a, inter);
+                sv = m > 0.0f ? (inter - a) / m : 0.0f;  // 0/0 -> NaN -> 0 (nan_to_num)
+            }
+            tot += (double)sv;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if ((t & 63) == 0) part[t >> 6] = tot;
+    __syncthreads();
+    if (t == 0) {
+        double m = 0.0;
+        for (int w = 0; w < kSilT / 64; ++w) m += part[w];
+        out[(size_t)l * S + s] = m / (double)n;
+    }
+}
+
 }  // namespace tda

@@ -26,7 +26,7 @@ from . import _lib
 class _Batch:
     """Host copies of one batched call's outputs; LayerResults are views into it."""
 
-    __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist")
+    __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist", "sil")
 
 
 class LayerResult:
@@ -91,6 +91,12 @@ class LayerResult:
         return self._b.nadd[self._l].tolist()
 
     @property
+    def silhouette(self) -> list:
+        """Silhouette score per label set passed to ``ripser_batch(labels=...)``
+        (sklearn.metrics.silhouette_score semantics), or [] when none."""
+        return [] if self._b.sil is None else self._b.sil[self._l].tolist()
+
+    @property
     def dist(self):
         return None if self._b.dist is None else self._b.dist[self._l]
 
@@ -102,7 +108,7 @@ def _arr(ptr, n, dtype):
     return np.frombuffer(ctypes.string_at(ptr, n * np.dtype(dtype).itemsize), dtype=dtype)
 
 
-def _unpack(res_p, want_dist: bool) -> tuple[list, dict]:
+def _unpack(res_p, want_dist: bool, n_sets: int = 0) -> tuple[list, dict]:
     r = res_p.contents
     L, md, N = int(r.L), int(r.maxdim), int(r.N)
     nd = md + 1
@@ -126,6 +132,9 @@ def _unpack(res_p, want_dist: bool) -> tuple[list, dict]:
     b.thr = _arr(r.thresh, L, np.float32)
     b.ne = _arr(r.num_edges, L, np.int64)
     b.dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N) if want_dist and bool(r.dist) else None
+    b.sil = None
+    if bool(r.silhouette):
+        b.sil = _arr(r.silhouette, L * n_sets, np.float64).reshape(L, n_sets)
     out = [LayerResult(b, l) for l in range(L)]
     stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(int(r.n_stages))]
     return out, {"device_ms": float(r.device_ms), "stages": stages}
@@ -136,7 +145,7 @@ def _call_batch(args: _lib.RipsArgs, want_dist: bool):
     res = ctypes.POINTER(_lib.RipsResult)()
     _lib.check(L.tda_rips_batch(ctypes.byref(args), ctypes.byref(res)))
     try:
-        return _unpack(res, want_dist)
+        return _unpack(res, want_dist, int(args.n_label_sets))
     finally:
         L.tda_rips_free(res)
 
@@ -160,8 +169,27 @@ def _check_common(maxdim, coeff, do_cocycles, n_perm, metric):
         raise NotImplementedError("maxdim > 2 is not implemented")
 
 
+def encode_labels(label_sets, n: int) -> np.ndarray:
+    """sklearn LabelEncoder codes (sorted unique classes -> 0..K-1) of each
+    label set, as a contiguous (S, n) int32 array; checks sklearn's
+    ``check_number_of_labels`` bound (2 <= K <= n - 1)."""
+    rows = []
+    for lab in label_sets:
+        lab = np.asarray(lab)
+        if lab.ndim != 1 or lab.shape[0] != n:
+            raise ValueError(f"labels must have one entry per point ({n})")
+        _, codes = np.unique(lab, return_inverse=True)
+        k = int(codes.max()) + 1 if n else 0
+        if not 2 <= k <= n - 1:
+            raise ValueError(f"Number of labels is {k}. Valid values are 2 to n_samples - 1 (inclusive)")
+        if k > 32:
+            raise NotImplementedError("silhouette with more than 32 clusters is not implemented")
+        rows.append(codes.astype(np.int32))
+    return np.ascontiguousarray(np.stack(rows)) if rows else np.zeros((0, n), np.int32)
+
+
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
-                 want_dist: bool = False, return_time: bool = False, stage_times: bool = False):
+                 want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None):
     """Persistence of L layers in one call.
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
@@ -170,6 +198,10 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     Returns a list of ``LayerResult``; with return_time also a dict
     {"device_ms", "stages": [(name, ms), ...]} (stages filled when stage_times,
     timed with HIP events on the library's stream).
+    labels: optional sequence of label sets (each N labels, shared by every
+    layer); each layer's ``silhouette`` then holds sklearn's
+    ``silhouette_score(cloud, labels)`` per set, computed on the GPU from the
+    same distance matrix (debug_tda_pipeline.py:117-118).
     """
     _check_common(maxdim, 2, False, None, "euclidean")
     a = _lib.RipsArgs()
@@ -212,6 +244,11 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     a.device = int(device)
     a.want_dist = 1 if want_dist else 0
     a.flags = _lib.TDA_FLAG_STAGE_TIMES if stage_times else 0
+    lab = None
+    if labels is not None:
+        lab = encode_labels(labels, N)
+        a.labels = lab.ctypes.data
+        a.n_label_sets = lab.shape[0]
     out, info = _call_batch(a, want_dist)
     return (out, info) if return_time else out
 
@@ -268,3 +305,13 @@ def rips_dm(D_condensed, maxdim: int = 1, thresh: float = np.inf) -> LayerResult
         return _unpack(res, False)[0][0]
     finally:
         L.tda_rips_free(res)
+
+
+def silhouette_score(X, labels) -> float:
+    """Drop-in for the reference's ``sklearn.metrics.silhouette_score(cloud,
+    labels)`` (debug_tda_pipeline.py:117-118; metric='euclidean'), computed by
+    k_silhouette on the GPU distance matrix (one call, H0 only)."""
+    X = np.asarray(X)
+    if X.ndim != 2:
+        raise ValueError("X must be a 2-D array")
+    return ripser_batch(X[None], maxdim=0, labels=[labels])[0].silhouette[0]

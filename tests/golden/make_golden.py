@@ -15,8 +15,14 @@ files next to this script:
                            small random clouds (maxdim 2) and on reference layers
                            5/17/19/0 at maxdim 2 (H2 is not in the reference
                            run: SURVEY 4 cross-check values)
+* silhouette.json        -- sklearn.metrics.silhouette_score (the reference's
+                           call at debug_tda_pipeline.py:117-118) on the 32
+                           reference clouds with the shape / color labels of
+                           the 36 'bound' samples (data/physics_experiment_6x6/
+                           metadata.json, sorted ids as at :46-53), and on small
+                           synthetic clouds (inputs stored in the file)
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [--silhouette-only]
 """
 from __future__ import annotations
 
@@ -82,5 +88,37 @@ def main():
         json.dump(cases, f)
 
 
+def silhouette_golden():
+    from sklearn.metrics import silhouette_score
+
+    with open("/root/reference/data/physics_experiment_6x6/metadata.json") as f:
+        meta = json.load(f)
+    bound = sorted(m["id"] for m in meta if m["type"] == "bound")
+    by_id = {m["id"]: m for m in meta}
+    shape = [by_id[i]["shape"] for i in bound]
+    color = [by_id[i]["color"] for i in bound]
+    z = np.load(os.path.join(HERE, "reference_clouds.npz"))
+    ref = []
+    for l in range(32):
+        X = z[f"layer_{l}"]
+        ref.append({"layer": l, "silhouette_shape": float(silhouette_score(X, shape)),
+                    "silhouette_color": float(silhouette_score(X, color))})
+    rng = np.random.default_rng(7)
+    syn = []
+    for name, n, d, k in (("n48_k6", 48, 3, 6), ("n144_k12", 144, 3, 12), ("n40_k2_d8", 40, 8, 2), ("n60_k32", 60, 3, 32)):
+        X = (rng.standard_normal((n, d)) * 2.0).astype(np.float32)
+        lab = np.arange(n) % k
+        rng.shuffle(lab)
+        syn.append({"name": name, "X": X.tolist(), "labels": lab.tolist(), "score": float(silhouette_score(X, lab))})
+    # a singleton cluster (its sample scores 0) and string labels
+    X = (rng.standard_normal((20, 3))).astype(np.float32)
+    lab = ["b"] * 9 + ["a"] * 10 + ["c"]
+    syn.append({"name": "n20_singleton", "X": X.tolist(), "labels": lab, "score": float(silhouette_score(X, lab))})
+    with open(os.path.join(HERE, "silhouette.json"), "w") as f:
+        json.dump({"shape_labels": shape, "color_labels": color, "reference": ref, "synthetic": syn}, f)
+
+
 if __name__ == "__main__":
-    main()
+    if "--silhouette-only" not in sys.argv:
+        main()
+    silhouette_golden()

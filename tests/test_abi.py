@@ -33,7 +33,7 @@ def test_library_is_gfx950_code_object(built_lib):
 
 def test_version_and_no_device_here(pkg, built_lib):
     L = pkg.lib()
-    assert L.tda_version() == 1
+    assert L.tda_version() == 2  # ABI 2: silhouette labels / scores appended to args / result
     assert L.tda_device_ok(12345) == 0
 
 
@@ -68,3 +68,26 @@ def test_product_path_does_not_reference_oracle():
             if f.endswith((".py", ".hip", ".h")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in txt and "from oracle" not in txt and "rips_oracle" not in txt, f
+
+
+def test_ctypes_structs_match_header_layout(pkg, tmp_path):
+    """The ctypes mirrors in _lib.py have the C header's sizes and offsets
+    (compiled with gcc against include/tda_rips.h)."""
+    import ctypes
+    import os
+    import subprocess
+
+    from importlib import import_module
+
+    lb = import_module("tda-multimodal_amd._lib")
+    src = tmp_path / "layout.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "tda_rips.h"\n'
+        'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(tda_rips_args), offsetof(tda_rips_args, labels),'
+        ' offsetof(tda_rips_args, n_label_sets), sizeof(tda_rips_result), offsetof(tda_rips_result, silhouette));return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", lb.INCLUDE, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    want = [ctypes.sizeof(lb.RipsArgs), lb.RipsArgs.labels.offset, lb.RipsArgs.n_label_sets.offset,
+            ctypes.sizeof(lb.RipsResult), lb.RipsResult.silhouette.offset]
+    assert got == want

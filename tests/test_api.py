@@ -71,3 +71,38 @@ def test_synthetic_generators(pkg):
     assert np.array_equal(syn.layer48(3), X[3])
     assert syn.torus(64).shape == (64, 3)
     assert syn.sweep144(2).shape == (2, 144, 3)
+
+
+def test_silhouette_labels_host_checks(pkg):
+    """Label encoding and sklearn's check_number_of_labels bounds, on the host."""
+    from importlib import import_module
+
+    rp = import_module("tda-multimodal_amd.ripser")
+    codes = rp.encode_labels([["b", "a", "b", "c"]], 4)
+    assert codes.dtype == np.int32 and codes.tolist() == [[1, 0, 1, 2]]
+    with pytest.raises(ValueError):
+        rp.encode_labels([[0, 0, 0, 0]], 4)  # one cluster
+    with pytest.raises(ValueError):
+        rp.encode_labels([[0, 1, 2, 3]], 4)  # K = n
+    with pytest.raises(ValueError):
+        rp.encode_labels([[0, 1, 0]], 4)  # wrong length
+    with pytest.raises(NotImplementedError):
+        rp.encode_labels([np.arange(40) % 33], 40)
+
+
+def test_summary_stats_writer_and_peak_layer(pkg, tmp_path):
+    """debug_tda_pipeline.py:121-130 key order, :154-156 json.dump(indent=2), :195 argmax."""
+    import json
+
+    dg = [np.array([[0.0, 1.0], [0.0, np.inf]]), np.array([[1.0, 2.5]])]
+    recs = [pkg.layer_record(i, dg, silhouette_shape=s, silhouette_color=-s) for i, s in enumerate([0.1, 0.7, 0.3])]
+    assert list(recs[0]) == ["layer", "n_h1_features", "max_h1_persistence", "all_h1_persistence_values",
+                             "n_h0_features", "max_h0_persistence", "silhouette_shape", "silhouette_color"]
+    p = tmp_path / "summary_stats.json"
+    pkg.write_summary_stats(str(p), recs)
+    text = p.read_text()
+    assert text == json.dumps(recs, indent=2)
+    assert pkg.peak_layer(json.loads(text)) == 1
+    pipe = __import__("importlib").import_module("tda-multimodal_amd.pipeline")
+    back = pipe.unpack_record(pipe.pack_record(recs[1]))
+    assert back["silhouette_shape"] == 0.7 and back["silhouette_color"] == -0.7

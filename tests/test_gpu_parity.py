@@ -238,3 +238,61 @@ def test_values_within_tolerance_of_sklearn(gpu, ref_clouds):
     r = gpu.ripser_batch(X[None], maxdim=1, want_dist=True)[0]
     Dref = pairwise_distances(X).astype(np.float64)
     assert np.max(np.abs(r.dist.astype(np.float64) - Dref)) <= TOL
+
+
+# ---- silhouette: k_silhouette on the same distance matrices
+SIL_TOL = 1e-5  # FP: sklearn accumulates the mean in f32, the kernel in f64
+
+
+def _sil_golden():
+    with open(os.path.join(GOLDEN, "silhouette.json")) as f:
+        return json.load(f)
+
+
+def test_sweep_with_silhouettes_matches_reference_and_sklearn(gpu, ref_clouds, summary_stats):
+    """The reference loop's record (debug_tda_pipeline.py:112-130) from ONE
+    batched call: persistence keys equal the committed summary_stats.json, the
+    shape/color silhouettes match sklearn's silhouette_score on each cloud."""
+    g = _sil_golden()
+    for rep in range(3):  # the 2nd and 3rd calls replay the captured graph
+        shp = g["shape_labels"] if rep != 1 else g["color_labels"]
+        col = g["color_labels"] if rep != 1 else g["shape_labels"]
+        recs, res = gpu.run_sweep(ref_clouds, maxdim=1, shape_labels=shp, color_labels=col)
+        for l, r in enumerate(recs):
+            base = {k: v for k, v in r.items() if not k.startswith("silhouette")}
+            assert base == summary_stats[l], l
+            want = g["reference"][l]
+            ws, wc = (want["silhouette_shape"], want["silhouette_color"]) if rep != 1 else \
+                (want["silhouette_color"], want["silhouette_shape"])
+            assert abs(r["silhouette_shape"] - ws) < SIL_TOL, (rep, l)
+            assert abs(r["silhouette_color"] - wc) < SIL_TOL, (rep, l)
+    assert gpu.peak_layer(recs) == int(np.argmax([x["silhouette_shape"] for x in g["reference"]]))
+
+
+def test_silhouette_synthetic_vs_sklearn_and_oracle(gpu, oracle):
+    g = _sil_golden()
+    for c in g["synthetic"]:
+        X = np.asarray(c["X"], dtype=np.float32)
+        got = gpu.silhouette_score(X, c["labels"])
+        assert abs(got - c["score"]) < SIL_TOL, c["name"]
+        assert abs(got - oracle.silhouette(oracle.distances(X), c["labels"])) < 1e-9, c["name"]
+
+
+def test_silhouette_large_n_and_h2_path(gpu, oracle):
+    """N=1024 (k_silhouette loops over point blocks) and the dense H2 path
+    (N=48, maxdim=2, four streams) with labels attached: scores vs the oracle,
+    persistence unchanged."""
+    X = gpu.synthetic.torus(1024)
+    lab = (np.arange(1024) * 7) % 5
+    res = gpu.ripser_batch(X[None], maxdim=0, labels=[lab], want_dist=True)[0]
+    assert abs(res.silhouette[0] - oracle.silhouette(res.dist, lab)) < 1e-9
+    Xs = gpu.synthetic.sweep48(4)
+    labs = [np.arange(48) % 6, np.arange(48) // 8]
+    a = gpu.ripser_batch(Xs, maxdim=2, labels=labs)
+    b = gpu.ripser_batch(Xs, maxdim=2)
+    for l in range(4):
+        for d in range(3):
+            assert _pairs(a[l], d) == _pairs(b[l], d)
+        for q in range(2):
+            want = oracle.silhouette(oracle.distances(Xs[l]), labs[q])
+            assert abs(a[l].silhouette[q] - want) < 1e-9, (l, q)

@@ -115,3 +115,22 @@ def test_oracle_random_vs_naive_live(oracle, n, md):
             got = [(float(b), float(e), int(bi), int(di)) for (b, e), bi, di in
                    zip(r["dgms"][d], r["birth_idx"][d], r["death_idx"][d])]
             assert got == [(float(b), float(e), bi, di) for b, e, bi, di in em[d]]
+
+
+def _sil_golden():
+    with open(os.path.join(GOLDEN, "silhouette.json")) as f:
+        return json.load(f)
+
+
+def test_oracle_silhouette_matches_sklearn_goldens(oracle, ref_clouds):
+    """oracle.silhouette (restatement of sklearn's silhouette_score) against the
+    committed sklearn values: 32 reference clouds x (shape, color) labels and
+    synthetic cases (K = 2..32, a singleton cluster, string labels)."""
+    g = _sil_golden()
+    for r in g["reference"]:
+        D = oracle.distances(ref_clouds[r["layer"]])
+        assert abs(oracle.silhouette(D, g["shape_labels"]) - r["silhouette_shape"]) < 1e-6
+        assert abs(oracle.silhouette(D, g["color_labels"]) - r["silhouette_color"]) < 1e-6
+    for c in g["synthetic"]:
+        D = oracle.distances(np.asarray(c["X"], dtype=np.float32))
+        assert abs(oracle.silhouette(D, c["labels"]) - c["score"]) < 1e-6, c["name"]
