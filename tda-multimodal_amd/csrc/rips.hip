@@ -65,6 +65,10 @@ struct Plan {
     uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, vcap_g = 0, sstride = 0;
     bool lds_mode = false;
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
+    int b1G = 0;       // k_big_phase1 workgroups per layer (0: no parallel H1 phase 1)
+    uint64_t b1cap = 0, b1pool = 0;  // phase-1 workspace capacity, saved-column pool per layer
+    size_t o_b1log = 0, o_b1idx = 0, o_b1fill = 0, o_b1bref = 0, o_b1pool = 0, o_b1piv = 0, o_b1info = 0, o_b1off = 0,
+           o_b1len = 0;
     bool dense = false;  // N <= 64: dense-bitmap H1 chain + column-parallel H2 phase 1 (rips_reduce_small.h)
     int dK = 0;          // dense H1 bitmap words per lane (a k_h1_chain instantiation)
     uint32_t inv_stride = 0;  // rank -> edge table stride (C(N,3) rounded up)
@@ -235,6 +239,23 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
             p.o_wp = take(L * p.wcap_g / 4 * 4);   // bucket fill counters
         }
         if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
+        if (p.big && getenv_is("TDA_BIG_P1", "1")) {
+            // parallel H1 phase 1 (EXPERIMENTAL, opt-in: not parity-green yet at N >= 128):
+            // ~64 radix-heap workspaces in all (10 GB at N > 640 of the 288 GB HBM)
+            p.b1G = (int)std::max<int64_t>(1, 64 / L);
+            p.b1cap = std::min<uint64_t>(p.wcap_g, 1ull << 20);
+            p.b1pool = std::min<uint64_t>((uint64_t)p.b1G * p.b1cap, 1ull << 25);
+            const uint64_t P1 = (uint64_t)L * p.b1G;
+            p.o_b1log = take(P1 * p.b1cap * 8);
+            p.o_b1idx = take(P1 * p.b1cap * 2 * 8);
+            p.o_b1fill = take(P1 * (p.b1cap * 2 / 8) * 4);
+            p.o_b1bref = take(P1 * kNB * p.b1cap * 4);
+            p.o_b1pool = take(L * p.b1pool * 8);
+            p.o_b1piv = take(L * p.rcap[1] * 8);
+            p.o_b1info = take(L * p.rcap[1] * 4);
+            p.o_b1off = take(L * p.rcap[1] * 8);
+            p.o_b1len = take(L * p.rcap[1] * 4);
+        }
         if (p.dense) {
             p.o_recs = take(L * binom(N, 2) * 16);
             p.o_cls2 = take(L * (uint64_t)p.n2p * 2);
@@ -590,7 +611,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.force_global = force_global;
     gk.scale = scale;
     gk.force_big = force_big;
-    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4);
+    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.b1G ? 1 << 8 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
     gk.x = xsrc;
@@ -902,8 +923,31 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             gb.cap = p.wcap_g;
             gb.bcap = p.wcap_g;
             gb.step_limit = step_limit();
+            BigP1Bufs pb1 = {};
+            if (p.b1G) {
+                const uint64_t P1 = (uint64_t)L * p.b1G;
+                pb1.log = (uint64_t*)(B + p.o_b1log);
+                pb1.index = (uint64_t*)(B + p.o_b1idx);
+                pb1.fill = (uint32_t*)(B + p.o_b1fill);
+                pb1.bref = (uint32_t*)(B + p.o_b1bref);
+                pb1.cap = p.b1cap;
+                pb1.pool = (uint64_t*)(B + p.o_b1pool);
+                pb1.pool_cap = p.b1pool;
+                pb1.used = (unsigned long long*)(B + p.o_p1used);  // zeroed per call (memset region)
+                pb1.piv = (uint64_t*)(B + p.o_b1piv);
+                pb1.info = (uint32_t*)(B + p.o_b1info);
+                pb1.off = (uint64_t*)(B + p.o_b1off);
+                pb1.len = (uint32_t*)(B + p.o_b1len);
+                pb1.G = p.b1G;
+                pb1.step_limit = step_limit();
+                HIPC(hipMemsetAsync(pb1.index, 0, P1 * p.b1cap * 2 * 8, s));
+                HIPC(hipMemsetAsync(pb1.fill, 0, P1 * (p.b1cap * 2 / 8) * 4, s));
+                hipLaunchKernelGGL(k_big_phase1, dim3(p.b1G, L), dim3(kBigT), 0, s, dist, n, stats, db[1], rb, pb1);
+                HIPC(hipGetLastError());
+                MARK("k_big_phase1");
+            }
             hipLaunchKernelGGL(k_reduce_big, dim3(L), dim3(kBigT), 0, s, dist, n, p.maxdim, stats, db[1], db[2], rb, gb, pairs1,
-                               pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0);
+                               pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0, pb1, p.b1G ? 1 : 0);
         } else if (p.lds_mode) {
             if (p2) TDA_LAUNCH_RED(true, true, true); else if (p1) TDA_LAUNCH_RED(true, true, false); else TDA_LAUNCH_RED(true, false, false);
         } else {
@@ -1024,6 +1068,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)tt, (unsigned long long)sc, (unsigned long long)cb, (unsigned long long)ad, (unsigned long long)mx,
                 (unsigned long long)mxa);
     }
+    if (p.big)
+        for (int d = 1; d <= p.maxdim; ++d) {
+            const uint64_t* q = w.hstats[0].prof[d];
+            fprintf(stderr, "[tda-prof] big dim %d layer 0: cob0 %llu pop %llu owner_add %llu app_add %llu store %llu reset %llu total %llu cycles; owner adds %llu entries %llu, all adds %lld\n",
+                    d, (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[2], (unsigned long long)q[3],
+                    (unsigned long long)q[4], (unsigned long long)q[5], (unsigned long long)q[7], (unsigned long long)(q[6] >> 40),
+                    (unsigned long long)(q[6] & ((1ull << 40) - 1)), (long long)w.hstats[0].n_adds[d]);
+        }
     for (int d = 1; d <= p.maxdim; ++d) {
         uint64_t mx[8] = {0};
         int arg = 0;

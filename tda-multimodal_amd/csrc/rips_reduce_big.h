@@ -311,10 +311,200 @@ struct BigHeap {
     }
 };
 
+// Phase 1 of the large-N H1 reduction (k_big_phase1): every residual column
+// is reduced IN PARALLEL by its own workgroup with the apparent columns only
+// (their coboundaries are implicit and do not depend on any other residual
+// column), up to its first pivot that is not an apparent pivot.  Which
+// residual column owns that pivot is only known in column order, so the
+// serial kernel then walks the columns: a column whose phase-1 pivot is free
+// becomes a pair at once (its saved working column is R_j); only a column
+// whose pivot an earlier column owns is rebuilt from its saved entries and
+// continued serially.  On torus N=1024 that moves 16.7K of 16.8K column
+// additions out of the serial walk.
+constexpr uint32_t kB1Defer = 1u << 31;  // phase 1 gave up (capacity / step limit): serial from scratch
+struct BigP1Bufs {
+    uint64_t* log;        // [L * G] workspaces, as BigBufs (cap each)
+    uint64_t* index;
+    uint32_t* fill;
+    uint32_t* bref;
+    uint64_t cap;
+    uint64_t* pool;       // [L][pool_cap] saved working columns (live keys)
+    uint64_t pool_cap;
+    unsigned long long* used;  // [L] pool bump counters (zeroed per call)
+    uint64_t* piv;        // [L][rcap] pivot key after phase 1 (kEmpty64: zero column)
+    uint32_t* info;       // [L][rcap] additions | kB1Defer
+    uint64_t* off;        // [L][rcap] saved column offset in pool
+    uint32_t* len;        // [L][rcap] saved column length
+    int G;                // workgroups (workspaces) per layer
+    uint64_t step_limit;
+};
+
+// the oldest facet of the apparent cofacet pidx (its apparent column), with diameter
+template <int DIM>
+__device__ __forceinline__ float apparent_facet(const float* __restrict__ D, int n, uint64_t pidx, int (&fv)[DIM + 1]) {
+    constexpr int NV = DIM + 2;
+    int t[NV];
+    decode<DIM + 1>(pidx, n, t);
+    float fd = -1.0f;
+    int fu = 0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        float d = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+            for (int k = i + 1; k < NV; ++k)
+                if (i != u && k != u) d = fmaxf(d, ld_glb(D, (size_t)t[i] * n + t[k]));
+        if (d > fd) {
+            fd = d;
+            fu = u;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        if (u != fu) continue;
+#pragma unroll
+        for (int i = 0, q = 0; i < NV; ++i)
+            if (i != u) fv[q++] = t[i];
+    }
+    return fd;
+}
+
+// toggle the coboundary of vs (diam sd) into H -- one thread per new vertex
+template <int DIM>
+__device__ __forceinline__ void big_cob(BigHeap& H, const float* __restrict__ D, int n, float r, const int (&vs)[DIM + 1], float sd) {
+    for (int v0 = 0; v0 < n; v0 += kBigT) {
+        const int v = v0 + (int)threadIdx.x;
+        bool ok = v < n;
+#pragma unroll
+        for (int i = 0; i <= DIM; ++i) ok &= (vs[i] != v);
+        float cd = sd;
+        uint64_t key = 0;
+        if (ok) {
+#pragma unroll
+            for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, ld_glb(D, (size_t)vs[i] * n + v));
+            ok = cd <= r;
+            key = filt_key(cd, cofacet_index<DIM>(vs, v));
+        }
+        H.toggle_pass(key, ok);
+    }
+}
+
+__global__ __launch_bounds__(kBigT) void k_big_phase1(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                      DimBufs b, Reduce2Bufs rb, BigP1Bufs pb) {
+    __shared__ BigShared S;
+    const int l = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+    LayerStats* st = stats + l;
+    const float r = st->thresh;
+    const float* D = dist + (size_t)l * n * n;
+    uint64_t nres = (uint64_t)st->n_residual[1];
+    if (nres > b.rcap) nres = b.rcap;
+    const uint64_t* resid = b.resid + (size_t)l * b.rcap;
+    const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
+    const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
+    const size_t wsi = (size_t)l * pb.G + g;
+    BigHeap H;
+    H.log = pb.log + wsi * pb.cap;
+    H.index = pb.index + wsi * 2 * pb.cap;
+    H.fill = pb.fill + wsi * (2 * pb.cap / 8);
+    H.bref = pb.bref + wsi * kNB * pb.cap;
+    H.cap = pb.cap;
+    H.bcap = pb.cap;
+    H.imask = (uint32_t)(2 * pb.cap - 1);
+    H.S = &S;
+    uint64_t* pool = pb.pool + (size_t)l * pb.pool_cap;
+    if (tid == 0) {
+        S.cnt = 0;
+        for (int q = 0; q < kNB; ++q) S.nb[q] = 0;
+    }
+    for (uint64_t j = g; j < nres; j += pb.G) {
+        __syncthreads();
+        const uint64_t key = ld_glb(resid, j);
+        const uint64_t sidx = key_idx(key);
+        const float sdm = key_diam(key);
+        if ((ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u) continue;  // cleared (H0 forest edge): serial skips it
+        int vs[2];
+        decode<1>(sidx, n, vs);
+        if (tid == 0) {
+            S.err = 0;
+            S.last = __float_as_uint(sdm + 0.0f);
+        }
+        __syncthreads();
+        big_cob<1>(H, D, n, r, vs, sdm);
+        uint32_t adds = 0;
+        bool defer = false;
+        uint64_t pk = kEmpty64, off = 0;
+        uint32_t len = 0;
+        for (uint64_t step = 0;; ++step) {
+            pk = H.pop_min();
+            if (S.err || step >= pb.step_limit) {
+                defer = true;
+                break;
+            }
+            if (pk == kEmpty64) break;  // zero column: an essential class
+            const uint64_t pidx = 0xFFFFFFFFull - (pk & 0xFFFFFFFFull);
+            if ((ld_glb(pivg, pidx >> 5) >> (pidx & 31)) & 1u) {  // apparent pivot: add its implicit column
+                int fv[2];
+                const float fd = apparent_facet<1>(D, n, pidx, fv);
+                big_cob<1>(H, D, n, r, fv, fd);
+                ++adds;
+                continue;
+            }
+            // first non-apparent pivot: save the live entries (the serial walk decides ownership)
+            const uint32_t c = S.cnt;
+            uint64_t live = 0;
+            for (uint32_t e = tid; e < c; e += kBigT) live += H.log[e] < kDead ? 1 : 0;
+            live = block_sum_u64(live, S);
+            if (tid == 0) S.bc[0] = atomicAdd(pb.used + l, (unsigned long long)live);
+            __syncthreads();
+            off = S.bc[0];
+            if (off + live > pb.pool_cap) {
+                defer = true;
+                break;
+            }
+            uint64_t wr = 0;
+            for (uint32_t e0 = 0; e0 < c; e0 += kBigT) {
+                const uint32_t e = e0 + tid;
+                const uint64_t k = e < c ? H.log[e] : kEmpty64;
+                const bool lv = k < kDead;
+                uint32_t tot;
+                const uint32_t o = block_prefix(lv, S, &tot);
+                if (lv) pool[off + wr + o] = k;
+                wr += tot;
+            }
+            len = (uint32_t)live;
+#ifdef TDA_PROFILE
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t z = 0;
+                for (uint32_t e = 0; e < len; ++e) z += pool[off + e] == 0;
+                if (z || j == 14) printf("[p1] col %llu saved len %u off %llu zeros %u wr %llu c %u\n", (unsigned long long)j, len,
+                                (unsigned long long)off, z, (unsigned long long)wr, c);
+            }
+#endif
+            break;
+        }
+#ifdef TDA_PROFILE
+        if (tid == 0 && defer)
+            printf("[p1] layer %d col %llu adds %u defer %d err %d piv %016llx len %u off %llu cnt %u\n", l, (unsigned long long)j,
+                   adds, (int)defer, S.err, (unsigned long long)pk, len, (unsigned long long)off, S.cnt);
+#endif
+        if (tid == 0) {
+            const size_t q = (size_t)l * b.rcap + j;
+            pb.piv[q] = pk;
+            pb.info[q] = adds | (defer ? kB1Defer : 0u);
+            pb.off[q] = off;
+            pb.len[q] = len;
+        }
+        __syncthreads();
+        H.reset();
+    }
+}
+
 template <int DIM>
 __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, LayerStats* st, int l, const DimBufs& b,
                                const Reduce2Bufs& rb, const BigBufs& gb, BigShared& S, PivMap& map, const PivMap* prev,
-                               Pair* __restrict__ pairs, uint64_t pcap) {
+                               Pair* __restrict__ pairs, uint64_t pcap, const BigP1Bufs* p1 = nullptr) {
     constexpr int NV = DIM + 2;
     const int tid = threadIdx.x, ln = tid & 63;
     uint64_t nres = (uint64_t)st->n_residual[DIM];
@@ -345,6 +535,12 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
     uint64_t rused = 0;
     Pair* P = pairs + (size_t)l * pcap;
     uint64_t cs = 0, npairs = 0, nadds = 0, nskip = 0;
+#ifdef TDA_PROFILE
+    int dbg_n = 0;
+    // cob0, pop_min, owner adds, apparent adds, store R_j, reset, (owner adds << 40 | owner entries), total
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_all = clock64();
+#endif
     if (tid == 0) {
         S.cnt = 0;
         S.err = 0;
@@ -391,15 +587,114 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             if (tid == 0) rlen[j] = 0;
             continue;
         }
-        if (tid == 0) S.last = __float_as_uint(sdm + 0.0f);
-        __syncthreads();
-        cob(vs, sdm);
+        bool resume = false;
+#ifdef TDA_PROFILE
+        uint64_t dbg_prev = kEmpty64;
+        int64_t dbg_owner = -1;
+#endif
+        if (p1) {
+            const size_t q = (size_t)l * b.rcap + j;
+            const uint32_t inf = ld_glb((const uint32_t*)p1->info, q);
+            if (!(inf & kB1Defer)) {
+                const uint64_t pk = ld_glb((const uint64_t*)p1->piv, q);
+                if (pk == kEmpty64) {  // zero after apparent additions: essential
+                    nadds += inf;
+                    if (tid == 0) {
+                        uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
+                        if (pos < pcap)
+                            P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
+                        else
+                            atomicOr(&st->err, ERR_PAIR_CAP);
+                        rlen[j] = 0;
+                    }
+                    continue;
+                }
+                const uint64_t pidx = 0xFFFFFFFFull - (pk & 0xFFFFFFFFull);
+                const float pd = __uint_as_float((uint32_t)(pk >> 32));
+                // the bit was clear in phase 1, so it is set now only by an earlier residual column
+                const bool app = (ld_glb((const uint32_t*)pivg, pidx >> 5) >> (pidx & 31)) & 1u;
+                const int64_t owner = app ? map.find((uint32_t)pidx, ln) : -1;
+                const uint64_t so = ld_glb((const uint64_t*)p1->off, q);
+                const uint32_t sl = ld_glb((const uint32_t*)p1->len, q);
+                const uint64_t* sp = p1->pool + (size_t)l * p1->pool_cap + so;
+                if (owner < 0) {  // free pivot: pair now; the saved column is R_j
+                    nadds += inf;
+                    if (tid == 0) {
+                        if (pd > sdm) {
+                            uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
+                            if (pos < pcap)
+                                P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
+                            else
+                                atomicOr(&st->err, ERR_PAIR_CAP);
+                        }
+                        map.insert((uint32_t)pidx, (uint32_t)j);
+                        atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
+                    }
+                    cs += pair_hash(sidx, pidx);
+                    npairs += 1;
+                    uint64_t wr = sl;
+                    if (rused + wr > rb.rpool_cap) {
+                        if (tid == 0) S.err = 2;
+                        wr = 0;
+                    }
+                    for (uint32_t e = tid; e < wr; e += kBigT) rpool[rused + e] = ld_glb(sp, e);
+                    if (tid == 0) {
+                        roff[j] = rused;
+                        rlen[j] = (uint32_t)wr;
+                    }
+                    rused += wr;
+                    continue;
+                }
+                // owned pivot: the column is reduced serially from its coboundary
+#ifdef TDA_BIG_RESUME
+                nadds += inf;
+#ifdef TDA_PROFILE
+                if (tid == 0) {
+                    uint32_t z = 0;
+                    uint64_t mn = kEmpty64;
+                    for (uint32_t e = 0; e < sl; ++e) {
+                        z += sp[e] == 0;
+                        mn = sp[e] < mn ? sp[e] : mn;
+                    }
+                    const uint64_t r0 = ld_glb((const uint64_t*)roff, owner);
+                    const uint32_t rl = ld_glb((const uint32_t*)rlen, owner);
+                    uint64_t omn = kEmpty64;
+                    for (uint32_t e = 0; e < rl; ++e) omn = rpool[r0 + e] < omn ? rpool[r0 + e] : omn;
+                    printf("[ser] col %llu resume: so %llu sl %u zeros %u pk %016llx min %016llx owner %lld (roff %llu rlen %u min %016llx) rused %llu\n",
+                           (unsigned long long)j, (unsigned long long)so, sl, z, (unsigned long long)pk, (unsigned long long)mn,
+                           (long long)owner, (unsigned long long)r0, rl, (unsigned long long)omn, (unsigned long long)rused);
+                }
+#endif
+                if (tid == 0) S.last = (uint32_t)(pk >> 32);
+                __syncthreads();
+                for (uint32_t e0 = 0; e0 < sl; e0 += kBigT) {
+                    const uint32_t e = e0 + tid;
+                    H.toggle_pass(e < sl ? ld_glb(sp, e) : 0, e < sl);
+                }
+                resume = true;
+#endif
+            }
+        }
+        if (!resume) {
+            if (tid == 0) S.last = __float_as_uint(sdm + 0.0f);
+            __syncthreads();
+        }
+        TDA_STAMP(t_c0);
+        if (!resume) cob(vs, sdm);
+        TDA_ACC(0, t_c0);
         for (uint64_t step = 0;; ++step) {
+            TDA_STAMP(t_p0);
             const uint64_t pk = H.pop_min();
+            TDA_ACC(1, t_p0);
+#ifdef TDA_PROFILE
+            if (resume && step < 3 && tid == 0 && j < 12)
+                printf("[ser] col %llu step %llu pop %016llx last %08x cnt %u\n", (unsigned long long)j, (unsigned long long)step,
+                       (unsigned long long)pk, S.last, S.cnt);
+#endif
             if (step >= gb.step_limit) {
                 if (tid == 0) {
-                    printf("k_reduce_big: layer %d dim %d column %llu (idx %llu) step limit: pivot %016llx cnt %u last %08x\n", l,
-                           DIM, (unsigned long long)j, (unsigned long long)sidx, (unsigned long long)pk, S.cnt, S.last);
+                    printf("k_reduce_big: layer %d dim %d column %llu (idx %llu) step limit: pivot %016llx cnt %u last %08x resume %d\n", l,
+                           DIM, (unsigned long long)j, (unsigned long long)sidx, (unsigned long long)pk, S.cnt, S.last, (int)resume);
                     S.err = 3;
                 }
                 __syncthreads();
@@ -420,6 +715,26 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             const float pd = __uint_as_float((uint32_t)(pk >> 32));
             const bool app = (ld_glb((const uint32_t*)pivg, pidx >> 5) >> (pidx & 31)) & 1u;
             const int64_t owner = app ? map.find((uint32_t)pidx, ln) : -1;
+#ifdef TDA_PROFILE
+            if (pk == dbg_prev && pk != kEmpty64 && tid == 0 && dbg_n < 3) {
+                ++dbg_n;
+                const uint64_t o0d = ld_glb((const uint64_t*)roff, dbg_owner);
+                const uint32_t old = ld_glb((const uint32_t*)rlen, dbg_owner);
+                uint64_t mn = kEmpty64;
+                bool has = false;
+                for (uint32_t e = 0; e < old; ++e) {
+                    const uint64_t k = rpool[o0d + e];
+                    mn = k < mn ? k : mn;
+                    has |= k == pk;
+                }
+                printf("[dbg] col %llu resume %d: pivot %016llx repeats after adding owner %lld (off %llu len %u min %016llx has %d) app %d\n",
+                       (unsigned long long)j, (int)resume, (unsigned long long)pk, (long long)dbg_owner, (unsigned long long)o0d, old,
+                       (unsigned long long)mn, (int)has, (int)app);
+            }
+            dbg_prev = pk;
+            dbg_owner = owner;
+#endif
+            TDA_STAMP(t_a0);
             if (owner >= 0) {
                 const uint64_t o0 = ld_glb((const uint64_t*)roff, owner);
                 const uint32_t ol = ld_glb((const uint32_t*)rlen, owner);
@@ -428,34 +743,16 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                     H.toggle_pass(e < ol ? ld_glb((const uint64_t*)rpool, o0 + e) : 0, e < ol);
                 }
                 ++nadds;
+                TDA_ACC(2, t_a0);
+#ifdef TDA_PROFILE
+                prof[6] += (1ull << 40) + ol;
+#endif
             } else if (app) {
-                int t[NV];
-                decode<DIM + 1>(pidx, n, t);
-                float fd = -1.0f;
-                int fu = 0;
-#pragma unroll
-                for (int u = 0; u < NV; ++u) {
-                    float d = 0.0f;
-#pragma unroll
-                    for (int i = 0; i < NV; ++i)
-#pragma unroll
-                        for (int k = i + 1; k < NV; ++k)
-                            if (i != u && k != u) d = fmaxf(d, ld_glb(D, (size_t)t[i] * n + t[k]));
-                    if (d > fd) {
-                        fd = d;
-                        fu = u;
-                    }
-                }
                 int fv[DIM + 1];
-#pragma unroll
-                for (int u = 0; u < NV; ++u) {
-                    if (u != fu) continue;
-#pragma unroll
-                    for (int i = 0, q = 0; i < NV; ++i)
-                        if (i != u) fv[q++] = t[i];
-                }
+                const float fd = apparent_facet<DIM>(D, n, pidx, fv);
                 cob(fv, fd);
                 ++nadds;
+                TDA_ACC(3, t_a0);
             } else {
                 if (tid == 0) {
                     if (pd > sdm) {
@@ -491,11 +788,14 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                     rlen[j] = (uint32_t)wr;
                 }
                 rused += wr;
+                TDA_ACC(4, t_a0);
                 break;
             }
         }
         __syncthreads();
+        TDA_STAMP(t_r0);
         H.reset();
+        TDA_ACC(5, t_r0);
     }
     __syncthreads();
     if (tid == 0) {
@@ -507,6 +807,10 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
         atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)nadds);
         atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)(0ull - nskip));
         st->nskip[DIM] = nskip;
+#ifdef TDA_PROFILE
+        prof[7] = clock64() - t_all;
+        for (int i = 0; i < 8; ++i) st->prof[DIM][i] = prof[i];
+#endif
     }
     __syncthreads();
 }
@@ -515,14 +819,14 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
 __global__ __launch_bounds__(kBigT) void k_reduce_big(const float* __restrict__ dist, int n, int maxdim,
                                                        LayerStats* __restrict__ stats, DimBufs b1, DimBufs b2, Reduce2Bufs rb,
                                                        BigBufs gb, Pair* __restrict__ pairs1, Pair* __restrict__ pairs2,
-                                                       uint64_t pcap1, uint64_t pcap2) {
+                                                       uint64_t pcap1, uint64_t pcap2, BigP1Bufs p1, int use_p1) {
     __shared__ BigShared S;
     const int l = blockIdx.x;
     LayerStats* st = stats + l;
     const float r = st->thresh;
     const float* D = dist + (size_t)l * n * n;
     PivMap m1, m2;
-    big_reduce_dim<1>(D, n, r, st, l, b1, rb, gb, S, m1, nullptr, pairs1, pcap1);
+    big_reduce_dim<1>(D, n, r, st, l, b1, rb, gb, S, m1, nullptr, pairs1, pcap1, use_p1 ? &p1 : nullptr);
     if (maxdim >= 2) big_reduce_dim<2>(D, n, r, st, l, b2, rb, gb, S, m2, &m1, pairs2, pcap2);
 }
 
