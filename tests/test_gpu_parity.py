@@ -296,3 +296,23 @@ def test_silhouette_large_n_and_h2_path(gpu, oracle):
         for q in range(2):
             want = oracle.silhouette(oracle.distances(Xs[l]), labs[q])
             assert abs(a[l].silhouette[q] - want) < 1e-9, (l, q)
+
+
+def test_torus2048_maxdim1_invariants(gpu):
+    """Top of the north-star N range (N=2048, H0/H1; the CPU oracle needs about a
+    minute here, so this case is checked through size-independent properties):
+    one component at the enclosing radius, forest = N - 1 edges, every H1 column
+    paired or essential, two dominant H1 classes, bitwise-repeatable."""
+    X = gpu.synthetic.torus(2048, seed=3)
+    a = gpu.ripser_batch(X[None], maxdim=1)[0]
+    b = gpu.ripser_batch(X[None], maxdim=1)[0]
+    for d in range(2):
+        assert _pairs(a, d) == _pairs(b, d) and a.checksum[d] == b.checksum[d]
+    assert int(np.isinf(a.dgms[0][:, 1]).sum()) == 1
+    assert a.n_all_pairs[0] == 2047
+    assert a.n_columns[1] == a.num_edges - a.n_all_pairs[0]
+    assert a.n_columns[1] == a.n_all_pairs[1] + int(np.isinf(a.dgms[1][:, 1]).sum())
+    births = a.dgms[1][:, 0]
+    assert np.all(np.diff(births) <= 0)  # emission order: decreasing birth
+    pers = np.sort(a.dgms[1][:, 1] - a.dgms[1][:, 0])[::-1]
+    assert pers[1] > 2.0 * pers[2]
