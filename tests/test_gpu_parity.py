@@ -316,3 +316,13 @@ def test_torus2048_maxdim1_invariants(gpu):
     assert np.all(np.diff(births) <= 0)  # emission order: decreasing birth
     pers = np.sort(a.dgms[1][:, 1] - a.dgms[1][:, 0])[::-1]
     assert pers[1] > 2.0 * pers[2]
+
+
+@pytest.mark.parametrize("n,maxdim", [(180, 1), (324, 2)])
+def test_adversarial_sizes_vs_oracle(gpu, oracle, n, maxdim):
+    """The point counts of the adversarial experiment's ripser call
+    (analyze_adversarial_tda.py:100; 180 / 324 clouds) on a noisy
+    torus: pairs, indices and checksums bit-exact against the oracle."""
+    X = gpu.synthetic.torus(n, seed=n)
+    res = gpu.ripser_batch(X[None], maxdim=maxdim)[0]
+    assert_same(res, oracle.rips(X, maxdim=maxdim), maxdim, f"torus{n}")
