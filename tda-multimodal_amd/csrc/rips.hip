@@ -239,9 +239,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
             p.o_wp = take(L * p.wcap_g / 4 * 4);   // bucket fill counters
         }
         if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
-        if (p.big && getenv_is("TDA_BIG_P1", "1")) {
-            // parallel H1 phase 1 (EXPERIMENTAL, opt-in: not parity-green yet at N >= 128):
-            // ~64 radix-heap workspaces in all (10 GB at N > 640 of the 288 GB HBM)
+        if (p.big && !getenv_is("TDA_BIG_P1", "0")) {
+            // parallel H1 phase 1 (k_big_phase1): ~64 radix-heap workspaces in all
+            // (10 GB at N > 640 of the 288 GB HBM); TDA_BIG_P1=0 disables it
             p.b1G = (int)std::max<int64_t>(1, 64 / L);
             p.b1cap = std::min<uint64_t>(p.wcap_g, 1ull << 20);
             p.b1pool = std::min<uint64_t>((uint64_t)p.b1G * p.b1cap, 1ull << 25);
@@ -947,7 +947,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 MARK("k_big_phase1");
             }
             hipLaunchKernelGGL(k_reduce_big, dim3(L), dim3(kBigT), 0, s, dist, n, p.maxdim, stats, db[1], db[2], rb, gb, pairs1,
-                               pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0, pb1, p.b1G ? 1 : 0);
+                               pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0, pb1,
+                               (p.b1G && !getenv_is("TDA_BIG_P1", "2")) ? 1 : 0);  // 2: run phase 1, ignore it (debug)
         } else if (p.lds_mode) {
             if (p2) TDA_LAUNCH_RED(true, true, true); else if (p1) TDA_LAUNCH_RED(true, true, false); else TDA_LAUNCH_RED(true, false, false);
         } else {

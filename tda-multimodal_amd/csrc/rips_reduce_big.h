@@ -473,22 +473,8 @@ __global__ __launch_bounds__(kBigT) void k_big_phase1(const float* __restrict__ 
                 wr += tot;
             }
             len = (uint32_t)live;
-#ifdef TDA_PROFILE
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t z = 0;
-                for (uint32_t e = 0; e < len; ++e) z += pool[off + e] == 0;
-                if (z || j == 14) printf("[p1] col %llu saved len %u off %llu zeros %u wr %llu c %u\n", (unsigned long long)j, len,
-                                (unsigned long long)off, z, (unsigned long long)wr, c);
-            }
-#endif
             break;
         }
-#ifdef TDA_PROFILE
-        if (tid == 0 && defer)
-            printf("[p1] layer %d col %llu adds %u defer %d err %d piv %016llx len %u off %llu cnt %u\n", l, (unsigned long long)j,
-                   adds, (int)defer, S.err, (unsigned long long)pk, len, (unsigned long long)off, S.cnt);
-#endif
         if (tid == 0) {
             const size_t q = (size_t)l * b.rcap + j;
             pb.piv[q] = pk;
@@ -536,7 +522,6 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
     Pair* P = pairs + (size_t)l * pcap;
     uint64_t cs = 0, npairs = 0, nadds = 0, nskip = 0;
 #ifdef TDA_PROFILE
-    int dbg_n = 0;
     // cob0, pop_min, owner adds, apparent adds, store R_j, reset, (owner adds << 40 | owner entries), total
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_all = clock64();
@@ -588,10 +573,6 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             continue;
         }
         bool resume = false;
-#ifdef TDA_PROFILE
-        uint64_t dbg_prev = kEmpty64;
-        int64_t dbg_owner = -1;
-#endif
         if (p1) {
             const size_t q = (size_t)l * b.rcap + j;
             const uint32_t inf = ld_glb((const uint32_t*)p1->info, q);
@@ -619,6 +600,9 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                 const uint64_t* sp = p1->pool + (size_t)l * p1->pool_cap + so;
                 if (owner < 0) {  // free pivot: pair now; the saved column is R_j
                     nadds += inf;
+                    // every wave has read pivg / the map for this pivot before tid 0 publishes it
+                    // (a lagging wave would otherwise see its own column as the owner)
+                    __syncthreads();
                     if (tid == 0) {
                         if (pd > sdm) {
                             uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
@@ -645,26 +629,8 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                     rused += wr;
                     continue;
                 }
-                // owned pivot: the column is reduced serially from its coboundary
-#ifdef TDA_BIG_RESUME
+                // owned pivot: rebuild the phase-1 working column and continue serially
                 nadds += inf;
-#ifdef TDA_PROFILE
-                if (tid == 0) {
-                    uint32_t z = 0;
-                    uint64_t mn = kEmpty64;
-                    for (uint32_t e = 0; e < sl; ++e) {
-                        z += sp[e] == 0;
-                        mn = sp[e] < mn ? sp[e] : mn;
-                    }
-                    const uint64_t r0 = ld_glb((const uint64_t*)roff, owner);
-                    const uint32_t rl = ld_glb((const uint32_t*)rlen, owner);
-                    uint64_t omn = kEmpty64;
-                    for (uint32_t e = 0; e < rl; ++e) omn = rpool[r0 + e] < omn ? rpool[r0 + e] : omn;
-                    printf("[ser] col %llu resume: so %llu sl %u zeros %u pk %016llx min %016llx owner %lld (roff %llu rlen %u min %016llx) rused %llu\n",
-                           (unsigned long long)j, (unsigned long long)so, sl, z, (unsigned long long)pk, (unsigned long long)mn,
-                           (long long)owner, (unsigned long long)r0, rl, (unsigned long long)omn, (unsigned long long)rused);
-                }
-#endif
                 if (tid == 0) S.last = (uint32_t)(pk >> 32);
                 __syncthreads();
                 for (uint32_t e0 = 0; e0 < sl; e0 += kBigT) {
@@ -672,7 +638,6 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                     H.toggle_pass(e < sl ? ld_glb(sp, e) : 0, e < sl);
                 }
                 resume = true;
-#endif
             }
         }
         if (!resume) {
@@ -686,11 +651,6 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             TDA_STAMP(t_p0);
             const uint64_t pk = H.pop_min();
             TDA_ACC(1, t_p0);
-#ifdef TDA_PROFILE
-            if (resume && step < 3 && tid == 0 && j < 12)
-                printf("[ser] col %llu step %llu pop %016llx last %08x cnt %u\n", (unsigned long long)j, (unsigned long long)step,
-                       (unsigned long long)pk, S.last, S.cnt);
-#endif
             if (step >= gb.step_limit) {
                 if (tid == 0) {
                     printf("k_reduce_big: layer %d dim %d column %llu (idx %llu) step limit: pivot %016llx cnt %u last %08x resume %d\n", l,
@@ -715,25 +675,6 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             const float pd = __uint_as_float((uint32_t)(pk >> 32));
             const bool app = (ld_glb((const uint32_t*)pivg, pidx >> 5) >> (pidx & 31)) & 1u;
             const int64_t owner = app ? map.find((uint32_t)pidx, ln) : -1;
-#ifdef TDA_PROFILE
-            if (pk == dbg_prev && pk != kEmpty64 && tid == 0 && dbg_n < 3) {
-                ++dbg_n;
-                const uint64_t o0d = ld_glb((const uint64_t*)roff, dbg_owner);
-                const uint32_t old = ld_glb((const uint32_t*)rlen, dbg_owner);
-                uint64_t mn = kEmpty64;
-                bool has = false;
-                for (uint32_t e = 0; e < old; ++e) {
-                    const uint64_t k = rpool[o0d + e];
-                    mn = k < mn ? k : mn;
-                    has |= k == pk;
-                }
-                printf("[dbg] col %llu resume %d: pivot %016llx repeats after adding owner %lld (off %llu len %u min %016llx has %d) app %d\n",
-                       (unsigned long long)j, (int)resume, (unsigned long long)pk, (long long)dbg_owner, (unsigned long long)o0d, old,
-                       (unsigned long long)mn, (int)has, (int)app);
-            }
-            dbg_prev = pk;
-            dbg_owner = owner;
-#endif
             TDA_STAMP(t_a0);
             if (owner >= 0) {
                 const uint64_t o0 = ld_glb((const uint64_t*)roff, owner);
@@ -754,6 +695,7 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                 ++nadds;
                 TDA_ACC(3, t_a0);
             } else {
+                __syncthreads();  // all waves decided before tid 0 publishes the pivot (see the phase-1 path)
                 if (tid == 0) {
                     if (pd > sdm) {
                         uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
