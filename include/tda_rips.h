@@ -113,6 +113,10 @@ typedef struct tda_rips_result {
 } tda_rips_result;
 
 #define TDA_FLAG_STAGE_TIMES 1
+/* with TDA_FLAG_STAGE_TIMES: run every stage on one stream so each stage time
+ * is one kernel's duration (no overlap with, or queueing behind, the side
+ * streams); for per-kernel measurement only */
+#define TDA_FLAG_STAGE_SERIAL 2
 
 /* Batched point clouds (or distance matrices) -> persistence diagrams. */
 int tda_rips_batch(const tda_rips_args *args, tda_rips_result **out);

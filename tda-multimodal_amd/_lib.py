@@ -74,6 +74,7 @@ class RipsResult(ctypes.Structure):
 
 
 TDA_FLAG_STAGE_TIMES = 1
+TDA_FLAG_STAGE_SERIAL = 2
 
 
 # every symbol declared in include/tda_rips.h

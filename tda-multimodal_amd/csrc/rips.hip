@@ -346,8 +346,10 @@ struct StageTimer {
     hipStream_t s;
     bool on;
     std::vector<const char*> names;
+    StageTimer* fwd = nullptr;  // serial stage timing: marks go to the main stream's timer
     hipError_t rec(hipEvent_t e) { return hipEventRecord(e, s); }
     int mark(const char* name) {
+        if (fwd) return fwd->mark(name);
         if (!on) return 0;
         size_t i = names.size() + 1;
         while (ev.size() <= i) {
@@ -360,7 +362,7 @@ struct StageTimer {
         return 0;
     }
     int begin() {
-        if (!on) return 0;
+        if (!on || fwd) return 0;
         while (ev.empty()) {
             hipEvent_t e;
             HIPC(hipEventCreate(&e));
@@ -594,10 +596,24 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         std::memcpy(w.hsil, a.labels, (size_t)nls * n * 4);
     }
 
+    // TDA_FLAG_STAGE_SERIAL: every stage on the main stream, so each pair of
+    // events brackets one kernel only (no time spent queued behind the side
+    // streams' kernels); the side streams are restored on return
+    const bool serial_stages = (a.flags & TDA_FLAG_STAGE_TIMES) && (a.flags & TDA_FLAG_STAGE_SERIAL);
+    struct StreamSwap {
+        Workspace& w;
+        hipStream_t s2, s3, s4;
+        bool on;
+        ~StreamSwap() {
+            if (on) w.stream2 = s2, w.stream3 = s3, w.stream4 = s4;
+        }
+    } swap_guard{w, w.stream2, w.stream3, w.stream4, serial_stages};
+    if (serial_stages) w.stream2 = w.stream3 = w.stream4 = s;
     StageTimer tm{w.stage_ev, s, (a.flags & TDA_FLAG_STAGE_TIMES) != 0, {}};
     StageTimer tm2{w.stage_ev2, w.stream2, tm.on, {}};
     StageTimer tm3{w.stage_ev3, w.stream3, tm.on, {}};
     StageTimer tm4{w.stage_ev4, w.stream4, tm.on, {}};
+    if (serial_stages) tm2.fwd = tm3.fwd = tm4.fwd = &tm;
     GraphKey gk;
     std::memset(&gk, 0, sizeof(gk));
     gk.L = p.L;

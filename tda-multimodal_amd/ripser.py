@@ -189,7 +189,8 @@ def encode_labels(label_sets, n: int) -> np.ndarray:
 
 
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
-                 want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None):
+                 want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None,
+                 stage_serial: bool = False):
     """Persistence of L layers in one call.
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
@@ -243,7 +244,7 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     a.modulus = 2
     a.device = int(device)
     a.want_dist = 1 if want_dist else 0
-    a.flags = _lib.TDA_FLAG_STAGE_TIMES if stage_times else 0
+    a.flags = (_lib.TDA_FLAG_STAGE_TIMES | (_lib.TDA_FLAG_STAGE_SERIAL if stage_serial else 0)) if stage_times else 0
     lab = None
     if labels is not None:
         lab = encode_labels(labels, N)
