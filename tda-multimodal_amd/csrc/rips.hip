@@ -54,8 +54,8 @@ constexpr uint64_t kRCapMax = 1ull << 22;    // residual columns per layer and d
 constexpr uint64_t kPCapMax = 1ull << 16;    // emitted pairs per layer and dim (H>=1)
 constexpr int kLdsMax = 160 * 1024;
 constexpr int kSmallN = 64;                  // one-wave H0 + LDS-resident reduction up to here
-constexpr int kAppLdsMaxN = 128;
-constexpr int kBigMinN = 256;                // k_reduce_big above this N (global mode)             // k_apparent stages the distance matrix in LDS up to here
+constexpr int kAppLdsMaxN = 128;             // k_apparent stages the distance matrix in LDS up to here
+constexpr int kBigMinN = 256;                // large-N reducer above this N (global mode)
 
 // ------------------------------------------------------------------ plan
 struct Plan {
@@ -304,7 +304,7 @@ struct Workspace {
     OutPair* hout = nullptr;  // host-mapped
     OutPair* hout_dev = nullptr;
     size_t hout_cap = 0;      // in pairs
-    LayerStats* hstats = nullptr;  // host-mapped: k_compact writes it
+    LayerStats* hstats = nullptr;  // host-mapped: k_emit writes it
     char* hsil = nullptr;          // host-mapped: silhouette labels [S][N] i32, then scores [L][S] f64
     char* hsil_dev = nullptr;
     size_t hsil_cap = 0;
@@ -329,7 +329,7 @@ struct Workspace {
 // a single hipGraphLaunch when the same plan, input address and flags recur
 struct GraphKey {
     int64_t L, N, D;
-    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets;
+    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets, sil_K;
     float thresh;
     const void* x;
     uint64_t gen;
@@ -630,6 +630,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.b1G ? 1 << 8 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
+    gk.sil_K = sil_K;  // baked into the k_silhouette launch (argument K and its LDS size)
     gk.x = xsrc;
     gk.gen = w.gen;
     GraphEntry* ge = nullptr;

@@ -9,9 +9,12 @@
 //   k_h0 / k_h0_wave enclosing radius, num_edges, spanning forest, H0 pairs (a3, a4)
 //   k_apparent<d>   column enumeration + apparent-pair test     (a5, parallel part)
 //   k_sort_resid    per-layer sort of the residual columns
-//   k_reduce2<d>    Z/2 cohomology reduction of residual columns (a5, serial part; rips_reduce.h)
-//   k_finalize      per-layer emission order of the pairs        (a6)
-//   k_compact       pack all layers' pairs into the host-mapped result
+//   k_emit          per-layer emission order of the pairs, packed into the
+//                   host-mapped result                           (a6)
+//   k_silhouette    sklearn silhouette_score on the same distances (8f row 1)
+// The residual reductions are in rips_reduce.h (one wave per layer),
+// rips_reduce_small.h (N <= 64 dense chain), rips_reduce_par.h (large N,
+// many columns in flight) and rips_reduce_big.h (its fallback).
 #pragma once
 #include "rips_device.h"
 
@@ -744,88 +747,17 @@ struct PairSet {
     uint64_t cap[4];
 };
 
-// ------------------------------------------------------------------ finalize
-// Emission order of dims >= 1 (reference: births_and_deaths_by_dim filled in
-// column order, i.e. birth desc / column index asc; pinned 32/32 by
-// summary_stats.json all_h1_persistence_values).
-__global__ __launch_bounds__(1024) void k_finalize(LayerStats* __restrict__ stats, int maxdim, PairSet ps, uint64_t* __restrict__ skeys,
-                                                   uint32_t* __restrict__ svals, uint64_t sstride, int sort_log2) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x;
-    const uint64_t CH = 1ull << sort_log2;
-    uint64_t* sk = (uint64_t*)smem;
-    uint32_t* sv = (uint32_t*)(sk + CH);
-    for (int d = 1; d <= maxdim; ++d) {
-        uint64_t cnt = (uint64_t)stats[l].count[d];
-        if (cnt > ps.cap[d]) cnt = ps.cap[d];
-        if (cnt < 2) continue;
-        Pair* P = ps.p[d] + (size_t)l * ps.cap[d];
-        uint64_t* k = skeys + (size_t)l * sstride * 2;
-        uint32_t* v = svals + (size_t)l * sstride * 2;
-        for (uint64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-            k[e] = col_key(P[e].birth, (uint64_t)P[e].birth_idx);
-            v[e] = (uint32_t)e;
-        }
-        __syncthreads();
-        block_sort<true>(k, v, cnt, k + sstride, v + sstride, sk, sv, sort_log2);
-        // permute through the scratch (pairs -> scratch bytes -> pairs)
-        Pair* tmpP = (Pair*)(k + sstride);  // sstride*8 bytes >= cnt*24? ensured by host (sstride >= 3*pcap)
-        for (uint64_t e = threadIdx.x; e < cnt; e += blockDim.x) tmpP[e] = P[v[e]];
-        __syncthreads();
-        for (uint64_t e = threadIdx.x; e < cnt; e += blockDim.x) P[e] = tmpP[e];
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------ compact
-// Pack every (layer, dim) segment into the host-mapped output.
+// ------------------------------------------------------------------ output
 struct OutPair {
     float birth, death;
     int64_t birth_idx, death_idx;
 };
-// The layer stats and segment offsets also go straight to host-mapped memory
-// (no copy kernels after this one).
-__global__ __launch_bounds__(1024) void k_compact(LayerStats* __restrict__ stats, int L, int maxdim, PairSet ps, int64_t* __restrict__ out_off,
-                                                  OutPair* __restrict__ out, uint64_t out_cap, LayerStats* __restrict__ stats_host) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int64_t* off = (int64_t*)smem;  // L*nd + 1
-    const int nd = maxdim + 1, S = L * nd, t = threadIdx.x;
-    for (int i = t; i < S; i += blockDim.x) {
-        int l = i / nd, d = i % nd;
-        int64_t c = stats[l].count[d];
-        if ((uint64_t)c > ps.cap[d]) c = (int64_t)ps.cap[d];
-        off[i + 1] = c;
-    }
-    __syncthreads();
-    if (t == 0) {
-        off[0] = 0;
-        for (int i = 1; i <= S; ++i) off[i] += off[i - 1];
-        if ((uint64_t)off[S] > out_cap)
-            for (int l = 0; l < L; ++l) stats[l].err |= ERR_OUT_CAP;
-    }
-    __syncthreads();
-    for (int i = t; i < S; i += blockDim.x) out_off[i] = off[i];
-    {
-        static_assert(sizeof(LayerStats) % 8 == 0, "LayerStats copies as u64 words");
-        const uint64_t* src = (const uint64_t*)stats;
-        uint64_t* dst = (uint64_t*)stats_host;
-        const int nw8 = L * (int)(sizeof(LayerStats) / 8);
-        for (int i = t; i < nw8; i += blockDim.x) dst[i] = src[i];
-    }
-    if ((uint64_t)off[S] > out_cap) return;
-    const int w = t >> 6, ln = t & 63, nw = blockDim.x >> 6;
-    for (int i = w; i < S; i += nw) {
-        const int l = i / nd, d = i % nd;
-        const int64_t c = off[i + 1] - off[i];
-        const Pair* P = ps.p[d] + (size_t)l * ps.cap[d];
-        OutPair* o = out + off[i];
-        for (int64_t e = ln; e < c; e += 64) o[e] = OutPair{P[e].birth, P[e].death, P[e].birth_idx, P[e].death_idx};
-    }
-}
 
 // ------------------------------------------------------------------ emit
-// k_finalize + k_compact in one launch: block l sorts its layer's dims >= 1
-// into emission order and writes every segment straight into the host-mapped
+// Emission order of dims >= 1 (reference: births_and_deaths_by_dim filled in
+// column order, i.e. birth desc / column index asc; pinned 32/32 by
+// summary_stats.json all_h1_persistence_values).  Block l sorts its layer's
+// dims >= 1 into emission order and writes every segment straight into the host-mapped
 // output at its global offset (a prefix over the stats' counts, recomputed
 // per block), then its LayerStats.  LDS: the sort chunk (8 KiB keys * 12 B)
 // and 16 x 2 words of reduction scratch behind it.

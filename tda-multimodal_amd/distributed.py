@@ -3,15 +3,26 @@
 SURVEY 8(e): layers are independent units, so each rank takes a contiguous
 block of layers, runs the batched GPU pipeline on its shard with no data-path
 collective, and the only exchange is ONE gather of fixed-size per-layer
-summary records (``pipeline.pack_record``) to rank 0 -- over RCCL/xGMI
-(backend "nccl") on the GPU box, gloo in CPU tests.  The reference itself is a
-single-process loop (debug_tda_pipeline.py:92); this is the build's addition.
+summary records to rank 0 -- over RCCL/xGMI (backend "nccl") on the GPU box,
+gloo in CPU tests.  The reference itself is a single-process loop
+(debug_tda_pipeline.py:92); this is the build's addition.
+
+Record size: the records carry every finite H1/H2 persistence value (the
+reference writes them all, debug_tda_pipeline.py:125).  Their number is only
+known after the reduction, so a step is a one-scalar all-reduce (MAX of the
+per-layer value counts) followed by the payload gather padded to that global
+maximum -- nothing is truncated.
+
+Collective: ``torch.distributed.gather`` (on "nccl" it is RCCL point-to-point
+sends inside one group call, i.e. what RCCL's ``ncclGather`` extension does,
+rccl.h:745).  The payload is ~1 KB per layer, so it is a single latency-bound
+xGMI hop either way.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .pipeline import REC_LEN, pack_record, unpack_record
+from .pipeline import pack_results, rec_len, unpack_record
 
 
 def shard_range(n_layers: int, rank: int, world: int) -> tuple[int, int]:
@@ -22,29 +33,101 @@ def shard_range(n_layers: int, rank: int, world: int) -> tuple[int, int]:
     return lo, hi
 
 
-def gather_records(records: list, n_layers: int, dist=None, device=None) -> list | None:
-    """Gather every rank's packed records to rank 0 (returns None elsewhere).
-
-    Uses all_gather_into_tensor on a fixed-size padded buffer (ceil(L/W)
-    records per rank), which maps to a single RCCL collective on "nccl".
-    """
+def _gather_packed(packed: np.ndarray, per: int, cap: int, dist, device):
+    """Gather (per, rec_len(cap)) float64 rows from every rank to rank 0."""
     import torch
-    import torch.distributed as tdist
 
-    dist = dist or tdist
     world, rank = dist.get_world_size(), dist.get_rank()
-    per = -(-n_layers // world)
-    buf = np.full((per, REC_LEN), np.nan, dtype=np.float64)
-    for i, r in enumerate(records):
-        buf[i] = pack_record(r)
+    buf = np.full((per, rec_len(cap)), np.nan, dtype=np.float64)
+    buf[:packed.shape[0]] = packed
     t = torch.from_numpy(buf)
     if device is not None:
         t = t.to(device)
-    out = torch.empty((world * per, REC_LEN), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, t)
+    outs = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, outs, dst=0)
     if rank != 0:
         return None
-    rows = out.cpu().numpy()
-    recs = [unpack_record(v) for v in rows if not np.isnan(v[0])]
-    recs.sort(key=lambda r: r["layer"])
-    return recs
+    rows = torch.cat(outs).cpu().numpy()
+    return rows[~np.isnan(rows[:, 0])]
+
+
+def _global_cap(local_cap: int, dist, device) -> int:
+    import torch
+
+    t = torch.tensor([local_cap], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
+
+
+def gather_packed(packed: np.ndarray, local_cap: int, n_layers: int, dist=None, device=None):
+    """All-reduce the value capacity, then gather every rank's packed rows
+    (``pipeline.pack_results`` output) to rank 0; returns the (n_layers, ...)
+    rows sorted by layer on rank 0, None elsewhere."""
+    import torch.distributed as tdist
+
+    dist = dist or tdist
+    world = dist.get_world_size()
+    cap = _global_cap(local_cap, dist, device)
+    if packed.shape[1] != rec_len(cap):  # re-pad to the global capacity
+        packed = _repad(packed, local_cap, cap)
+    per = -(-n_layers // world)
+    rows = _gather_packed(packed, per, cap, dist, device)
+    if rows is None:
+        return None
+    return rows[np.argsort(rows[:, 0], kind="stable")], cap
+
+
+def _repad(packed: np.ndarray, old: int, new: int) -> np.ndarray:
+    from .pipeline import REC_HDR
+
+    out = np.zeros((packed.shape[0], rec_len(new)), dtype=np.float64)
+    out[:, :REC_HDR] = packed[:, :REC_HDR]
+    out[:, REC_HDR:REC_HDR + old] = packed[:, REC_HDR:REC_HDR + old]
+    out[:, REC_HDR + new:REC_HDR + new + old] = packed[:, REC_HDR + old:REC_HDR + 2 * old]
+    return out
+
+
+def gather_records(records: list, n_layers: int, dist=None, device=None) -> list | None:
+    """Dict-record form of :func:`gather_packed` (records from
+    ``pipeline.layer_record``); returns the full sorted list on rank 0."""
+    from .pipeline import pack_record
+
+    cap = max([1] + [max(len(r["all_h1_persistence_values"]), len(r.get("all_h2_persistence_values", [])))
+                     for r in records])
+    packed = np.stack([pack_record(r, cap) for r in records]) if records else np.zeros((0, rec_len(cap)))
+    out = gather_packed(packed, cap, n_layers, dist, device)
+    if out is None:
+        return None
+    rows, cap = out
+    return [unpack_record(v, cap) for v in rows]
+
+
+def sharded_sweep_step(X, maxdim: int, rank: int, world: int, dist=None, device=None, layer_base: int = 0,
+                       shard: bool = True, run=None):
+    """One multi-GPU step of the layer sweep (bench.py runs exactly this).
+
+    X: the (L, N, D) sweep (resident on this rank's GPU, or numpy).
+    shard=True  (strong scaling, configs[2]/[4]): this rank takes layers
+                shard_range(L, rank, world) of X;
+    shard=False (weak scaling): this rank takes all of X, as layers
+                [rank * L, (rank + 1) * L) of a world * L sweep.
+    run: the per-shard batch call (default ``ripser_batch``; CPU tests pass
+    an oracle-backed stand-in with the same result interface).
+    Returns the gathered packed rows (sorted by layer) and the capacity on
+    rank 0, (None, None) elsewhere.
+    """
+    from .ripser import ripser_batch
+
+    run = run or ripser_batch
+    L = int(X.shape[0])
+    if shard:
+        lo, hi = shard_range(L, rank, world)
+        total = L
+    else:
+        lo, hi = 0, L
+        total = L * world
+    ids = np.arange(lo, hi) + (layer_base if shard else rank * L)
+    res = run(X[lo:hi], maxdim=maxdim) if hi > lo else []
+    packed, cap = pack_results(res, ids, maxdim)
+    out = gather_packed(packed, cap, total, dist, device)
+    return out if out is not None else (None, None)

@@ -24,8 +24,6 @@ import numpy as np
 
 from .ripser import ripser_batch
 
-H_CAP = 64  # per-layer persistence values carried in a packed record
-
 
 def get_persistence(dgm: np.ndarray):
     """debug_tda_pipeline.py:79-89."""
@@ -106,54 +104,103 @@ def peak_layer(records: list) -> int:
     return int(np.argmax([r["silhouette_shape"] for r in records]))
 
 
-# ---- fixed-size packed record (the payload gathered across ranks) ----------
-REC_LEN = 8 + 2 * (1 + H_CAP) + 2
+# ---- packed record (the payload gathered across ranks) ---------------------
+# [layer, n_h0_inf, max_h0, n_h1, max_h1, n_h2 (-1: no H2), max_h2,
+#  silhouette_shape, silhouette_color, h1[cap], h2[cap]] as float64; NaN marks
+# an absent silhouette.  cap = the largest per-layer value count of the step
+# (distributed.gather_packed agrees on it across ranks), so nothing is cut.
+REC_HDR = 9
 
 
-def pack_record(rec: dict) -> np.ndarray:
-    """[layer, n_h0_inf, max_h0, n_h1, max_h1, n_h2, max_h2, overflow,
-        n1, h1[H_CAP], n2, h2[H_CAP], silhouette_shape, silhouette_color]
-    as float64 (NaN marks an absent silhouette)."""
-    v = np.zeros(REC_LEN, dtype=np.float64)
+def rec_len(cap: int) -> int:
+    return REC_HDR + 2 * cap
+
+
+def pack_record(rec: dict, cap: int) -> np.ndarray:
     h1 = rec["all_h1_persistence_values"]
     h2 = rec.get("all_h2_persistence_values", [])
-    v[0] = rec["layer"]
-    v[1] = rec["n_h0_features"]
-    v[2] = rec["max_h0_persistence"]
-    v[3] = rec["n_h1_features"]
-    v[4] = rec["max_h1_persistence"]
-    v[5] = rec.get("n_h2_features", -1)
-    v[6] = rec.get("max_h2_persistence", 0.0)
-    v[7] = float(len(h1) > H_CAP or len(h2) > H_CAP)
-    v[8] = min(len(h1), H_CAP)
-    v[9:9 + int(v[8])] = h1[:H_CAP]
-    o = 9 + H_CAP
-    v[o] = min(len(h2), H_CAP)
-    v[o + 1:o + 1 + int(v[o])] = h2[:H_CAP]
-    v[-2] = rec.get("silhouette_shape", np.nan)
-    v[-1] = rec.get("silhouette_color", np.nan)
+    if len(h1) > cap or len(h2) > cap:
+        raise ValueError(f"record of layer {rec['layer']} holds more than cap={cap} values")
+    v = np.zeros(rec_len(cap), dtype=np.float64)
+    v[:REC_HDR] = (rec["layer"], rec["n_h0_features"], rec["max_h0_persistence"], rec["n_h1_features"],
+                   rec["max_h1_persistence"], rec.get("n_h2_features", -1), rec.get("max_h2_persistence", 0.0),
+                   rec.get("silhouette_shape", np.nan), rec.get("silhouette_color", np.nan))
+    v[REC_HDR:REC_HDR + len(h1)] = h1
+    v[REC_HDR + cap:REC_HDR + cap + len(h2)] = h2
     return v
 
 
-def unpack_record(v: np.ndarray) -> dict:
-    n1 = int(v[8])
-    o = 9 + H_CAP
-    n2 = int(v[o])
+def unpack_record(v: np.ndarray, cap: int) -> dict:
+    """Inverse of pack_record: the dict of layer_record (same keys, same order)."""
+    n1, n2 = int(v[3]), int(v[5])
     rec = {
         "layer": int(v[0]),
-        "n_h1_features": int(v[3]),
+        "n_h1_features": n1,
         "max_h1_persistence": float(v[4]),
-        "all_h1_persistence_values": v[9:9 + n1].tolist(),
+        "all_h1_persistence_values": v[REC_HDR:REC_HDR + n1].tolist(),
         "n_h0_features": int(v[1]),
         "max_h0_persistence": float(v[2]),
     }
-    if not np.isnan(v[-2]):
-        rec["silhouette_shape"] = float(v[-2])
-    if not np.isnan(v[-1]):
-        rec["silhouette_color"] = float(v[-1])
-    if v[5] >= 0:
-        rec["n_h2_features"] = int(v[5])
+    if not np.isnan(v[7]):
+        rec["silhouette_shape"] = float(v[7])
+    if not np.isnan(v[8]):
+        rec["silhouette_color"] = float(v[8])
+    if n2 >= 0:
+        rec["n_h2_features"] = n2
         rec["max_h2_persistence"] = float(v[6])
-        rec["all_h2_persistence_values"] = v[o + 1:o + 1 + n2].tolist()
-    rec["_truncated"] = bool(v[7])
+        rec["all_h2_persistence_values"] = v[REC_HDR + cap:REC_HDR + cap + n2].tolist()
     return rec
+
+
+def pack_results(results: list, layer_ids, maxdim: int):
+    """Packed records of a batch's LayerResults in a few vectorised numpy
+    passes (no per-layer Python work): the same values layer_record computes
+    (get_persistence of dgms[0..2], debug_tda_pipeline.py:79-89, :121-130).
+    Returns (rows (L, rec_len(cap)), cap)."""
+    L = len(results)
+    nd = maxdim + 1
+    if L and all(getattr(r, "_b", None) is getattr(results[0], "_b", None) is not None for r in results):
+        b = results[0]._b
+        ls = np.fromiter((r._l for r in results), dtype=np.int64, count=L)
+        cnt, off, pairs = b.cnt[ls][:, :nd], b.off[ls][:, :nd], b.pairs
+    else:  # generic results (anything with .dgms)
+        cnt = np.array([[len(r.dgms[d]) for d in range(nd)] for r in results], dtype=np.int64).reshape(L, nd)
+        flat = [r.dgms[d] for r in results for d in range(nd)]
+        pairs = np.concatenate(flat) if flat else np.zeros((0, 2))
+        off = np.concatenate([[0], np.cumsum(cnt.ravel())[:-1]]).reshape(L, nd) if L else cnt
+    S = L * nd
+    sc, so = cnt.ravel(), off.ravel()
+    tot = int(sc.sum())
+    seg = np.repeat(np.arange(S), sc)
+    first = np.concatenate([[0], np.cumsum(sc)[:-1]]) if S else sc
+    p = pairs[np.repeat(so - first, sc) + np.arange(tot)]
+    pers = p[:, 1] - p[:, 0]
+    fin = np.isfinite(pers)
+    fseg, fval = seg[fin], pers[fin]
+    nfin = np.bincount(fseg, minlength=S)
+    mx = np.zeros(S)
+    if fval.size:
+        m = np.full(S, -np.inf)
+        np.maximum.at(m, fseg, fval)
+        mx = np.where(nfin > 0, m, 0.0)
+    nfin, mx = nfin.reshape(L, nd), mx.reshape(L, nd)
+    cap = max(1, int(nfin[:, 1:].max()) if nd > 1 and L else 1)
+    out = np.zeros((L, rec_len(cap)), dtype=np.float64)
+    out[:, 0] = np.asarray(layer_ids, dtype=np.float64)[:L]
+    out[:, 1] = cnt[:, 0] - nfin[:, 0]
+    out[:, 2] = mx[:, 0]
+    if nd > 1:
+        out[:, 3], out[:, 4] = nfin[:, 1], mx[:, 1]
+    out[:, 5] = nfin[:, 2] if nd > 2 else -1
+    out[:, 6] = mx[:, 2] if nd > 2 else 0.0
+    out[:, 7:9] = np.nan
+    for q, r in enumerate(results):
+        sil = r.silhouette if hasattr(r, "silhouette") else []
+        out[q, 7:7 + min(2, len(sil))] = sil[:2]
+    if fval.size:
+        ffirst = np.concatenate([[0], np.cumsum(nfin.ravel())[:-1]])
+        rank = np.arange(fval.size) - ffirst[fseg]
+        lay, dim = fseg // nd, fseg % nd
+        sel = dim >= 1
+        out[lay[sel], REC_HDR + (dim[sel] - 1) * cap + rank[sel]] = fval[sel]
+    return out, cap

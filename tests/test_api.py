@@ -48,9 +48,40 @@ def test_pack_unpack_roundtrip(pkg):
     rec = {"layer": 7, "n_h1_features": 2, "max_h1_persistence": 0.5, "all_h1_persistence_values": [0.5, 0.125],
            "n_h0_features": 1, "max_h0_persistence": 3.0, "n_h2_features": 1, "max_h2_persistence": 0.25,
            "all_h2_persistence_values": [0.25]}
-    back = pipe.unpack_record(pipe.pack_record(rec))
-    assert back.pop("_truncated") is False
-    assert back == rec
+    back = pipe.unpack_record(pipe.pack_record(rec, 2), 2)
+    assert back == rec and list(back) == list(rec)
+    with pytest.raises(ValueError):
+        pipe.pack_record(rec, 1)  # never truncates silently
+
+
+class _Res:
+    def __init__(self, dgms, sil=()):
+        self.dgms, self.silhouette = dgms, list(sil)
+
+
+def test_pack_results_matches_layer_record(pkg):
+    """The vectorised packer (bench.py's per-step path) equals layer_record,
+    including > 64 persistence values per layer (nothing cut)."""
+    pipe = pkg.pipeline
+    rng = np.random.default_rng(3)
+    res, recs = [], []
+    for l, nh1 in enumerate([0, 3, 130, 1]):
+        b0 = np.sort(rng.random(5))
+        d0 = np.concatenate([[0.0] * 4, [np.inf]])
+        h0 = np.stack([np.zeros(5), np.where(np.isinf(d0), np.inf, b0)], 1)
+        b1 = rng.random(nh1 + 1)
+        h1 = np.stack([b1, b1 + rng.random(nh1 + 1)], 1)
+        h1[-1, 1] = np.inf  # one essential H1 bar per layer
+        h2 = np.stack([b1[:2], b1[:2] + 0.5], 1)
+        dg = [h0, h1, h2]
+        res.append(_Res(dg, (0.25 * l, -0.5)))
+        recs.append(pkg.layer_record(10 + l, dg, 0.25 * l, -0.5))
+    rows, cap = pipe.pack_results(res, np.arange(10, 14), 2)
+    assert cap == 130
+    assert [pipe.unpack_record(v, cap) for v in rows] == recs
+    rows1, cap1 = pipe.pack_results([_Res(r.dgms[:2]) for r in res], np.arange(4), 1)
+    back = pipe.unpack_record(rows1[2], cap1)
+    assert back["all_h1_persistence_values"] == recs[2]["all_h1_persistence_values"] and "n_h2_features" not in back
 
 
 def test_shard_range_covers_all_layers(pkg):
@@ -104,5 +135,5 @@ def test_summary_stats_writer_and_peak_layer(pkg, tmp_path):
     assert text == json.dumps(recs, indent=2)
     assert pkg.peak_layer(json.loads(text)) == 1
     pipe = __import__("importlib").import_module("tda-multimodal_amd.pipeline")
-    back = pipe.unpack_record(pipe.pack_record(recs[1]))
+    back = pipe.unpack_record(pipe.pack_record(recs[1], 1), 1)
     assert back["silhouette_shape"] == 0.7 and back["silhouette_color"] == -0.7

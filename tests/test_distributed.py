@@ -1,7 +1,8 @@
-"""CPU test of the multi-rank path: world_size 2 over gloo, layer sharding +
-one all-gather of packed per-layer records (the RCCL payload on the GPU box).
-Per-layer diagrams come from the oracle here (no GPU); the GPU variant of the
-same path is exercised by bench.py under torchrun."""
+"""CPU tests of the multi-rank path: world_size 2 over gloo.  They run the
+same function bench.py runs per step (distributed.sharded_sweep_step: layer
+shard -> batched persistence -> packed records -> capacity all-reduce -> one
+gather to rank 0), with the per-shard batch call served by the oracle (no
+GPU here; on the GPU box the same function calls ripser_batch over RCCL)."""
 import os
 import socket
 
@@ -17,7 +18,23 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+class _Res:
+    def __init__(self, dgms):
+        self.dgms, self.silhouette = dgms, []
+
+
+def _oracle_run(X, maxdim):
+    from oracle import oracle
+
+    return [_Res(oracle.rips(np.asarray(x), maxdim=maxdim)["dgms"]) for x in X]
+
+
+def _circle(n):
+    t = np.linspace(0, 2 * np.pi, n, endpoint=False)
+    return np.stack([np.cos(t), np.sin(t), 0.01 * np.cos(7 * t)], 1).astype(np.float32)
+
+
+def _worker(rank, world, port, q, case):
     import importlib
     import sys
 
@@ -28,30 +45,65 @@ def _worker(rank, world, port, q):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pkg = importlib.import_module("tda-multimodal_amd")
-    from oracle import oracle
+    pipe = pkg.pipeline
+    out = {}
+    if case == "reference":
+        clouds = pkg.synthetic.reference_clouds()
+        rows, cap = pkg.distributed.sharded_sweep_step(clouds, 1, rank, world, run=_oracle_run)
+        if rank == 0:
+            out["strong"] = [pipe.unpack_record(v, cap) for v in rows]
+        rows, cap = pkg.distributed.sharded_sweep_step(clouds[:3], 1, rank, world, shard=False, run=_oracle_run)
+        if rank == 0:
+            out["weak"] = [pipe.unpack_record(v, cap) for v in rows]
+        # dict-record form (gather_records) on an uneven shard
+        lo, hi = pkg.distributed.shard_range(5, rank, world)
+        from oracle import oracle
 
-    clouds = pkg.synthetic.reference_clouds()
-    lo, hi = pkg.distributed.shard_range(32, rank, world)
-    recs = [pkg.layer_record(l, oracle.rips(clouds[l], maxdim=1)["dgms"]) for l in range(lo, hi)]
-    out = pkg.distributed.gather_records(recs, 32)
+        recs = [pkg.layer_record(l, oracle.rips(clouds[l], maxdim=1)["dgms"]) for l in range(lo, hi)]
+        g = pkg.distributed.gather_records(recs, 5)
+        if rank == 0:
+            out["dict"] = g
+    else:  # many H1 bars on one rank only: the capacity all-reduce re-pads the other
+        X = np.stack([pkg.synthetic.torus(260, seed=7), _circle(260)])
+        rows, cap = pkg.distributed.sharded_sweep_step(X, 1, rank, world, run=_oracle_run)
+        if rank == 0:
+            out["big"] = ([pipe.unpack_record(v, cap) for v in rows], cap)
     if rank == 0:
         q.put(out)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_and_gather(summary_stats):
+def _run(case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, case)) for r in range(2)]
     for p in ps:
         p.start()
-    out = q.get(timeout=120)
+    out = q.get(timeout=240)
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    assert len(out) == 32
-    for rec, exp in zip(out, summary_stats):
-        assert rec.pop("_truncated") is False
-        assert rec == exp
+    return out
+
+
+def test_two_rank_sweep_step_matches_reference(summary_stats):
+    out = _run("reference")
+    assert out["strong"] == summary_stats  # 32 layers sharded 16 + 16
+    # weak scaling: every rank runs the same 3-layer batch as its own layers
+    assert [r["layer"] for r in out["weak"]] == [0, 1, 2, 3, 4, 5]
+    for r in out["weak"]:
+        exp = dict(summary_stats[r["layer"] % 3])
+        exp["layer"] = r["layer"]
+        assert r == exp
+    assert out["dict"] == summary_stats[:5]
+
+
+def test_two_rank_step_carries_every_value(pkg, oracle):
+    """> 64 H1 values on rank 0's layer: all of them reach rank 0."""
+    recs, cap = _run("big")["big"]
+    exp = pkg.layer_record(0, oracle.rips(pkg.synthetic.torus(260, seed=7), maxdim=1)["dgms"])
+    assert exp["n_h1_features"] > 64 and cap >= exp["n_h1_features"]
+    assert recs[0] == exp
+    assert recs[1] == pkg.layer_record(1, oracle.rips(_circle(260), maxdim=1)["dgms"])

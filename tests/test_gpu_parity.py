@@ -326,3 +326,15 @@ def test_adversarial_sizes_vs_oracle(gpu, oracle, n, maxdim):
     X = gpu.synthetic.torus(n, seed=n)
     res = gpu.ripser_batch(X[None], maxdim=maxdim)[0]
     assert_same(res, oracle.rips(X, maxdim=maxdim), maxdim, f"torus{n}")
+
+
+def test_silhouette_graph_replay_with_different_class_counts(gpu, oracle):
+    """the captured launch sequence is keyed by the class
+    count K too.  Same cloud, same N/L and one label set, first K=2 then K=6
+    then K=2 again (the reference scores one cloud under several labelings,
+    analyze_adversarial_tda.py:108-111): every score matches the oracle."""
+    X = gpu.synthetic.sweep48(1)[0]
+    Dm = oracle.distances(X)
+    for lab in (np.arange(48) % 2, np.arange(48) % 6, np.arange(48) // 24, np.arange(48) % 6):
+        got = gpu.silhouette_score(X, lab)
+        assert abs(got - oracle.silhouette(Dm, lab)) < 1e-9, int(lab.max()) + 1
