@@ -19,6 +19,7 @@
 #include "../../include/tda_rips.h"
 #include "rips_kernels.h"
 #include "rips_reduce_big.h"
+#include "rips_reduce_par.h"
 #include "rips_reduce_small.h"
 
 using namespace tda;
@@ -65,10 +66,11 @@ struct Plan {
     uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, vcap_g = 0, sstride = 0;
     bool lds_mode = false;
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
-    int b1G = 0;       // k_big_phase1 workgroups per layer (0: no parallel H1 phase 1)
-    uint64_t b1cap = 0, b1pool = 0;  // phase-1 workspace capacity, saved-column pool per layer
-    size_t o_b1log = 0, o_b1idx = 0, o_b1fill = 0, o_b1bref = 0, o_b1pool = 0, o_b1piv = 0, o_b1info = 0, o_b1off = 0,
-           o_b1len = 0;
+    bool par = false;  // H1 on k_reduce_par (many columns in flight), k_reduce_big for H2 / fallback
+    bool packed = false;  // k_reduce_par keys carry packed vertices + apparent facet (N <= 1024)
+    bool serial_tables = false;  // HBM working tables of k_reduce_all (global mode) / k_reduce_big
+    uint64_t ostride = 0, rec_cap = 0, rpool_cap = 0, bpool_cap = 0, rq_cap = 0;
+    size_t o_pctl = 0, o_pitem = 0, o_pokey = 0, o_poval = 0, o_colpiv = 0, o_prec = 0, o_prpool = 0, o_pbpool = 0, o_prq = 0;
     bool dense = false;  // N <= 64: dense-bitmap H1 chain + column-parallel H2 phase 1 (rips_reduce_small.h)
     int dK = 0;          // dense H1 bitmap words per lane (a k_h1_chain instantiation)
     uint32_t inv_stride = 0;  // rank -> edge table stride (C(N,3) rounded up)
@@ -134,7 +136,7 @@ ReduceAllCfg reduce_cfg(int n, int maxdim, const uint64_t* piv_words, bool lds_m
     return c;
 }
 
-int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
+int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par) {
     const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
     p.mst_words = (binom(N, 2) + 31) / 32 + 1;
     for (int d = 1; d <= p.maxdim; ++d) {
@@ -157,6 +159,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         // 20.6 vs 26.8 ms, torus256 md2 64 vs 91 ms); the radix heap above
         const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big");
         p.big = !p.lds_mode && (force_big || want_big || (!want_wave && p.N > kBigMinN));
+        // TDA_PAR=0: H1 on the serial k_reduce_big as well (comparison / debugging)
+        p.par = p.big && p.maxdim >= 1 && !no_par && !getenv_is("TDA_PAR", "0");
+        p.packed = p.N <= 1024;
         p.dense = p.lds_mode && p.maxdim >= 1 && p.N <= kDenseMaxN && p.N >= 3 && !want_wave;
     }
     if (p.dense) {  // carve of rips_reduce_small.h (h1_chain / h2_phase1), mirrored here
@@ -233,28 +238,34 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big) {
         p.o_voff = take(L * p.max_rcap * 8);
         uint64_t wmax = p.lds_mode ? 8192 : p.wcap_g;
         if (!p.big) p.o_wt = take(L * wmax * 8 * 2);  // slot scratch + compaction keys
-        if (!p.lds_mode) {
+        // global working tables of the one-wave / serial radix-heap kernels (not needed when
+        // k_reduce_par takes H1 and there is no H2)
+        p.serial_tables = !p.lds_mode && !(p.par && p.maxdim < 2);
+        if (p.serial_tables) {
             p.o_wk = take(L * p.wcap_g * 8);       // key log
             p.o_wl = take(L * p.wcap_g * 2 * 8);   // u64 index, 2 * wcap slots
             p.o_wp = take(L * p.wcap_g / 4 * 4);   // bucket fill counters
+            if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
         }
-        if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
-        if (p.big && !getenv_is("TDA_BIG_P1", "0")) {
-            // parallel H1 phase 1 (k_big_phase1): ~64 radix-heap workspaces in all
-            // (10 GB at N > 640 of the 288 GB HBM); TDA_BIG_P1=0 disables it
-            p.b1G = (int)std::max<int64_t>(1, 64 / L);
-            p.b1cap = std::min<uint64_t>(p.wcap_g, 1ull << 20);
-            p.b1pool = std::min<uint64_t>((uint64_t)p.b1G * p.b1cap, 1ull << 25);
-            const uint64_t P1 = (uint64_t)L * p.b1G;
-            p.o_b1log = take(P1 * p.b1cap * 8);
-            p.o_b1idx = take(P1 * p.b1cap * 2 * 8);
-            p.o_b1fill = take(P1 * (p.b1cap * 2 / 8) * 4);
-            p.o_b1bref = take(P1 * kNB * p.b1cap * 4);
-            p.o_b1pool = take(L * p.b1pool * 8);
-            p.o_b1piv = take(L * p.rcap[1] * 8);
-            p.o_b1info = take(L * p.rcap[1] * 4);
-            p.o_b1off = take(L * p.rcap[1] * 8);
-            p.o_b1len = take(L * p.rcap[1] * 4);
+        if (p.par) {
+            // k_reduce_par: owner maps, final pivots, records, bucket chunks, requeue slots
+            p.ostride = next_pow2(2 * p.rcap[1] + 16);
+            p.rec_cap = 2 * (uint64_t)L * p.rcap[1] + 4096;
+            // bucket chunks: every workgroup keeps its peak bucket sizes (torus N=1024 needs ~2^26 keys
+            // in all, N=2048 ~2^28); records: raw copies of the paired columns.  HBM is 288 GB.
+            auto clampp = [](uint64_t x, int lo, int hi) { return std::min<uint64_t>(std::max<uint64_t>(next_pow2(x), 1ull << lo), 1ull << hi); };
+            p.bpool_cap = clampp(N * N * 128, 24, 30) << scale;
+            p.rpool_cap = clampp(N * N * 64, 22, 29) << scale;
+            p.rq_cap = 1ull << 16;
+            p.o_pctl = take(sizeof(ParCtl));
+            p.o_pitem = take((L + 1) * 8);
+            p.o_pokey = take(L * p.ostride * 8);
+            p.o_poval = take(L * p.ostride * 8);
+            p.o_colpiv = take(L * p.rcap[1] * 8);
+            p.o_prec = take(p.rec_cap * 32);
+            p.o_prpool = take(p.rpool_cap * 8);
+            p.o_pbpool = take(p.bpool_cap * 8);
+            p.o_prq = take(p.rq_cap * 8);
         }
         if (p.dense) {
             p.o_recs = take(L * binom(N, 2) * 16);
@@ -329,7 +340,7 @@ struct Workspace {
 // a single hipGraphLaunch when the same plan, input address and flags recur
 struct GraphKey {
     int64_t L, N, D;
-    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets, sil_K;
+    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets, sil_K, no_par;
     float thresh;
     const void* x;
     uint64_t gen;
@@ -468,6 +479,8 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, true, false);
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
 #define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -509,13 +522,14 @@ std::string err_flags(int e) {
     if (e & ERR_VPOOL_CAP) s += " reduction-pool-capacity";
     if (e & ERR_OUT_CAP) s += " output-capacity";
     if (e & ERR_STEP_LIMIT) s += " reduction-step-limit";
+    if (e & ERR_PAR) s += " parallel-reduction-abort";
     return s;
 }
 
 // ------------------------------------------------------------------ pipeline
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
-                 bool force_global = false, int scale = 0, bool force_big = false) {
+                 bool force_global = false, int scale = 0, bool force_big = false, bool no_par = false) {
     Plan p;
     p.L = a.L;
     p.N = a.N;
@@ -523,7 +537,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     p.maxdim = a.maxdim;
     p.dtype = a.dtype;
     p.is_dist = input_kind != 0;
-    make_plan(p, force_global, scale, force_big);
+    make_plan(p, force_global, scale, force_big, no_par);
     const int dev = a.device;
     HIPC(hipSetDevice(dev));
     Workspace& w = *get_ws(dev);
@@ -627,7 +641,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.force_global = force_global;
     gk.scale = scale;
     gk.force_big = force_big;
-    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.b1G ? 1 << 8 : 0);
+    gk.no_par = no_par;
+    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
     gk.sil_K = sil_K;  // baked into the k_silhouette launch (argument K and its LDS size)
@@ -892,7 +907,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipGetLastError());
             MARK("k_sort_resid");
         }
-        if (!p.lds_mode) {
+        if (p.serial_tables) {
             HIPC(hipMemsetAsync(rb.windex, 0, (size_t)L * p.wcap_g * 2 * 8, s));
             HIPC(hipMemsetAsync(rb.wfill, 0, (size_t)L * p.wcap_g / 4 * 4, s));
         }
@@ -940,32 +955,44 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             gb.cap = p.wcap_g;
             gb.bcap = p.wcap_g;
             gb.step_limit = step_limit();
-            BigP1Bufs pb1 = {};
-            if (p.b1G) {
-                const uint64_t P1 = (uint64_t)L * p.b1G;
-                pb1.log = (uint64_t*)(B + p.o_b1log);
-                pb1.index = (uint64_t*)(B + p.o_b1idx);
-                pb1.fill = (uint32_t*)(B + p.o_b1fill);
-                pb1.bref = (uint32_t*)(B + p.o_b1bref);
-                pb1.cap = p.b1cap;
-                pb1.pool = (uint64_t*)(B + p.o_b1pool);
-                pb1.pool_cap = p.b1pool;
-                pb1.used = (unsigned long long*)(B + p.o_p1used);  // zeroed per call (memset region)
-                pb1.piv = (uint64_t*)(B + p.o_b1piv);
-                pb1.info = (uint32_t*)(B + p.o_b1info);
-                pb1.off = (uint64_t*)(B + p.o_b1off);
-                pb1.len = (uint32_t*)(B + p.o_b1len);
-                pb1.G = p.b1G;
-                pb1.step_limit = step_limit();
-                HIPC(hipMemsetAsync(pb1.index, 0, P1 * p.b1cap * 2 * 8, s));
-                HIPC(hipMemsetAsync(pb1.fill, 0, P1 * (p.b1cap * 2 / 8) * 4, s));
-                hipLaunchKernelGGL(k_big_phase1, dim3(p.b1G, L), dim3(kBigT), 0, s, dist, n, stats, db[1], rb, pb1);
+            int start_dim = 1;
+            if (p.par) {
+                ParBufs pb;
+                pb.ctl = (ParCtl*)(B + p.o_pctl);
+                pb.item_base = (uint64_t*)(B + p.o_pitem);
+                pb.okey = (uint64_t*)(B + p.o_pokey);
+                pb.oval = (uint64_t*)(B + p.o_poval);
+                pb.ostride = p.ostride;
+                pb.colpiv = (uint64_t*)(B + p.o_colpiv);
+                pb.rec = (uint64_t*)(B + p.o_prec);
+                pb.rec_cap = p.rec_cap;
+                pb.rpool = (uint64_t*)(B + p.o_prpool);
+                pb.rpool_cap = p.rpool_cap;
+                pb.bpool = (uint64_t*)(B + p.o_pbpool);
+                pb.bpool_cap = p.bpool_cap;
+                pb.rq = (uint64_t*)(B + p.o_prq);
+                pb.rq_cap = p.rq_cap;
+                pb.step_limit = step_limit();
+                HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
+                hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb);
                 HIPC(hipGetLastError());
-                MARK("k_big_phase1");
+                MARK("k_par_init");
+                // persistent workers: two 71-KB-LDS workgroups per CU; the surplus exits at once
+                static const unsigned par_grid = getenv("TDA_PAR_GRID") ? (unsigned)atoi(getenv("TDA_PAR_GRID")) : 512u;
+                if (p.packed)
+                    hipLaunchKernelGGL(k_reduce_par<true>, dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], rb, pb);
+                else
+                    hipLaunchKernelGGL(k_reduce_par<false>, dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], rb, pb);
+                HIPC(hipGetLastError());
+                MARK("k_reduce_par");
+                hipLaunchKernelGGL(k_par_emit, dim3(L), dim3(1024), 0, s, stats, db[1], rb, pb, pairs1, p.pcap[1], p.maxdim >= 2 ? 1 : 0);
+                HIPC(hipGetLastError());
+                MARK("k_par_emit");
+                start_dim = 2;
             }
-            hipLaunchKernelGGL(k_reduce_big, dim3(L), dim3(kBigT), 0, s, dist, n, p.maxdim, stats, db[1], db[2], rb, gb, pairs1,
-                               pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0, pb1,
-                               (p.b1G && !getenv_is("TDA_BIG_P1", "2")) ? 1 : 0);  // 2: run phase 1, ignore it (debug)
+            if (start_dim <= p.maxdim)
+                hipLaunchKernelGGL(k_reduce_big, dim3(L), dim3(kBigT), 0, s, dist, n, p.maxdim, stats, db[1], db[2], rb, gb, pairs1,
+                                   pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0, start_dim);
         } else if (p.lds_mode) {
             if (p2) TDA_LAUNCH_RED(true, true, true); else if (p1) TDA_LAUNCH_RED(true, true, false); else TDA_LAUNCH_RED(true, false, false);
         } else {
@@ -973,7 +1000,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         }
 #undef TDA_LAUNCH_RED
         HIPC(hipGetLastError());
-        if (!p.dense) MARK(p.big ? "k_reduce_big" : "k_reduce_all");
+        if (!p.dense && !(p.par && p.maxdim < 2)) MARK(p.big ? "k_reduce_big" : "k_reduce_all");
     } else {
         HIPC(hipStreamWaitEvent(s, w.evh, 0));
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
@@ -1035,21 +1062,40 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     if (errs && getenv("TDA_DEBUG"))
         fprintf(stderr, "[tda] N=%d L=%d errs=%s force_global=%d scale=%d\n", n, L, err_flags(errs).c_str(), (int)force_global, scale);
+    if (errs & ERR_PAR) {
+        // k_reduce_par gave up (a capacity or spin limit): reduce H1 on the serial radix-heap kernel
+        ParCtl c;
+        HIPC(hipMemcpy(&c, B + p.o_pctl, sizeof(c), hipMemcpyDeviceToHost));
+        if (getenv("TDA_DEBUG"))
+            fprintf(stderr, "[tda] k_reduce_par aborted: code %llu, evictions %llu, records %llu, pools %llu / %llu keys\n", c.err,
+                    c.evictions, c.rec_used, c.rpool_used, c.bpool_used);
+        const unsigned code = (unsigned)(c.err & 0xFFFF);
+        const bool capacity = code == 21 || code == 22 || code == 41 || code == 53;  // pools / requeue slots
+        if (capacity && scale < 2) {  // the same parallel reduction with larger pools
+            guard.unlock();
+            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, false);
+        }
+        if (getenv_is("TDA_PAR_STRICT", "1"))  // tests: the parallel path itself must succeed
+            return fail(TDA_E_CAPACITY, "k_reduce_par aborted: item " + std::to_string(c.err >> 16) + " code " +
+                                            std::to_string(code));
+        guard.unlock();
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, true);
+    }
     if ((errs & ERR_LDS_SPILL) && !force_global) {
         // a working column outgrew LDS: redo the batch with global-memory tables
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, scale);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par);
     }
     if ((errs & ERR_WORK_CAP) && !p.big && !getenv_is("TDA_REDUCE", "wave")) {
         // a working column outgrew the one-wave HBM tables: full scans of a
         // large column are the slow case, so switch to the radix-heap kernel
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true, no_par);
     }
     if ((errs & ~(ERR_LDS_SPILL)) == (errs & (ERR_WORK_CAP | ERR_VPOOL_CAP)) && errs && scale < 2) {
         // working column / reduced-column pool too small: retry with larger buffers
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par);
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
 #ifdef TDA_PROFILE
@@ -1086,7 +1132,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)tt, (unsigned long long)sc, (unsigned long long)cb, (unsigned long long)ad, (unsigned long long)mx,
                 (unsigned long long)mxa);
     }
-    if (p.big)
+    if (p.par) {
+        const uint64_t* q = w.hstats[0].prof[2];
+        fprintf(stderr, "[tda-prof] k_reduce_par longest column: %llu steps, %llu cycles: front_min %llu, pivot+rows %llu, apparent adds %llu, refills %llu (%llu), owner path %llu; avg front log %llu, compactions %llu, spills %llu\n",
+                (unsigned long long)q[6], (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[2], (unsigned long long)q[3],
+                (unsigned long long)q[4], (unsigned long long)((q[7] >> 16) & 0xFFFF), (unsigned long long)q[5], (unsigned long long)(q[7] & 0xFFFF),
+                (unsigned long long)((q[7] >> 32) & 0xFFFF), (unsigned long long)(q[7] >> 48));
+    }
+    if (p.big && !p.par)
         for (int d = 1; d <= p.maxdim; ++d) {
             const uint64_t* q = w.hstats[0].prof[d];
             fprintf(stderr, "[tda-prof] big dim %d layer 0: cob0 %llu pop %llu owner_add %llu app_add %llu store %llu reset %llu total %llu cycles; owner adds %llu entries %llu, all adds %lld\n",

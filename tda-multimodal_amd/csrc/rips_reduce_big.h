@@ -1,5 +1,7 @@
 // rips_reduce_big.h -- serial reduction for large N (one 1024-thread workgroup
-// per layer, working tables in HBM).
+// per layer, working tables in HBM).  H1 normally runs on k_reduce_par
+// (rips_reduce_par.h, many columns in flight); this kernel reduces H2 above
+// N = 256 and is the fallback when k_reduce_par aborts on a capacity limit.
 //
 // Same algorithm as rips_reduce.h (Ripser's compute_pairs over Z/2 with stored
 // reduced columns and implicit apparent columns), but the working coboundary
@@ -311,34 +313,6 @@ struct BigHeap {
     }
 };
 
-// Phase 1 of the large-N H1 reduction (k_big_phase1): every residual column
-// is reduced IN PARALLEL by its own workgroup with the apparent columns only
-// (their coboundaries are implicit and do not depend on any other residual
-// column), up to its first pivot that is not an apparent pivot.  Which
-// residual column owns that pivot is only known in column order, so the
-// serial kernel then walks the columns: a column whose phase-1 pivot is free
-// becomes a pair at once (its saved working column is R_j); only a column
-// whose pivot an earlier column owns is rebuilt from its saved entries and
-// continued serially.  On torus N=1024 that moves 16.7K of 16.8K column
-// additions out of the serial walk.
-constexpr uint32_t kB1Defer = 1u << 31;  // phase 1 gave up (capacity / step limit): serial from scratch
-struct BigP1Bufs {
-    uint64_t* log;        // [L * G] workspaces, as BigBufs (cap each)
-    uint64_t* index;
-    uint32_t* fill;
-    uint32_t* bref;
-    uint64_t cap;
-    uint64_t* pool;       // [L][pool_cap] saved working columns (live keys)
-    uint64_t pool_cap;
-    unsigned long long* used;  // [L] pool bump counters (zeroed per call)
-    uint64_t* piv;        // [L][rcap] pivot key after phase 1 (kEmpty64: zero column)
-    uint32_t* info;       // [L][rcap] additions | kB1Defer
-    uint64_t* off;        // [L][rcap] saved column offset in pool
-    uint32_t* len;        // [L][rcap] saved column length
-    int G;                // workgroups (workspaces) per layer
-    uint64_t step_limit;
-};
-
 // the oldest facet of the apparent cofacet pidx (its apparent column), with diameter
 template <int DIM>
 __device__ __forceinline__ float apparent_facet(const float* __restrict__ D, int n, uint64_t pidx, int (&fv)[DIM + 1]) {
@@ -390,107 +364,10 @@ __device__ __forceinline__ void big_cob(BigHeap& H, const float* __restrict__ D,
     }
 }
 
-__global__ __launch_bounds__(kBigT) void k_big_phase1(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
-                                                      DimBufs b, Reduce2Bufs rb, BigP1Bufs pb) {
-    __shared__ BigShared S;
-    const int l = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
-    LayerStats* st = stats + l;
-    const float r = st->thresh;
-    const float* D = dist + (size_t)l * n * n;
-    uint64_t nres = (uint64_t)st->n_residual[1];
-    if (nres > b.rcap) nres = b.rcap;
-    const uint64_t* resid = b.resid + (size_t)l * b.rcap;
-    const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
-    const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
-    const size_t wsi = (size_t)l * pb.G + g;
-    BigHeap H;
-    H.log = pb.log + wsi * pb.cap;
-    H.index = pb.index + wsi * 2 * pb.cap;
-    H.fill = pb.fill + wsi * (2 * pb.cap / 8);
-    H.bref = pb.bref + wsi * kNB * pb.cap;
-    H.cap = pb.cap;
-    H.bcap = pb.cap;
-    H.imask = (uint32_t)(2 * pb.cap - 1);
-    H.S = &S;
-    uint64_t* pool = pb.pool + (size_t)l * pb.pool_cap;
-    if (tid == 0) {
-        S.cnt = 0;
-        for (int q = 0; q < kNB; ++q) S.nb[q] = 0;
-    }
-    for (uint64_t j = g; j < nres; j += pb.G) {
-        __syncthreads();
-        const uint64_t key = ld_glb(resid, j);
-        const uint64_t sidx = key_idx(key);
-        const float sdm = key_diam(key);
-        if ((ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u) continue;  // cleared (H0 forest edge): serial skips it
-        int vs[2];
-        decode<1>(sidx, n, vs);
-        if (tid == 0) {
-            S.err = 0;
-            S.last = __float_as_uint(sdm + 0.0f);
-        }
-        __syncthreads();
-        big_cob<1>(H, D, n, r, vs, sdm);
-        uint32_t adds = 0;
-        bool defer = false;
-        uint64_t pk = kEmpty64, off = 0;
-        uint32_t len = 0;
-        for (uint64_t step = 0;; ++step) {
-            pk = H.pop_min();
-            if (S.err || step >= pb.step_limit) {
-                defer = true;
-                break;
-            }
-            if (pk == kEmpty64) break;  // zero column: an essential class
-            const uint64_t pidx = 0xFFFFFFFFull - (pk & 0xFFFFFFFFull);
-            if ((ld_glb(pivg, pidx >> 5) >> (pidx & 31)) & 1u) {  // apparent pivot: add its implicit column
-                int fv[2];
-                const float fd = apparent_facet<1>(D, n, pidx, fv);
-                big_cob<1>(H, D, n, r, fv, fd);
-                ++adds;
-                continue;
-            }
-            // first non-apparent pivot: save the live entries (the serial walk decides ownership)
-            const uint32_t c = S.cnt;
-            uint64_t live = 0;
-            for (uint32_t e = tid; e < c; e += kBigT) live += H.log[e] < kDead ? 1 : 0;
-            live = block_sum_u64(live, S);
-            if (tid == 0) S.bc[0] = atomicAdd(pb.used + l, (unsigned long long)live);
-            __syncthreads();
-            off = S.bc[0];
-            if (off + live > pb.pool_cap) {
-                defer = true;
-                break;
-            }
-            uint64_t wr = 0;
-            for (uint32_t e0 = 0; e0 < c; e0 += kBigT) {
-                const uint32_t e = e0 + tid;
-                const uint64_t k = e < c ? H.log[e] : kEmpty64;
-                const bool lv = k < kDead;
-                uint32_t tot;
-                const uint32_t o = block_prefix(lv, S, &tot);
-                if (lv) pool[off + wr + o] = k;
-                wr += tot;
-            }
-            len = (uint32_t)live;
-            break;
-        }
-        if (tid == 0) {
-            const size_t q = (size_t)l * b.rcap + j;
-            pb.piv[q] = pk;
-            pb.info[q] = adds | (defer ? kB1Defer : 0u);
-            pb.off[q] = off;
-            pb.len[q] = len;
-        }
-        __syncthreads();
-        H.reset();
-    }
-}
-
 template <int DIM>
 __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, LayerStats* st, int l, const DimBufs& b,
                                const Reduce2Bufs& rb, const BigBufs& gb, BigShared& S, PivMap& map, const PivMap* prev,
-                               Pair* __restrict__ pairs, uint64_t pcap, const BigP1Bufs* p1 = nullptr) {
+                               Pair* __restrict__ pairs, uint64_t pcap) {
     constexpr int NV = DIM + 2;
     const int tid = threadIdx.x, ln = tid & 63;
     uint64_t nres = (uint64_t)st->n_residual[DIM];
@@ -572,80 +449,10 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             if (tid == 0) rlen[j] = 0;
             continue;
         }
-        bool resume = false;
-        if (p1) {
-            const size_t q = (size_t)l * b.rcap + j;
-            const uint32_t inf = ld_glb((const uint32_t*)p1->info, q);
-            if (!(inf & kB1Defer)) {
-                const uint64_t pk = ld_glb((const uint64_t*)p1->piv, q);
-                if (pk == kEmpty64) {  // zero after apparent additions: essential
-                    nadds += inf;
-                    if (tid == 0) {
-                        uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-                        if (pos < pcap)
-                            P[pos] = Pair{sdm, INFINITY, (int64_t)sidx, -1};
-                        else
-                            atomicOr(&st->err, ERR_PAIR_CAP);
-                        rlen[j] = 0;
-                    }
-                    continue;
-                }
-                const uint64_t pidx = 0xFFFFFFFFull - (pk & 0xFFFFFFFFull);
-                const float pd = __uint_as_float((uint32_t)(pk >> 32));
-                // the bit was clear in phase 1, so it is set now only by an earlier residual column
-                const bool app = (ld_glb((const uint32_t*)pivg, pidx >> 5) >> (pidx & 31)) & 1u;
-                const int64_t owner = app ? map.find((uint32_t)pidx, ln) : -1;
-                const uint64_t so = ld_glb((const uint64_t*)p1->off, q);
-                const uint32_t sl = ld_glb((const uint32_t*)p1->len, q);
-                const uint64_t* sp = p1->pool + (size_t)l * p1->pool_cap + so;
-                if (owner < 0) {  // free pivot: pair now; the saved column is R_j
-                    nadds += inf;
-                    // every wave has read pivg / the map for this pivot before tid 0 publishes it
-                    // (a lagging wave would otherwise see its own column as the owner)
-                    __syncthreads();
-                    if (tid == 0) {
-                        if (pd > sdm) {
-                            uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
-                            if (pos < pcap)
-                                P[pos] = Pair{sdm, pd, (int64_t)sidx, (int64_t)pidx};
-                            else
-                                atomicOr(&st->err, ERR_PAIR_CAP);
-                        }
-                        map.insert((uint32_t)pidx, (uint32_t)j);
-                        atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
-                    }
-                    cs += pair_hash(sidx, pidx);
-                    npairs += 1;
-                    uint64_t wr = sl;
-                    if (rused + wr > rb.rpool_cap) {
-                        if (tid == 0) S.err = 2;
-                        wr = 0;
-                    }
-                    for (uint32_t e = tid; e < wr; e += kBigT) rpool[rused + e] = ld_glb(sp, e);
-                    if (tid == 0) {
-                        roff[j] = rused;
-                        rlen[j] = (uint32_t)wr;
-                    }
-                    rused += wr;
-                    continue;
-                }
-                // owned pivot: rebuild the phase-1 working column and continue serially
-                nadds += inf;
-                if (tid == 0) S.last = (uint32_t)(pk >> 32);
-                __syncthreads();
-                for (uint32_t e0 = 0; e0 < sl; e0 += kBigT) {
-                    const uint32_t e = e0 + tid;
-                    H.toggle_pass(e < sl ? ld_glb(sp, e) : 0, e < sl);
-                }
-                resume = true;
-            }
-        }
-        if (!resume) {
-            if (tid == 0) S.last = __float_as_uint(sdm + 0.0f);
-            __syncthreads();
-        }
+        if (tid == 0) S.last = __float_as_uint(sdm + 0.0f);
+        __syncthreads();
         TDA_STAMP(t_c0);
-        if (!resume) cob(vs, sdm);
+        cob(vs, sdm);
         TDA_ACC(0, t_c0);
         for (uint64_t step = 0;; ++step) {
             TDA_STAMP(t_p0);
@@ -653,8 +460,8 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             TDA_ACC(1, t_p0);
             if (step >= gb.step_limit) {
                 if (tid == 0) {
-                    printf("k_reduce_big: layer %d dim %d column %llu (idx %llu) step limit: pivot %016llx cnt %u last %08x resume %d\n", l,
-                           DIM, (unsigned long long)j, (unsigned long long)sidx, (unsigned long long)pk, S.cnt, S.last, (int)resume);
+                    printf("k_reduce_big: layer %d dim %d column %llu (idx %llu) step limit: pivot %016llx cnt %u last %08x\n", l,
+                           DIM, (unsigned long long)j, (unsigned long long)sidx, (unsigned long long)pk, S.cnt, S.last);
                     S.err = 3;
                 }
                 __syncthreads();
@@ -695,7 +502,7 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                 ++nadds;
                 TDA_ACC(3, t_a0);
             } else {
-                __syncthreads();  // all waves decided before tid 0 publishes the pivot (see the phase-1 path)
+                __syncthreads();  // all waves decided before tid 0 publishes the pivot (a lagging wave would see its own column as the owner)
                 if (tid == 0) {
                     if (pd > sdm) {
                         uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
@@ -758,17 +565,31 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
 }
 
 // Large-N serial reductions: one 1024-thread workgroup per layer, H1 then H2.
+// start_dim 2: H1 was reduced by k_reduce_par (rips_reduce_par.h), whose
+// k_par_emit left the H1 residual pivots in the dim-1 map that H2 clears with.
 __global__ __launch_bounds__(kBigT) void k_reduce_big(const float* __restrict__ dist, int n, int maxdim,
                                                        LayerStats* __restrict__ stats, DimBufs b1, DimBufs b2, Reduce2Bufs rb,
                                                        BigBufs gb, Pair* __restrict__ pairs1, Pair* __restrict__ pairs2,
-                                                       uint64_t pcap1, uint64_t pcap2, BigP1Bufs p1, int use_p1) {
+                                                       uint64_t pcap1, uint64_t pcap2, int start_dim) {
     __shared__ BigShared S;
     const int l = blockIdx.x;
     LayerStats* st = stats + l;
     const float r = st->thresh;
     const float* D = dist + (size_t)l * n * n;
     PivMap m1, m2;
-    big_reduce_dim<1>(D, n, r, st, l, b1, rb, gb, S, m1, nullptr, pairs1, pcap1, use_p1 ? &p1 : nullptr);
+    if (start_dim <= 1) {
+        big_reduce_dim<1>(D, n, r, st, l, b1, rb, gb, S, m1, nullptr, pairs1, pcap1);
+    } else {  // the map k_par_emit filled (same region and mask rule as big_reduce_dim<1>)
+        uint64_t nres = (uint64_t)st->n_residual[1];
+        if (nres > b1.rcap) nres = b1.rcap;
+        uint64_t rc2 = 16;
+        while (rc2 < 2 * nres + 16) rc2 <<= 1;
+        if (rc2 > rb.rmap_stride) rc2 = rb.rmap_stride;
+        m1.k = rb.rmap_keys + ((size_t)l * 2 + 0) * rb.rmap_stride;
+        m1.v = rb.rmap_vals + ((size_t)l * 2 + 0) * rb.rmap_stride;
+        m1.mask = rc2 - 1;
+        m1.lds = false;
+    }
     if (maxdim >= 2) big_reduce_dim<2>(D, n, r, st, l, b2, rb, gb, S, m2, &m1, pairs2, pcap2);
 }
 

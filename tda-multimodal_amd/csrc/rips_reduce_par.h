@@ -1,0 +1,1105 @@
+// rips_reduce_par.h -- large-N H1 reduction with many residual columns in
+// flight at once (k_reduce_par), one 256-thread workgroup per column.
+//
+// [upstream ripser.cpp compute_pairs] reduces the residual columns one after
+// the other.  The persistence PAIRING does not depend on that order: any
+// reduction R = D V with V upper triangular and pairwise distinct pivots gives
+// the same pairs.  So every residual column is reduced concurrently, lock-free
+// (the scheme of Morozov & Nigmetov, "Towards lockfree persistent homology",
+// SPAA 2020), with a per-layer pivot -> owner map in HBM:
+//   * pivot p apparent (k_apparent's bitmap): add the implicit apparent column;
+//   * p free: publish R_j as an immutable record, then claim p (CAS);
+//   * p owned by i < j: add R_i (its record) and go on;
+//   * p owned by i > j: publish R_j, CAS the owner from i to j and requeue i,
+//     which resumes from its own record and adds R_j.
+// Every addition is of an EARLIER column, so V stays upper triangular; the
+// owner of every pivot only ever moves to a smaller column, so the process
+// terminates.  Pairs are read from the final owners by k_par_emit.
+//
+// One column's working coboundary (torus N=1024: two columns need 8,632 and
+// 6,644 additions and grow to millions of raw entries) is a RADIX HEAP over
+// the f32 diameter bits whose low levels live in LDS:
+//   * the FRONT (levels 0..kf relative to `last`) is an LDS Z/2 toggle set:
+//     key log (parity = bit 63) + 8-slot hashed index; the pivot is a min scan
+//     of the log;
+//   * levels kf+1..32 are append-only HBM buckets (chunks of 256 << k keys,
+//     addressed from LDS, reused across the columns of one workgroup);
+//     duplicates cancel when a bucket is pulled into the front;
+//   * when the front empties, the lowest non-empty bucket is redistributed
+//     relative to its minimum: the part that fits goes to the front, the rest
+//     one level down.
+// An apparent addition is then one dependent global round trip: the pivot's
+// bitmap word and the two distance rows of its apparent facet are loaded
+// together (for N <= 1024 the facet is encoded in the key's low bits, next to
+// the packed vertex triple), everything else is LDS work.
+//
+// Cross-workgroup hand-offs follow MI355X_MICROARCH.md "inter-workgroup
+// visibility": record payloads are written with sc1 (agent-scope relaxed)
+// stores, every storing wave drains with s_waitcnt vmcnt(0) before the
+// workgroup barrier that precedes the publishing CAS, and every load of a
+// record is an sc1 load; map words and queue words are agent-scope atomics.
+// Any capacity overflow, step limit or spin limit aborts the launch and the
+// host re-runs the layer batch on k_reduce_big (the serial radix-heap kernel).
+#pragma once
+#include "rips_reduce_big.h"
+
+namespace tda {
+
+constexpr int kParT = 256;
+constexpr int kParW = kParT / 64;
+constexpr uint32_t kFrontLog = 4096;   // front log entries (live + cancelled)
+constexpr uint32_t kFrontIdx = 4096;   // front index slots (512 buckets x 8)
+constexpr uint32_t kFrontLive = 1792;  // live front keys that trigger a spill
+constexpr uint32_t kFrontFill = 768;   // refill / spill target
+constexpr int kParChunks = 22;         // chunk k of an HBM bucket holds 256 << k keys
+constexpr int kParRegs = 8;            // bucket keys per thread held in registers by a refill
+constexpr int kParRV = 4;              // coboundary vertices per thread per round (kParT * 4 = 1024)
+constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
+constexpr uint64_t kParEss = kEmpty64;        // colpiv: essential (zero column)
+constexpr uint64_t kParSkip = kEmpty64 - 1;   // colpiv: cleared column (H0 death)
+constexpr uint32_t kParSpin = 1u << 22;       // polls before a wait on another workgroup is declared hung
+
+enum : int32_t { ERR_PAR = 128 };  // k_reduce_par aborted: the host falls back to k_reduce_big
+
+struct ParCtl {  // zeroed by k_par_init
+    unsigned long long next;     // next fresh item
+    unsigned long long rq_head, rq_tail;
+    unsigned long long bpool_used, rpool_used, rec_used;
+    unsigned long long abort;
+    unsigned long long err;      // first error code (diagnostics)
+    unsigned long long total;    // items over all layers
+    unsigned long long evictions;
+    unsigned long long pad[6];
+};
+
+struct ParBufs {
+    ParCtl* ctl;
+    uint64_t* item_base;  // [L + 1] prefix of per-layer residual counts
+    uint64_t* okey;       // [L][ostride] owner map keys: pivot index + 1 (0 = empty)
+    uint64_t* oval;       // [L][ostride] owner map values: column << 32 | record + 1
+    uint64_t ostride;
+    uint64_t* colpiv;     // [L][rcap] final pivot (filt_key form) | kParEss | kParSkip
+    uint64_t* rec;        // [rec_cap][4]: offset, length, pivot key, column
+    uint64_t rec_cap;
+    uint64_t* rpool;      // record payloads
+    uint64_t rpool_cap;
+    uint64_t* bpool;      // bucket chunks (per-workgroup, reused)
+    uint64_t bpool_cap;   // in keys, multiple of 256
+    uint64_t* rq;         // requeue slots (used once per launch, zero = not yet written): item << 32 | record + 1
+    uint64_t rq_cap;
+    uint64_t step_limit;
+};
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint64_t ald(const uint64_t* p) {  // sc1 load (agent scope)
+    return __hip_atomic_load((uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ald(const unsigned long long* p) {
+    return __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ast(uint64_t* p, uint64_t v) {  // sc1 store (write-through)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t acas(uint64_t* p, uint64_t cmp, uint64_t v) {  // returns old
+    __hip_atomic_compare_exchange_strong(p, &cmp, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return cmp;
+}
+__device__ __forceinline__ uint64_t aadd(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t par_bucket(uint32_t dbits, uint32_t last) {
+    const uint32_t x = dbits ^ last;
+    return x ? 32u - (uint32_t)__builtin_clz(x) : 0u;
+}
+__device__ __forceinline__ uint32_t chunk_of(uint32_t s) { return 31u - (uint32_t)__builtin_clz((s >> 8) + 1u); }
+__device__ __forceinline__ uint32_t chunk_start(uint32_t k) { return ((1u << k) - 1u) << 8; }
+
+// triangle keys.  PACKED (N <= 1024): lo32 = ~(x << 22 | y << 12 | z << 2 | f)
+// with x > y > z the vertices and f the apparent facet (the vertex t[f] it
+// omits: the longest edge, first in (x, y, z) order on ties -- the facet
+// apparent_facet<1> picks).  Colex order == order of the descending triples,
+// so the key order is Ripser's (diam asc, index desc).  Otherwise lo32 = ~index.
+template <bool PACKED>
+__device__ __forceinline__ uint32_t tri_lo(int x, int y, int z, int f) {
+    if (PACKED) return 0xFFFFFFFFu - (((uint32_t)x << 22) | ((uint32_t)y << 12) | ((uint32_t)z << 2) | (uint32_t)f);
+    const int vs[3] = {x, y, z};
+    return 0xFFFFFFFFu - (uint32_t)encode<2>(vs);
+}
+
+// ------------------------------------------------------------------ LDS
+struct ParLds {
+    uint64_t log[kFrontLog];
+    uint64_t idx[kFrontIdx];
+    uint32_t bcnt[33];
+    uint32_t cptr[33][kParChunks];
+    uint32_t hist[33];
+    uint64_t red[2][kParW];
+    uint32_t wsum[2][kParW];
+    uint64_t bc[8];
+    uint32_t fcnt;  // front log length
+    uint32_t last;  // radix reference (diameter bits)
+    uint32_t kf;    // front holds levels 0..kf
+    int32_t err;
+};
+extern __shared__ ParLds par_smem[];
+#define PS (par_smem[0])
+
+struct ParRed {  // double-buffered block reductions: one barrier each
+    uint32_t par = 0;
+    __device__ __forceinline__ uint64_t min(uint64_t v) {
+        v = wave_min_u64(v);
+        const uint32_t b = par++ & 1;
+        if ((threadIdx.x & 63) == 0) PS.red[b][threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint64_t m = PS.red[b][0];
+#pragma unroll
+        for (int w = 1; w < kParW; ++w) m = PS.red[b][w] < m ? PS.red[b][w] : m;
+        return m;
+    }
+    __device__ __forceinline__ uint64_t sum(uint64_t v) {
+        v = wave_sum_u64(v);
+        const uint32_t b = par++ & 1;
+        if ((threadIdx.x & 63) == 0) PS.red[b][threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint64_t m = 0;
+#pragma unroll
+        for (int w = 0; w < kParW; ++w) m += PS.red[b][w];
+        return m;
+    }
+    // exclusive block prefix of per-thread counts c; *tot = block total
+    __device__ __forceinline__ uint32_t prefix(uint32_t c, uint32_t* tot) {
+        // wave-inclusive scan with shuffles (c small)
+        const int ln = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (ln >= o) x += y;
+        }
+        const uint32_t b = par++ & 1;
+        if (ln == 63) PS.wsum[b][w] = x;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int q = 0; q < kParW; ++q) {
+            const uint32_t s = PS.wsum[b][q];
+            before += q < w ? s : 0;
+            all += s;
+        }
+        *tot = all;
+        return before + x - c;
+    }
+};
+
+// ------------------------------------------------------------------ front
+// Index: 8-slot buckets of u64 entries fp << 32 | (log pos + 1), claimed by
+// CAS on the first empty slot (slots of a bucket fill in order and are only
+// cleared by a full reset), so a probe stops at the first empty slot.
+constexpr uint32_t kFrontBkts = kFrontIdx / 8;
+constexpr uint32_t kReserved = 0xFFFFFFFFu;  // slot claimed, log position not written yet
+
+__device__ __forceinline__ void front_reset() {
+    for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
+    if (threadIdx.x == 0) PS.fcnt = 0;
+    __syncthreads();
+}
+
+// Toggle up to R keys per thread (bit r of vmask) into the front.  Keys may
+// repeat within the pass (bucket refills and records are raw multisets): the
+// first claimant of a key inserts it live, every other copy flips its parity.
+// Precondition: fcnt + R * kParT <= kFrontLog.
+template <int R>
+__device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vmask) {
+    constexpr uint32_t bmask = kFrontBkts - 1;
+    uint32_t bk[R], slot[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        bk[r] = mix32((uint32_t)k[r]) & bmask;
+        slot[r] = 0;
+    }
+    uint32_t pend = vmask, ins = 0, fol = 0;
+    const int ln = threadIdx.x & 63;
+    // phase A: find the key (flip it), or claim a slot (inserter), or find a claim of the same key (follower)
+    for (int it = 0; __syncthreads_or(pend != 0); ++it) {
+        if (it > 8 * (int)kFrontBkts) {  // cannot happen while the log precondition holds
+            if (threadIdx.x == 0) PS.err = 11;
+            break;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!((pend >> r) & 1u)) continue;
+            const uint32_t fp = (uint32_t)k[r];
+            const uint32_t bo = bk[r] * 8;
+            int found = -1, empty = -1;
+            uint64_t fe = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint64_t e = PS.idx[bo + u];
+                if (found < 0 && empty < 0) {
+                    if (e == 0) empty = u;
+                    else if ((uint32_t)(e >> 32) == fp) found = u, fe = e;
+                }
+            }
+            if (found >= 0) {
+                if ((uint32_t)fe == kReserved) {
+                    fol |= 1u << r;
+                    slot[r] = bo + found;
+                } else {
+                    __hip_atomic_fetch_xor(&PS.log[(uint32_t)fe - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                pend &= ~(1u << r);
+            } else if (empty >= 0) {
+                const uint64_t mine = ((uint64_t)fp << 32) | kReserved;
+                const uint64_t old = atomicCAS((unsigned long long*)&PS.idx[bo + empty], 0ull, (unsigned long long)mine);
+                if (old == 0) {
+                    ins |= 1u << r;
+                    slot[r] = bo + empty;
+                    pend &= ~(1u << r);
+                } else if ((uint32_t)(old >> 32) == fp) {
+                    fol |= 1u << r;
+                    slot[r] = bo + empty;
+                    pend &= ~(1u << r);
+                }  // else: another key took the slot; probe this bucket again
+            } else {
+                bk[r] = (bk[r] + 1) & bmask;  // bucket full: next one
+            }
+        }
+    }
+    // phase B: inserters take log positions (one LDS atomic per wave) and publish them
+    uint32_t off = 0, wtot = 0;
+    uint64_t m[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        m[r] = __ballot((ins >> r) & 1u);
+        wtot += (uint32_t)__popcll(m[r]);
+    }
+    uint32_t base = 0;
+    if (ln == 0 && wtot) base = atomicAdd(&PS.fcnt, wtot);
+    base = __shfl(base, 0, 64);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if ((ins >> r) & 1u) {
+            const uint32_t pos = base + off + lanes_below(m[r]);
+            if (pos < kFrontLog) {
+                PS.log[pos] = k[r];
+                PS.idx[slot[r]] = ((uint64_t)(uint32_t)k[r] << 32) | (pos + 1);
+            } else {
+                PS.err = 12;
+            }
+        }
+        off += (uint32_t)__popcll(m[r]);
+    }
+    // phase C: followers flip the inserted entry
+    if (__syncthreads_or(fol != 0)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!((fol >> r) & 1u)) continue;
+            const uint32_t pv = (uint32_t)PS.idx[slot[r]];
+            if (pv != kReserved && pv - 1 < kFrontLog)
+                __hip_atomic_fetch_xor(&PS.log[pv - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __syncthreads();
+    }
+}
+
+// min live front key (block-uniform; kEmpty64 if none)
+__device__ __forceinline__ uint64_t front_min(ParRed& rd) {
+    const uint32_t c = PS.fcnt;
+    uint64_t b = kEmpty64;
+    for (uint32_t e = threadIdx.x; e < c; e += kParT) {
+        const uint64_t x = PS.log[e];
+        b = x < b ? x : b;
+    }
+    b = b < kDead ? b : kEmpty64;
+    return rd.min(b);
+}
+
+// Keep the live front keys of level <= keep (relative to PS.last), in log
+// order; rebuild the index.  Returns the new length (block-uniform).
+__device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
+    __syncthreads();
+    const uint32_t c = PS.fcnt, last = PS.last;
+    uint32_t w = 0;
+    for (uint32_t e0 = 0; e0 < c; e0 += kParT) {
+        const uint32_t e = e0 + threadIdx.x;
+        const uint64_t x = e < c ? PS.log[e] : kEmpty64;
+        const bool lv = x < kDead && par_bucket((uint32_t)(x >> 32), last) <= keep;
+        uint32_t tot;
+        const uint32_t o = rd.prefix(lv ? 1u : 0u, &tot);  // barrier: the chunk has been read
+        if (lv) PS.log[w + o] = x;                        // w + o <= e
+        w += tot;
+    }
+    for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
+    __syncthreads();
+    constexpr uint32_t bmask = kFrontBkts - 1;
+    for (uint32_t e = threadIdx.x; e < w; e += kParT) {  // distinct keys: claim the first free slot
+        const uint32_t fp = (uint32_t)PS.log[e];
+        const uint64_t v = ((uint64_t)fp << 32) | (e + 1);
+        uint32_t h = (mix32(fp) & bmask) * 8;
+        for (uint32_t it = 0; it < kFrontIdx; ++it, h = (h + 1) & (kFrontIdx - 1))
+            if (PS.idx[h] == 0 && atomicCAS((unsigned long long*)&PS.idx[h], 0ull, (unsigned long long)v) == 0) break;
+    }
+    if (threadIdx.x == 0) PS.fcnt = w;
+    __syncthreads();
+    return w;
+}
+
+// ------------------------------------------------------------------ HBM buckets
+// Append key k[r] to bucket bb[r] (bit r of vmask); chunks that start in this
+// pass and were never allocated by this workgroup are taken from the pool.
+template <int R>
+__device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint32_t (&bb)[R], uint32_t vmask, const ParBufs& P) {
+    // slots: one LDS atomic per key, all R issued back to back (conflicting lanes serialise inside
+    // the LDS, which is far cheaper than a round trip per distinct level)
+    uint32_t slot[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) slot[r] = ((vmask >> r) & 1u) ? atomicAdd(&PS.bcnt[bb[r]], 1u) : 0u;
+    bool need = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!((vmask >> r) & 1u)) continue;
+        const uint32_t kc = chunk_of(slot[r]);
+        if (kc >= (uint32_t)kParChunks) {
+            PS.err = 21;
+            need = true;  // takes the barrier below, so every thread sees the error
+            vmask &= ~(1u << r);
+        } else if (slot[r] == chunk_start(kc) && PS.cptr[bb[r]][kc] == kNoChunk) {
+            need = true;
+        }
+    }
+    if (__syncthreads_or(need)) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!((vmask >> r) & 1u)) continue;
+            const uint32_t kc = chunk_of(slot[r]);
+            if (slot[r] == chunk_start(kc) && PS.cptr[bb[r]][kc] == kNoChunk) {
+                const uint64_t sz = 256ull << kc;
+                const uint64_t o = aadd(&P.ctl->bpool_used, sz);
+                if (o + sz <= P.bpool_cap)
+                    PS.cptr[bb[r]][kc] = (uint32_t)(o >> 8);
+                else
+                    PS.err = 22;
+            }
+        }
+        __syncthreads();
+        if (PS.err) return;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!((vmask >> r) & 1u)) continue;
+        const uint32_t kc = chunk_of(slot[r]);
+        const uint64_t at = (uint64_t)PS.cptr[bb[r]][kc] * 256 + (slot[r] - chunk_start(kc));
+        st_glb(P.bpool, at, k[r]);
+    }
+}
+
+__device__ __forceinline__ uint64_t bucket_at(const ParBufs& P, uint32_t b, uint32_t e) {
+    const uint32_t kc = chunk_of(e);
+    return ld_glb(P.bpool, (uint64_t)PS.cptr[b][kc] * 256 + (e - chunk_start(kc)));
+}
+
+// ------------------------------------------------------------------ column
+struct ParCol {
+    ParRed rd;
+    uint64_t steps = 0, adds = 0;
+#ifdef TDA_PROFILE
+    uint64_t ncompact = 0, nspill = 0;
+#endif
+};
+
+// Insert keys (bit r of vmask; all >= the current pivot) into the working
+// column: front levels toggle in LDS, the rest append to HBM buckets.
+template <int R>
+__device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
+    // room for R * T new log entries; compact, and spill front levels to HBM if too many keys are live
+    if (PS.fcnt + R * kParT > kFrontLog) {
+        uint32_t w = front_compact(C.rd, 33);
+#ifdef TDA_PROFILE
+        ++C.ncompact;
+#endif
+        if (w > kFrontLive || w + R * kParT > kFrontLog) {
+#ifdef TDA_PROFILE
+            ++C.nspill;
+#endif
+            // spill: histogram of the live front by level, keep the lowest levels up to kFrontFill
+            for (uint32_t q = threadIdx.x; q < 33; q += kParT) PS.hist[q] = 0;
+            __syncthreads();
+            const uint32_t last = PS.last;
+            for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket((uint32_t)(PS.log[e] >> 32), last)], 1u);
+            __syncthreads();
+            int keep = -1;
+            uint32_t cum = 0;
+            for (int q = 0; q <= (int)PS.kf; ++q) {
+                cum += PS.hist[q];
+                if (cum <= kFrontFill) keep = q;
+            }
+            if (keep < 0) {  // the exact-diameter level alone is too large for the front
+                if (PS.hist[0] + R * kParT <= kFrontLog) keep = 0;
+                else if (threadIdx.x == 0) PS.err = 31;
+            }
+            __syncthreads();
+            if (PS.err) return;
+            // move the levels above `keep` out to their HBM buckets, then drop them from the front
+            for (uint32_t e0 = 0; e0 < w; e0 += kParT) {
+                const uint32_t e = e0 + threadIdx.x;
+                uint64_t x[1] = {e < w ? PS.log[e] : 0};
+                uint32_t b[1] = {e < w ? par_bucket((uint32_t)(x[0] >> 32), last) : 0};
+                bucket_append<1>(x, b, (e < w && b[0] > (uint32_t)keep) ? 1u : 0u, P);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) PS.kf = (uint32_t)keep;
+            front_compact(C.rd, (uint32_t)keep);
+        }
+    }
+    const uint32_t last = PS.last, kf = PS.kf;
+    uint32_t fm = 0, bm = 0, bb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        bb[r] = par_bucket((uint32_t)(k[r] >> 32), last);
+        if ((vmask >> r) & 1u) {
+            if (bb[r] <= kf) fm |= 1u << r;
+            else bm |= 1u << r;
+        }
+    }
+    front_toggle<R>(k, fm);
+    bucket_append<R>(k, bb, bm, P);
+}
+
+// kParRegs keys per thread of bucket b at [e0, c), loads all in flight
+__device__ __forceinline__ uint32_t bucket_batch(const ParBufs& P, uint32_t b, uint32_t e0, uint32_t c, uint64_t (&x)[kParRegs]) {
+    uint32_t vm = 0;
+#pragma unroll
+    for (int r = 0; r < kParRegs; ++r) {
+        const uint32_t e = e0 + threadIdx.x + r * kParT;
+        x[r] = e < c ? bucket_at(P, b, e) : kEmpty64;
+        if (e < c) vm |= 1u << r;
+    }
+    return vm;
+}
+
+// Front empty: redistribute the lowest non-empty bucket relative to its
+// minimum.  Returns false when the working column is zero.  A bucket of up
+// to kParT * kParRegs keys is read once into registers; larger ones stream
+// three times (minimum, level histogram, distribution), 8 loads in flight.
+__device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
+    __syncthreads();
+    int b = -1;
+    for (int q = (int)PS.kf + 1; q <= 32; ++q)
+        if (PS.bcnt[q]) {
+            b = q;
+            break;
+        }
+    if (b < 0) return false;
+    const uint32_t c = PS.bcnt[b];
+    const bool inreg = c <= (uint32_t)(kParT * kParRegs);
+    for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
+    for (uint32_t q = threadIdx.x; q < 33; q += kParT) PS.hist[q] = 0;
+    if (threadIdx.x == 0) PS.fcnt = 0;
+    uint64_t x[kParRegs];
+    uint32_t vm = 0;
+    // pass 1: minimum (raw; a cancelled duplicate is still a lower bound of every live key)
+    uint64_t mn = kEmpty64;
+    if (inreg) {
+        vm = bucket_batch(P, (uint32_t)b, 0, c, x);
+#pragma unroll
+        for (int r = 0; r < kParRegs; ++r) mn = x[r] < mn ? x[r] : mn;
+    } else {
+        for (uint32_t e0 = 0; e0 < c; e0 += kParT * kParRegs) {
+            uint64_t y[kParRegs];
+            (void)bucket_batch(P, (uint32_t)b, e0, c, y);
+#pragma unroll
+            for (int r = 0; r < kParRegs; ++r) mn = y[r] < mn ? y[r] : mn;
+        }
+    }
+    mn = C.rd.min(mn);  // barrier: the resets above are done too
+    const uint32_t nl = (uint32_t)(mn >> 32);
+    // pass 2: histogram of the new levels (all < b)
+    if (inreg) {
+#pragma unroll
+        for (int r = 0; r < kParRegs; ++r)
+            if ((vm >> r) & 1u) atomicAdd(&PS.hist[par_bucket((uint32_t)(x[r] >> 32), nl)], 1u);
+    } else {
+        for (uint32_t e0 = 0; e0 < c; e0 += kParT * kParRegs) {
+            uint64_t y[kParRegs];
+            const uint32_t ym = bucket_batch(P, (uint32_t)b, e0, c, y);
+#pragma unroll
+            for (int r = 0; r < kParRegs; ++r)
+                if ((ym >> r) & 1u) atomicAdd(&PS.hist[par_bucket((uint32_t)(y[r] >> 32), nl)], 1u);
+        }
+    }
+    __syncthreads();
+    int keep = -1;
+    uint32_t cum = 0;
+    for (int q = 0; q < b; ++q) {
+        cum += PS.hist[q];
+        if (cum <= kFrontFill) keep = q;
+    }
+    if (keep < 0) {
+        if (PS.hist[0] <= kFrontLive) keep = 0;
+        else {
+            if (threadIdx.x == 0) PS.err = 32;
+            __syncthreads();
+            return false;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        PS.bcnt[b] = 0;  // consumed (its chunks stay with this workgroup)
+        PS.last = nl;
+        PS.kf = (uint32_t)keep;
+    }
+    __syncthreads();
+    // pass 3: distribute (front: toggles; below b: appends to empty lower buckets)
+    for (uint32_t e0 = 0; e0 < c; e0 += kParT * kParRegs) {
+        if (!inreg) vm = bucket_batch(P, (uint32_t)b, e0, c, x);
+        // the front takes at most kFrontLive keys in all: compaction keeps room
+        if (PS.fcnt + kParRegs * kParT > kFrontLog) front_compact(C.rd, 33);
+        uint32_t fm = 0, bm = 0, bb[kParRegs];
+#pragma unroll
+        for (int r = 0; r < kParRegs; ++r) {
+            bb[r] = par_bucket((uint32_t)(x[r] >> 32), nl);
+            if ((vm >> r) & 1u) {
+                if (bb[r] <= (uint32_t)keep) fm |= 1u << r;
+                else bm |= 1u << r;
+            }
+        }
+        front_toggle<kParRegs>(x, fm);
+        bucket_append<kParRegs>(x, bb, bm, P);
+        if (PS.err) return false;
+    }
+    __syncthreads();
+    return true;
+}
+
+// toggle the coboundary of edge (a > b), diameter sd, into the column.
+// Round 0's rows may already be in registers (da0 / db0, prefetched with the pivot).
+template <bool PACKED>
+__device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float* __restrict__ D, int n, float r, int a, int b, float sd,
+                        const float (&da0)[kParRV], const float (&db0)[kParRV]) {
+    for (int v0 = 0; v0 < n; v0 += kParT * kParRV) {
+        float da[kParRV], db[kParRV];
+#pragma unroll
+        for (int q = 0; q < kParRV; ++q) {
+            const int v = v0 + (int)threadIdx.x + q * kParT;
+            if (v0 == 0) {
+                da[q] = da0[q];
+                db[q] = db0[q];
+            } else {
+                da[q] = v < n ? ld_glb(D, (size_t)a * n + v) : 0.0f;
+                db[q] = v < n ? ld_glb(D, (size_t)b * n + v) : 0.0f;
+            }
+        }
+        uint64_t key[kParRV];
+        uint32_t vm = 0;
+#pragma unroll
+        for (int q = 0; q < kParRV; ++q) {
+            const int v = v0 + (int)threadIdx.x + q * kParT;
+            key[q] = 0;
+            if (v >= n || v == a || v == b) continue;
+            const float cd = fmaxf(sd, fmaxf(da[q], db[q]));
+            if (!(cd <= r)) continue;
+            // vertices descending; the edge omitting vertex u has length excl(u):
+            // excl(v) = sd, excl(a) = |bv| = db, excl(b) = |av| = da
+            int x, y, z;
+            float ex, ey, ez;
+            if (v > a) {
+                x = v, y = a, z = b;
+                ex = sd, ey = db[q], ez = da[q];
+            } else if (v > b) {
+                x = a, y = v, z = b;
+                ex = db[q], ey = sd, ez = da[q];
+            } else {
+                x = a, y = b, z = v;
+                ex = db[q], ey = da[q], ez = sd;
+            }
+            int f = 0;
+            float fd = ex;
+            if (ey > fd) f = 1, fd = ey;
+            if (ez > fd) f = 2;
+            key[q] = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | tri_lo<PACKED>(x, y, z, f);
+            vm |= 1u << q;
+        }
+        col_add<kParRV>(C, P, key, vm);
+        if (PS.err) return;
+    }
+}
+
+// Publish the working column as an immutable record (sc1 stores, drained).
+// Returns the record id (block-uniform), or -1 on overflow.
+__device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_t pkey, uint64_t item) {
+    const uint32_t c = PS.fcnt;
+    uint32_t lv = 0;
+    for (uint32_t e = threadIdx.x; e < c; e += kParT) lv += PS.log[e] < kDead;
+    const uint64_t nfront = C.rd.sum(lv);
+    uint64_t nback = 0;
+    for (int q = 0; q <= 32; ++q) nback += PS.bcnt[q];
+    const uint64_t total = nfront + nback;
+    if (threadIdx.x == 0) {
+        const uint64_t o = aadd(&P.ctl->rpool_used, (total + 15) & ~15ull);  // 128-B aligned records
+        const uint64_t id = aadd(&P.ctl->rec_used, 1ull);
+        PS.bc[0] = (o + total <= P.rpool_cap && id < P.rec_cap) ? o : kEmpty64;
+        PS.bc[1] = id;
+    }
+    __syncthreads();
+    const uint64_t off = PS.bc[0], id = PS.bc[1];
+    if (off == kEmpty64) {
+        if (threadIdx.x == 0) PS.err = 41;
+        __syncthreads();
+        return -1;
+    }
+    uint64_t* out = P.rpool + off;
+    uint32_t w = 0;
+    for (uint32_t e0 = 0; e0 < c; e0 += kParT) {
+        const uint32_t e = e0 + threadIdx.x;
+        const uint64_t x = e < c ? PS.log[e] : kEmpty64;
+        const bool live = x < kDead;
+        uint32_t tot;
+        const uint32_t o = C.rd.prefix(live ? 1u : 0u, &tot);
+        if (live) ast(out + w + o, x);
+        w += tot;
+    }
+    uint64_t pos = nfront;
+    for (int q = 0; q <= 32; ++q) {
+        const uint32_t cq = PS.bcnt[q];
+        for (uint32_t e = threadIdx.x; e < cq; e += kParT) ast(out + pos + e, bucket_at(P, (uint32_t)q, e));
+        pos += cq;
+    }
+    if (threadIdx.x == 0) {
+        uint64_t* rh = P.rec + id * 4;
+        ast(rh + 0, off);
+        ast(rh + 1, total);
+        ast(rh + 2, pkey);
+        ast(rh + 3, item);
+    }
+    drain_vm();  // every storing wave, before the barrier that precedes the publishing CAS
+    __syncthreads();
+    return (int64_t)id;
+}
+
+// add record `id` (sc1 loads) to the working column
+__device__ __forceinline__ void col_add_record(ParCol& C, const ParBufs& P, uint64_t id) {
+    if (threadIdx.x == 0) {
+        PS.bc[2] = ald(P.rec + id * 4 + 0);
+        PS.bc[3] = ald(P.rec + id * 4 + 1);
+    }
+    __syncthreads();
+    const uint64_t off = PS.bc[2], len = PS.bc[3];
+    __syncthreads();
+    for (uint64_t e0 = 0; e0 < len; e0 += kParT * kParRegs) {
+        uint64_t x[kParRegs];
+        uint32_t vm = 0;
+#pragma unroll
+        for (int q = 0; q < kParRegs; ++q) {
+            const uint64_t e = e0 + threadIdx.x + (uint64_t)q * kParT;
+            x[q] = e < len ? ald(P.rpool + off + e) : 0;
+            if (e < len) vm |= 1u << q;
+        }
+        col_add<kParRegs>(C, P, x, vm);
+        if (PS.err) return;
+    }
+}
+
+// owner-map probe (one lane): slot of pivot pidx, and its value (0 if absent: *slot = first empty)
+__device__ __forceinline__ uint64_t omap_find(const ParBufs& P, uint64_t* okey, uint64_t* oval, uint64_t mask, uint64_t pidx, uint64_t* slot,
+                              bool* found) {
+    uint64_t h = mix64(pidx) & mask;
+    for (uint64_t it = 0; it <= mask; ++it, h = (h + 1) & mask) {
+        const uint64_t k = ald(okey + h);
+        if (k == pidx + 1) {
+            *slot = h;
+            *found = true;
+            for (uint32_t s = 0; s < kParSpin; ++s) {  // the inserter stores the value right after its key CAS
+                const uint64_t v = ald(oval + h);
+                if (v) return v;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            return kEmpty64;  // hung
+        }
+        if (k == 0) {
+            *slot = h;
+            *found = false;
+            return 0;
+        }
+    }
+    *found = false;
+    return kEmpty64;  // map full
+}
+
+__device__ __forceinline__ uint64_t par_omask(uint64_t nres, uint64_t ostride) {
+    uint64_t m = 16;
+    while (m < 2 * nres + 16) m <<= 1;
+    return (m > ostride ? ostride : m) - 1;
+}
+
+template <bool PACKED>
+__global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ dist, int n, int L, LayerStats* __restrict__ stats,
+                                                      DimBufs b1, Reduce2Bufs rb, ParBufs P) {
+    ParCol C;
+    const int tid = threadIdx.x;
+    for (uint32_t e = tid; e < 33u * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
+    if (tid == 0) PS.err = 0;
+    __syncthreads();
+    const uint64_t total = ald(&P.ctl->total);
+    for (;;) {
+        // ---------------- get work (lane 0): requeued columns first, then fresh ones.
+        // A worker with nothing to take exits: every requeue push is made by a
+        // worker that dequeues again right after, so no item is ever stranded
+        // and nobody spins idle next to the columns still being reduced.
+        if (tid == 0) {
+            uint64_t got = kEmpty64;  // item << 32 | (record + 1)
+            for (uint32_t spin = 0; spin < kParSpin; ++spin) {
+                if (ald(&P.ctl->abort)) break;
+                const uint64_t h = ald(&P.ctl->rq_head), t = ald(&P.ctl->rq_tail);
+                if (h < t && h < P.rq_cap) {
+                    if (acas((uint64_t*)&P.ctl->rq_head, h, h + 1) != h) continue;
+                    uint64_t v = 0;
+                    for (uint32_t q = 0; q < kParSpin && !(v = ald(P.rq + h)); ++q) __builtin_amdgcn_s_sleep(1);
+                    if (!v) {  // the pusher never wrote its slot
+                        aadd(&P.ctl->abort, 1);
+                        acas((uint64_t*)&P.ctl->err, 0, 51);
+                        break;
+                    }
+                    ast(P.rq + h, 0);  // slots are used once per launch; leave the ring zeroed
+                    got = v;
+                    break;
+                }
+                if (ald(&P.ctl->next) < total) {
+                    const uint64_t c = aadd(&P.ctl->next, 1);
+                    if (c < total) got = c << 32;
+                }
+                break;
+            }
+            PS.bc[4] = got;
+        }
+        __syncthreads();
+        const uint64_t got = PS.bc[4];
+        __syncthreads();
+        if (got == kEmpty64) break;
+        const uint64_t item = got >> 32;
+        const uint64_t rec0 = got & 0xFFFFFFFFull;  // 0: fresh column, else resume from record rec0 - 1
+        // ---------------- layer / column
+        int l = 0;
+        while (l + 1 < L && ld_glb(P.item_base, l + 1) <= item) ++l;
+        const uint64_t j = item - ld_glb(P.item_base, l);
+        LayerStats* st = stats + l;
+        const float r = st->thresh;
+        const float* D = dist + (size_t)l * n * n;
+        const uint64_t* resid = b1.resid + (size_t)l * b1.rcap;
+        const uint32_t* pivg = b1.pivbits + (size_t)l * b1.piv_words;
+        const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
+        uint64_t* okey = P.okey + (size_t)l * P.ostride;
+        uint64_t* oval = P.oval + (size_t)l * P.ostride;
+        uint64_t nres_l = ld_glb(P.item_base, l + 1) - ld_glb(P.item_base, l);
+        const uint64_t omask = par_omask(nres_l, P.ostride);
+        uint64_t* colpiv = P.colpiv + (size_t)l * b1.rcap;
+        const uint64_t ckey = ld_glb(resid, j);
+        const uint64_t sidx = key_idx(ckey);
+        const float sdm = key_diam(ckey);
+        int sv[2];
+        decode<1>(sidx, n, sv);
+        if (!rec0 && ((ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u)) {  // cleared: an H0 death
+            if (tid == 0) ast(colpiv + j, kParSkip);
+            continue;
+        }
+        // ---------------- working column: reset (chunks stay), then the coboundary or the record
+        for (uint32_t q = tid; q < 33; q += kParT) PS.bcnt[q] = 0;
+        if (tid == 0) {
+            PS.kf = 32;
+            PS.last = __float_as_uint(sdm + 0.0f);
+        }
+        front_reset();
+        float z0[kParRV], z1[kParRV];
+        if (!rec0) {
+#pragma unroll
+            for (int q = 0; q < kParRV; ++q) {
+                const int v = tid + q * kParT;
+                z0[q] = v < n ? ld_glb(D, (size_t)sv[0] * n + v) : 0.0f;
+                z1[q] = v < n ? ld_glb(D, (size_t)sv[1] * n + v) : 0.0f;
+            }
+            col_cob<PACKED>(C, P, D, n, r, sv[0], sv[1], sdm, z0, z1);
+        } else {
+            if (tid == 0) PS.last = (uint32_t)(ald(P.rec + (rec0 - 1) * 4 + 2) >> 32);
+            __syncthreads();
+            col_add_record(C, P, rec0 - 1);
+        }
+        int64_t my_rec = -1;
+        uint64_t adds = 0;
+        bool done = false;
+#ifdef TDA_PROFILE
+        uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nref = 0, fsum = 0;
+        const uint64_t t_col = clock64();
+        C.ncompact = C.nspill = 0;
+#endif
+        uint64_t step = 0;
+        for (; !done; ++step) {
+            __syncthreads();
+            if (PS.err) break;
+            if (step > P.step_limit) {
+                if (tid == 0) PS.err = 61;
+                break;
+            }
+#ifdef TDA_PROFILE
+            fsum += PS.fcnt;
+            uint64_t t0 = clock64();
+#endif
+            uint64_t pk = front_min(C.rd);
+#ifdef TDA_PROFILE
+            pf[1] += clock64() - t0;
+            t0 = clock64();
+#endif
+            if (pk == kEmpty64) {
+#ifdef TDA_PROFILE
+                ++nref;
+#endif
+                const bool more = col_refill(C, P);
+#ifdef TDA_PROFILE
+                pf[4] += clock64() - t0;
+#endif
+                if (!more) {
+                    if (PS.err) break;
+                    if (tid == 0) ast(colpiv + j, kParEss);  // zero column: essential
+                    done = true;
+                }
+                continue;
+            }
+            // pivot: vertices, index, apparent facet
+            int t[3], fa, fb;
+            uint64_t pidx;
+            const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
+            const float pd = __uint_as_float((uint32_t)(pk >> 32));
+            if (PACKED) {
+                t[0] = (int)(plo >> 22);
+                t[1] = (int)((plo >> 12) & 1023u);
+                t[2] = (int)((plo >> 2) & 1023u);
+                const int f = (int)(plo & 3u);
+                fa = f == 0 ? t[1] : t[0];
+                fb = f == 2 ? t[1] : t[2];
+                pidx = encode<2>(t);
+            } else {
+                pidx = plo;
+                decode<2>(pidx, n, t);
+                int fv[2];
+                (void)apparent_facet<1>(D, n, pidx, fv);
+                fa = fv[0];
+                fb = fv[1];
+            }
+            // one round trip: the pivot's bitmap word and the facet's two rows
+            float da[kParRV], db[kParRV];
+#pragma unroll
+            for (int q = 0; q < kParRV; ++q) {
+                const int v = tid + q * kParT;
+                da[q] = v < n ? ld_glb(D, (size_t)fa * n + v) : 0.0f;
+                db[q] = v < n ? ld_glb(D, (size_t)fb * n + v) : 0.0f;
+            }
+            if (tid == 0) PS.bc[5] = (ld_glb(pivg, pidx >> 5) >> (pidx & 31)) & 1u;
+            __syncthreads();
+            const bool app = PS.bc[5] != 0;
+#ifdef TDA_PROFILE
+            pf[2] += clock64() - t0;
+            t0 = clock64();
+#endif
+            if (app) {
+                col_cob<PACKED>(C, P, D, n, r, fa, fb, pd, da, db);
+                ++adds;
+#ifdef TDA_PROFILE
+                pf[3] += clock64() - t0;
+#endif
+                continue;
+            }
+            // ---------------- residual pivot: owner map
+            const uint64_t fkey = filt_key(pd, pidx);
+            for (uint32_t round = 0;; ++round) {
+                if (tid == 0) {
+                    uint64_t slot = 0;
+                    bool found = false;
+                    const uint64_t v = round > 64 ? kEmpty64 : omap_find(P, okey, oval, omask, pidx, &slot, &found);
+                    PS.bc[6] = v;
+                    PS.bc[7] = slot | (found ? 1ull << 63 : 0);
+                }
+                __syncthreads();
+                const uint64_t v = PS.bc[6];
+                const uint64_t slot = PS.bc[7] & ~(1ull << 63);
+                __syncthreads();
+                if (v == kEmpty64) {
+                    if (tid == 0) PS.err = 71;
+                    break;
+                }
+                const uint64_t oi = v >> 32;
+                if (v != 0 && oi < j) {  // earlier owner: add its record
+                    col_add_record(C, P, (v & 0xFFFFFFFFull) - 1);
+                    ++adds;
+                    break;
+                }
+                if (v != 0 && oi == j) {
+                    if (tid == 0) PS.err = 72;
+                    break;
+                }
+                // free, or owned by a later column: publish R_j, then claim
+                if (my_rec < 0) {
+                    my_rec = col_save(C, P, pk, item);
+                    if (my_rec < 0) break;
+                }
+                const uint64_t mine = (j << 32) | (uint64_t)(my_rec + 1);
+                if (tid == 0) {
+                    bool ok;
+                    if (v == 0) {
+                        const uint64_t old = acas(okey + slot, 0, pidx + 1);
+                        ok = old == 0;
+                        if (ok) ast(oval + slot, mine);
+                        // lost the key race (same pivot) or the slot (another pivot): look again
+                    } else {
+                        ok = acas(oval + slot, v, mine) == v;
+                        if (ok) {  // evict the later owner: it resumes from its record
+                            const uint64_t qt = aadd(&P.ctl->rq_tail, 1);
+                            if (qt >= P.rq_cap) {
+                                aadd(&P.ctl->abort, 1);
+                                acas((uint64_t*)&P.ctl->err, 0, 53);
+                            } else {
+                                const uint64_t oitem = ld_glb(P.item_base, l) + oi;
+                                ast(P.rq + qt, (oitem << 32) | (v & 0xFFFFFFFFull));
+                            }
+                            aadd(&P.ctl->evictions, 1);
+                        }
+                    }
+                    if (ok) ast(colpiv + j, fkey);
+                    PS.bc[6] = ok;
+                }
+                __syncthreads();
+                const bool ok = PS.bc[6] != 0;
+                __syncthreads();
+                if (ok) {
+                    done = true;
+                    break;
+                }
+            }
+            // a record added above changes the column: any saved record is stale
+            if (!done) my_rec = -1;
+#ifdef TDA_PROFILE
+            pf[5] += clock64() - t0;
+#endif
+        }
+#ifdef TDA_PROFILE
+        // the column with the most steps so far publishes its profile (layer 0 slot, racy by design)
+        if (tid == 0 && step > stats[0].prof[2][6]) {
+            pf[0] = clock64() - t_col;
+            pf[6] = step;
+            pf[7] = (fsum / (step ? step : 1)) | (nref << 16) | (C.ncompact << 32) | (C.nspill << 48);
+            for (int q = 0; q < 8; ++q) stats[0].prof[2][q] = pf[q];
+        }
+#endif
+        if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[1], (unsigned long long)adds);
+        if (PS.err) {
+            if (tid == 0) {
+                acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)item << 16) | (uint64_t)PS.err);  // first error: item, code
+                aadd(&P.ctl->abort, 1);
+            }
+            break;
+        }
+    }
+}
+
+// per-layer residual counts -> item prefix, control block, owner maps cleared
+__global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats, int L, uint64_t rcap, ParBufs P) {
+    const int l = blockIdx.y;
+    uint64_t nres = (uint64_t)stats[l].n_residual[1];
+    if (nres > rcap) nres = rcap;
+    const uint64_t m = par_omask(nres, P.ostride) + 1;
+    uint64_t* ok = P.okey + (size_t)l * P.ostride;
+    uint64_t* ov = P.oval + (size_t)l * P.ostride;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+        ok[e] = 0;
+        ov[e] = 0;
+    }
+    if (blockIdx.x == 0 && l == 0 && threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (int q = 0; q < L; ++q) {
+            P.item_base[q] = s;
+            uint64_t c = (uint64_t)stats[q].n_residual[1];
+            s += c > rcap ? rcap : c;
+        }
+        P.item_base[L] = s;
+        unsigned long long* c = (unsigned long long*)P.ctl;
+        for (int q = 0; q < (int)(sizeof(ParCtl) / 8); ++q) c[q] = 0;
+        P.ctl->total = s;
+    }
+}
+
+// Pairs from the final owners (one block per layer): emission buffer, stats,
+// and the dim-1 residual pivot map that the H2 reduction clears with.
+__global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stats, DimBufs b1, Reduce2Bufs rb, ParBufs P,
+                                                   Pair* __restrict__ pairs, uint64_t pcap, int fill_map) {
+    __shared__ uint64_t red[3][16];
+    const int l = blockIdx.x, tid = threadIdx.x;
+    LayerStats* st = stats + l;
+    const uint64_t nres = P.item_base[l + 1] - P.item_base[l];
+    const uint64_t* resid = b1.resid + (size_t)l * b1.rcap;
+    const uint64_t* colpiv = P.colpiv + (size_t)l * b1.rcap;
+    Pair* Pp = pairs + (size_t)l * pcap;
+    PivMap map;
+    map.k = rb.rmap_keys + ((size_t)l * 2 + 0) * rb.rmap_stride;  // cleared by k_sort_resid
+    map.v = rb.rmap_vals + ((size_t)l * 2 + 0) * rb.rmap_stride;
+    {
+        uint64_t rc2 = 16;
+        while (rc2 < 2 * nres + 16) rc2 <<= 1;
+        if (rc2 > rb.rmap_stride) rc2 = rb.rmap_stride;
+        map.mask = rc2 - 1;
+    }
+    map.lds = false;
+    const bool failed = P.ctl->abort != 0;
+    uint64_t cs = 0, np = 0, nskip = 0;
+    if (!failed) {
+        for (uint64_t j = tid; j < nres; j += blockDim.x) {
+            const uint64_t cp = colpiv[j];
+            const uint64_t key = resid[j];
+            const uint64_t sidx = key_idx(key);
+            const float sdm = key_diam(key);
+            if (cp == kParSkip) {
+                ++nskip;
+                continue;
+            }
+            if (cp == kParEss) {
+                const uint64_t pos = atomicAdd((unsigned long long*)&st->count[1], 1ull);
+                if (pos < pcap) store_pair(Pp, pos, sdm, INFINITY, (int64_t)sidx, -1);
+                else atomicOr(&st->err, ERR_PAIR_CAP);
+                continue;
+            }
+            const uint64_t pidx = 0xFFFFFFFFull - (cp & 0xFFFFFFFFull);
+            const float pd = __uint_as_float((uint32_t)(cp >> 32));
+            if (pd > sdm) {
+                const uint64_t pos = atomicAdd((unsigned long long*)&st->count[1], 1ull);
+                if (pos < pcap) store_pair(Pp, pos, sdm, pd, (int64_t)sidx, (int64_t)pidx);
+                else atomicOr(&st->err, ERR_PAIR_CAP);
+            }
+            cs += pair_hash(sidx, pidx);
+            ++np;
+            if (fill_map) map.insert_par_t<false>((uint32_t)pidx, (uint32_t)j);
+        }
+    }
+    cs = wave_sum_u64(cs);
+    np = wave_sum_u64(np);
+    nskip = wave_sum_u64(nskip);
+    if ((tid & 63) == 0) {
+        red[0][tid >> 6] = cs;
+        red[1][tid >> 6] = np;
+        red[2][tid >> 6] = nskip;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t a = 0, b = 0, c = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) a += red[0][w], b += red[1][w], c += red[2][w];
+        if (failed) {
+            atomicOr(&st->err, ERR_PAR);
+        } else {
+            atomicAdd((unsigned long long*)&st->checksum[1], (unsigned long long)a);
+            atomicAdd((unsigned long long*)&st->all_pairs[1], (unsigned long long)b);
+            atomicAdd((unsigned long long*)&st->n_columns[1], (unsigned long long)(0ull - c));
+            st->nskip[1] = c;
+        }
+    }
+}
+
+#undef PS
+
+}  // namespace tda
