@@ -1,12 +1,23 @@
 """Benchmark of the hot path: per-layer pairwise distance + Vietoris-Rips
 persistence H0-H2 (BASELINE.json metric "layers/sec ... at 1/2/4/8 MI355X").
 
-A step = one pass of the hot path over one batch: the reference's 32-layer
-sweep (debug_tda_pipeline.py:92-150) of 48-point clouds (configs[1] per layer:
-48 points, D=3, H0/H1/H2), inputs already resident in HBM, diagrams returned
-to the host.  Multi-GPU: one process per GPU (torchrun), every rank runs its
-own 32-layer batch (weak scaling) and the per-layer summary records are
-all-gathered over RCCL each step.  Prints ONE JSON line on rank 0.
+A step = one pass of the hot path over one batch, inputs already resident in
+HBM, diagrams returned to the host:
+  * primary (``value``): the reference's 32-layer sweep (debug_tda_pipeline.py:
+    92-150) of 48-point clouds, configs[1] per layer (48 points, D=3, H0-H2);
+  * ``workloads`` (N=1 only): configs[4] grid144 (32 layers x 144 points,
+    H0-H2) and configs[3] torus1024 (one 1024-point layer, H0-H1), each with
+    its own roofline and CPU baseline.
+Multi-GPU: one process per GPU (torchrun).  ``--scaling weak`` (default):
+every rank runs its own 32-layer sweep; ``strong``: the 32 layers are sharded
+(configs[2]: 4 layers/GPU at 8 GPUs).  Either way a step ends with the one
+gather of per-layer records to rank 0 (distributed.sharded_sweep_step); at
+N > 1 a strong-scaling record is added next to the weak one.
+
+CPU baseline: the oracle (oracle/rips_oracle.c, a C restatement of the
+ripser semantics; "kind": "port") on the same inputs, 1 core and P worker
+processes (the host CPUs this job may use, at most 16 per GPU on the box),
+on bounded samples.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -15,6 +26,7 @@ import importlib
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -22,6 +34,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+METRIC = "layers/sec (pairwise-dist + VR persistence H0-H2) at 1/2/4/8 MI355X"
+
+WORKLOADS = {
+    # name: (layers, maxdim, description, default steps, default warmup)
+    "sweep48": (32, 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2", 50, 5),
+    "grid144": (32, 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2", 10, 2),
+    "torus1024": (1, 1, "S1xS1 torus N=1024 (configs[3]), D=3, H0-H1", 5, 2),
+}
+DATA = {
+    "sweep48": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
+    "grid144": "synthetic: 12x12 grid on the torus + N(0, 0.02^2) + random rotation per layer",
+    "torus1024": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 0",
+}
+NPOINTS = {"sweep48": 48, "grid144": 144, "torus1024": 1024}
 
 
 def algo_bytes_per_layer(n: int, d: int, maxdim: int) -> int:
@@ -29,16 +55,129 @@ def algo_bytes_per_layer(n: int, d: int, maxdim: int) -> int:
     return 4 * n * d + 4 * math.comb(n, 2) + sum(12 * math.comb(n, k + 1) for k in range(1, maxdim + 1))
 
 
-def workload(name: str, layers: int):
-    pkg = importlib.import_module("tda-multimodal_amd")
-    syn = pkg.synthetic
+def make_workload(name: str, layers: int | None = None):
+    syn = importlib.import_module("tda-multimodal_amd.synthetic")
+    L = layers or WORKLOADS[name][0]
     if name == "sweep48":
-        return syn.sweep48(layers), 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2"
+        return syn.sweep48(L)
     if name == "grid144":
-        return syn.sweep144(layers), 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2"
+        return syn.sweep144(L)
     if name == "torus1024":
-        return syn.torus(1024)[None].repeat(layers, 0), 1, "S1xS1 torus N=1024 (configs[3]), D=3, H0-H1"
+        return syn.torus(1024)[None].repeat(L, 0)
     raise ValueError(name)
+
+
+# ---------------------------------------------------------------- CPU baseline
+_WORKER_CACHE: dict = {}
+
+
+def _cpu_layers(task):
+    """Worker process: the oracle on layers [lo, hi) of a workload."""
+    name, lo, hi, maxdim = task
+    from oracle import oracle
+
+    if name not in _WORKER_CACHE:
+        _WORKER_CACHE[name] = make_workload(name)
+    X = _WORKER_CACHE[name]
+    oracle.lib()
+    if hi > lo:
+        oracle.rips_batch_f32(X[lo:hi], maxdim)
+    return hi - lo
+
+
+def cpu_info() -> dict:
+    model = ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": aff, "cpu_model": model}
+
+
+def cpu_workers() -> int:
+    """CPUs this job may use: the affinity set, at most 16 (a one-GPU box's share)."""
+    if os.environ.get("TDA_CPU_WORKERS"):
+        return max(1, int(os.environ["TDA_CPU_WORKERS"]))
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(aff, 16))
+
+
+def cpu_baseline(pool, P: int, name: str, X, maxdim: int, seconds: float) -> dict:
+    """The oracle on the workload's layers: 1 core in this process, then P
+    worker processes with one layer per task, each for about `seconds`."""
+    from oracle import oracle
+
+    oracle.lib()
+    L = X.shape[0]
+    done, t1 = 0, 0.0
+    t0 = time.perf_counter()
+    while t1 < seconds and done < 100000:
+        oracle.rips_batch_f32(X[done % L:done % L + 1], maxdim)
+        done += 1
+        t1 = time.perf_counter() - t0
+    one = done / t1
+    n_tasks = max(P, int(seconds * P * one))  # ~`seconds` of work per worker
+    tasks = [(name, i % L, i % L + 1, maxdim) for i in range(n_tasks)]
+    t0 = time.perf_counter()
+    got = sum(pool.imap_unordered(_cpu_layers, tasks, chunksize=max(1, n_tasks // (8 * P))))
+    tp = time.perf_counter() - t0
+    return {"value": got / tp, "unit": "layers/s", "cores": P, "kind": "port", "value_1core": one,
+            "sample": f"{got} layers on {P} worker processes ({tp:.1f} s) and {done} layers on 1 core ({t1:.1f} s): "
+                      f"oracle/rips_oracle.c (C restatement of the ripser semantics, -O3), same inputs ({name})"}
+
+
+# ---------------------------------------------------------------- GPU measurement
+def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | None = None) -> dict:
+    L, maxdim, desc, _, _ = WORKLOADS[name]
+    L = layers or L
+    X_host = make_workload(name, L)
+    n, d = X_host.shape[1], X_host.shape[2]
+    X = torch.from_numpy(X_host).to(dev)  # resident in HBM before the timed region
+    torch.cuda.synchronize()
+    dev_ms = []
+    for _ in range(warmup):
+        pkg.ripser_batch(X, maxdim=maxdim)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True)
+        dev_ms.append(info["device_ms"])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # per-kernel durations: HIP events around every kernel with all stages on
+    # ONE stream (each interval brackets exactly one kernel), same batch,
+    # after the timed region; the dominant kernel has the largest mean
+    acc: dict = {}
+    for _ in range(max(1, min(steps, 10))):
+        _, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, stage_times=True, stage_serial=True)
+        for k, ms in info["stages"]:
+            acc.setdefault(k, []).append(ms)
+    stages = {k: sum(v) / len(v) for k, v in acc.items()}
+    kern = {k: v for k, v in stages.items() if k.startswith("k_")}
+    dom = max(kern, key=kern.get)
+    bpl = algo_bytes_per_layer(n, d, maxdim)
+    achieved = bpl * L / (kern[dom] * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            traffic = json.load(f).get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+    return {
+        "value": L * steps / el, "unit": "layers/s", "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warmup,
+        "device_ms_per_step": sum(dev_ms) / len(dev_ms), "X_host": X_host, "maxdim": maxdim,
+        "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algo_bytes_per_layer": bpl,
+                     "layers_per_launch": L, "kernel_avg_ms": kern[dom],
+                     "kernel_timing": "HIP events around each kernel on its stream, all stages serialised on one "
+                                      "stream, after the timed region (same batch)"},
+        "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+    }
 
 
 def main():
@@ -46,9 +185,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--layers", type=int, default=32)
-    ap.add_argument("--workload", default="sweep48", choices=["sweep48", "grid144", "torus1024"])
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--layers", type=int, default=None)
+    ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
+    ap.add_argument("--extra", default="grid144,torus1024",
+                    help="secondary workloads measured at N=1 (comma list, '' for none)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: every rank runs its own L-layer batch; strong: the L layers are sharded over ranks")
@@ -57,7 +198,15 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    import numpy as np
+    do_cpu = rank == 0 and world == 1 and not args.no_cpu
+    pool, P = None, 0
+    if do_cpu:  # worker processes start before this process touches the GPU
+        import multiprocessing as mp
+
+        P = cpu_workers()
+        pool = mp.get_context("spawn").Pool(P)
+        pool.map(_cpu_layers, [(args.workload, 0, 0, 0)] * P)  # warm: imports, oracle load
+
     import torch
 
     torch.cuda.set_device(local)
@@ -71,114 +220,77 @@ def main():
     if pkg.lib().tda_device_ok(local) != 1:
         raise RuntimeError("no gfx950 device")
 
-    L = args.layers if args.workload != "torus1024" else max(1, min(args.layers, 1))
-    X_host, maxdim, wl_desc = workload(args.workload, L)
-    n, d = X_host.shape[1], X_host.shape[2]
-    X = torch.from_numpy(X_host).to(dev)  # resident in HBM before the timed region
-    torch.cuda.synchronize()
+    L, maxdim, desc, _, _ = WORKLOADS[args.workload]
+    L = args.layers or L
+    prim, strong = None, None
+    if world == 1:
+        prim = measure(pkg, torch, dev, args.workload, args.steps, args.warmup, args.layers)
+        value, el_ms = prim["value"], prim["ms_per_step"]
+    else:
+        X = torch.from_numpy(make_workload(args.workload, L)).to(dev)
 
-    stage_acc: dict = {}
-    stage_ser: dict = {}
-    dev_ms: list = []
+        def run_multi(shard: bool):
+            torch.cuda.synchronize()
+            for _ in range(args.warmup):
+                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=dev, shard=shard)
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=dev, shard=shard)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks
+            return float(t.item())
 
-    def step(record: bool, stages: bool = False, serial: bool = False):
-        # timed steps replay the library's captured hipGraph; stage-timed
-        # steps run the same kernels eagerly with HIP events between them
-        if world > 1 and not stages:
-            # the multi-GPU step: shard (strong) or own batch (weak) -> one gather of records to rank 0
-            pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=dev, shard=args.scaling == "strong")
-            return None
-        res, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, stage_times=stages, stage_serial=serial)
-        if record:
-            dev_ms.append(info["device_ms"])
-        if stages:
-            acc = stage_ser if serial else stage_acc
-            for name, ms in info["stages"]:
-                acc.setdefault(name, []).append(ms)
-        return res
+        el = run_multi(args.scaling == "strong")
+        value = (L if args.scaling == "strong" else L * world) * args.steps / el
+        el_ms = el / args.steps * 1e3
+        el_s = run_multi(True) if args.scaling == "weak" else el
+        strong = {"value": L * args.steps / el_s, "unit": "layers/s", "ms_per_step": el_s / args.steps * 1e3,
+                  "scaling": "strong", "layers_total": L, "layers_per_gpu": -(-L // world)}
 
-    for _ in range(args.warmup):
-        step(False)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-
-    value = (L if args.scaling == "strong" else L * world) * args.steps / el
-    # per-kernel durations: HIP events around each kernel, same batch, right
-    # after the timed region (events cannot ride inside the graph).  Two eager
-    # passes: the normal four-stream schedule (an interval can include time
-    # queued behind a side stream's kernel) and every stage back to back on
-    # one stream (an interval holds one kernel, but kernels that exit early on
-    # a concurrent kernel's results do more work).  Per kernel the smaller
-    # mean is its uncontended duration.
-    for _ in range(min(args.steps, 10)):
-        step(False, stages=True)
-    for _ in range(min(args.steps, 10)):
-        step(False, stages=True, serial=True)
-    stage_avg = {k: float(np.mean(v)) for k, v in stage_acc.items()}
-    ser_avg = {k: float(np.mean(v)) for k, v in stage_ser.items()}
-    kern = {k: min(v, ser_avg.get(k, v)) for k, v in stage_avg.items() if k.startswith("k_")}
-    dom = max(kern, key=kern.get)
-    bpl = algo_bytes_per_layer(n, d, maxdim)
-    achieved = bpl * L / (kern[dom] * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        traffic = pmc.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle import oracle
-
-        oracle.lib()
-        reps, t_cpu = 0, 0.0
-        tc0 = time.perf_counter()
-        while t_cpu < args.cpu_seconds and reps < 1000:
-            oracle.rips_batch_f32(X_host, maxdim)
-            reps += 1
-            t_cpu = time.perf_counter() - tc0
-        cpu = {"value": L * reps / t_cpu, "unit": "layers/s", "cores": 1, "kind": "port",
-               "sample": f"{reps} x the same {L}-layer batch ({wl_desc}), oracle/rips_oracle.c single thread, "
-                         f"{t_cpu:.1f} s"}
-
+    out = None
     if rank == 0:
         out = {
-            "metric": "layers/sec (pairwise-dist + VR persistence H0-H2) at 1/2/4/8 MI355X",
-            "value": value,
-            "unit": "layers/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
-            "config": {"workload": wl_desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d),
-                       "maxdim": maxdim, "parallelism": f"layers sharded, {world} process(es) x 1 GPU, RCCL all-gather of records"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algo_bytes_per_layer": bpl, "layers_per_launch": L, "kernel_avg_ms": kern[dom],
-                         "kernel_timing": "HIP events around the kernel after the timed region, min of the means of a four-stream and a single-stream eager pass of the same batch"},
-            "device_ms_per_step": float(np.mean(dev_ms)) if dev_ms else None,
-            "stages_ms": {k: round(v, 5) for k, v in stage_avg.items()},
-            "stages_ms_single_stream": {k: round(v, 5) for k, v in ser_avg.items()},
-            "cpu_baseline": cpu,
+            "metric": METRIC, "value": value, "unit": "layers/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el_ms, "higher_is_better": True, "scaling": args.scaling,
+            "vs_baseline": None, "dtype": "f32", "data": DATA[args.workload],
+            "config": {"workload": desc, "layers_per_gpu_step": L if args.scaling == "weak" else -(-L // world),
+                       "n_points": NPOINTS[args.workload], "dim": 3, "maxdim": maxdim,
+                       "parallelism": f"layers sharded ({args.scaling}), {world} process(es) x 1 GPU, "
+                                      f"RCCL gather of per-layer records"},
+            "roofline": prim["roofline"] if prim else None,
+            "cpu_baseline": None,
         }
+        if prim:
+            out["device_ms_per_step"] = prim["device_ms_per_step"]
+            out["stages_ms"] = prim["stages_ms"]
+        if strong:
+            out["strong"] = strong
+    if rank == 0 and world == 1:
+        if do_cpu:
+            cb = cpu_baseline(pool, P, args.workload, prim["X_host"], prim["maxdim"], args.cpu_seconds)
+            cb.update(cpu_info())
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu"] = {"all_cores": value / cb["value"], "one_core": value / cb["value_1core"]}
+        out["workloads"] = {}
+        for w in [w for w in args.extra.split(",") if w and w != args.workload]:
+            _, _, _, st, wu = WORKLOADS[w]
+            m = measure(pkg, torch, dev, w, st, wu)
+            rec = {k: m[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "device_ms_per_step",
+                                     "config", "roofline", "stages_ms")}
+            rec["data"] = DATA[w]
+            if do_cpu:
+                rec["cpu_baseline"] = cpu_baseline(pool, P, w, m["X_host"], m["maxdim"], args.cpu_seconds)
+                rec["speedup_vs_cpu"] = {"all_cores": m["value"] / rec["cpu_baseline"]["value"],
+                                         "one_core": m["value"] / rec["cpu_baseline"]["value_1core"]}
+            out["workloads"][w] = rec
+    if pool is not None:
+        pool.close()
+        pool.join()
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -341,6 +341,33 @@ static int64_t cofacets(const cx_t *c, const int64_t *vs, int dim, float sdiam, 
     return m;
 }
 
+/* the first (largest-index) cofacet with diameter == sdiam, if any: the
+   emergent-pair probe of Ripser's compute_pairs, which stops at it instead of
+   enumerating the whole coboundary.  Returns 0 if none. */
+static int first_equal_cofacet(const cx_t *c, const int64_t *vs, int dim, float sdiam, uint64_t sidx, uint64_t *out_idx) {
+    uint64_t idx_below = sidx, idx_above = 0;
+    int k = dim + 1, pos = 0;
+    for (int64_t v = c->n - 1; v >= 0; --v) {
+        if (pos <= dim && vs[pos] == v) {
+            idx_below -= C(&c->B, v, k);
+            idx_above += C(&c->B, v, k + 1);
+            --k;
+            ++pos;
+            continue;
+        }
+        float d = sdiam;
+        for (int i = 0; i <= dim; ++i) {
+            float x = dd(c, v, vs[i]);
+            if (x > d) d = x;
+        }
+        if (d == sdiam && d <= c->thresh) {
+            *out_idx = idx_above + C(&c->B, v, k + 1) + idx_below;
+            return 1;
+        }
+    }
+    return 0;
+}
+
 static float simplex_diam(const cx_t *c, const int64_t *vs, int dim) {
     float d = 0.0f;
     for (int i = 0; i <= dim; ++i)
@@ -391,6 +418,9 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
     cx_t c;
     c.n = n;
     c.dist = dist;
+    /* ORACLE_STATS=1: debug statistics (apparent pairs, heap sizes); off by
+       default so the CPU baseline does only the work the result needs */
+    const int stats = getenv("ORACLE_STATS") != NULL;
     /* threshold (ripser.py rips_dm): enclosing radius when thresh is inf/max */
     if (isinf(thresh) || thresh == 3.402823466e+38f) {
         float enc = INFINITY;
@@ -477,9 +507,22 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
         for (int64_t j = 0; j < ncols; ++j) {
             splx_t sg = cols[j];
             decode(&c.B, sg.idx, dim, n, vsig);
+            /* emergent pair shortcut: the first cofacet (largest idx) with
+               equal diameter is the pivot; if unclaimed it pairs immediately
+               (found without enumerating the rest of the coboundary). */
+            if (!stats) {
+                uint64_t e_idx;
+                if (first_equal_cofacet(&c, vsig, dim, sg.diam, sg.idx, &e_idx) && hm_get(&piv, e_idx) < 0) {
+                    hm_put(&piv, e_idx, j);
+                    res->n_all_pairs[dim]++;
+                    res->checksum[dim] += pair_hash(sg.idx, e_idx);
+                    voff[j + 1] = vn;
+                    continue;
+                }
+            }
             int64_t m = cofacets(&c, vsig, dim, sg.diam, sg.idx, cbuf);
-            /* apparent-pair statistic (not used for the result) */
-            {
+            /* apparent-pair statistic (ORACLE_STATS=1 only; not used for the result) */
+            if (stats) {
                 int64_t best = -1;
                 for (int64_t q = 0; q < m; ++q)
                     if (best < 0 || cbuf[q].diam < cbuf[best].diam) best = q; /* decreasing idx: first min = max idx */
@@ -529,8 +572,10 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
             }
             for (;;) {
                 splx_t p = heap_get_pivot(&work);
-                if (work.n > res->max_heap[dim]) res->max_heap[dim] = work.n;
-                res->sum_heap_steps[dim] += work.n;
+                if (stats) {
+                    if (work.n > res->max_heap[dim]) res->max_heap[dim] = work.n;
+                    res->sum_heap_steps[dim] += work.n;
+                }
                 if (p.idx == HM_EMPTY) {
                     pairs_push(&P[dim], sg.diam, INFINITY, (int64_t)sg.idx, -1);
                     voff[j + 1] = vn;

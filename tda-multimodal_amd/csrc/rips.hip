@@ -1099,7 +1099,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
 #ifdef TDA_PROFILE
-    if (p.dense) {
+    if (p.dense && !p.par) {
         int arg = 0;
         uint64_t p1max = 0;
         for (int l = 0; l < L; ++l) {
@@ -1138,6 +1138,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)q[6], (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[2], (unsigned long long)q[3],
                 (unsigned long long)q[4], (unsigned long long)((q[7] >> 16) & 0xFFFF), (unsigned long long)q[5], (unsigned long long)(q[7] & 0xFFFF),
                 (unsigned long long)((q[7] >> 32) & 0xFFFF), (unsigned long long)(q[7] >> 48));
+        const uint64_t* u = w.hstats[0].prof[3];
+        fprintf(stderr, "[tda-prof]   inside adds: keys %llu, capacity %llu, front toggles %llu, bucket appends %llu cycles; %llu record adds (%llu keys); refills moved %llu keys; waiting for the slowest wave's rows %llu\n",
+                (unsigned long long)u[0], (unsigned long long)u[3], (unsigned long long)u[1], (unsigned long long)u[2],
+                (unsigned long long)u[4], (unsigned long long)u[5], (unsigned long long)u[6], (unsigned long long)u[7]);
     }
     if (p.big && !p.par)
         for (int d = 1; d <= p.maxdim; ++d) {

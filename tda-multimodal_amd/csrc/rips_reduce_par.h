@@ -52,7 +52,8 @@ constexpr uint32_t kFrontIdx = 4096;   // front index slots (512 buckets x 8)
 constexpr uint32_t kFrontLive = 1792;  // live front keys that trigger a spill
 constexpr uint32_t kFrontFill = 768;   // refill / spill target
 constexpr int kParChunks = 22;         // chunk k of an HBM bucket holds 256 << k keys
-constexpr int kParRegs = 8;            // bucket keys per thread held in registers by a refill
+constexpr int kParRegs = 8;            // keys per thread per pass of refills and record adds
+constexpr int kParRefill = 2;          // a refill keeps up to kParRefill passes (4096 keys) in registers
 constexpr int kParRV = 4;              // coboundary vertices per thread per round (kParT * 4 = 1024)
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
 constexpr uint64_t kParEss = kEmpty64;        // colpiv: essential (zero column)
@@ -137,6 +138,7 @@ struct ParLds {
     uint32_t hist[33];
     uint64_t red[2][kParW];
     uint32_t wsum[2][kParW];
+    uint32_t anyf[2][kParW];
     uint64_t bc[8];
     uint32_t fcnt;  // front log length
     uint32_t last;  // radix reference (diameter bits)
@@ -148,6 +150,17 @@ extern __shared__ ParLds par_smem[];
 
 struct ParRed {  // double-buffered block reductions: one barrier each
     uint32_t par = 0;
+    // block-wide OR of p (HIP's OR-barrier builtin lowers to three barriers)
+    __device__ __forceinline__ bool any(bool p) {
+        const uint64_t m = __ballot(p);
+        const uint32_t b = par++ & 1;
+        if ((threadIdx.x & 63) == 0) PS.anyf[b][threadIdx.x >> 6] = m != 0;
+        __syncthreads();
+        uint32_t r = 0;
+#pragma unroll
+        for (int w = 0; w < kParW; ++w) r |= PS.anyf[b][w];
+        return r != 0;
+    }
     __device__ __forceinline__ uint64_t min(uint64_t v) {
         v = wave_min_u64(v);
         const uint32_t b = par++ & 1;
@@ -211,7 +224,7 @@ __device__ __forceinline__ void front_reset() {
 // first claimant of a key inserts it live, every other copy flips its parity.
 // Precondition: fcnt + R * kParT <= kFrontLog.
 template <int R>
-__device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vmask) {
+__device__ __forceinline__ void front_toggle(ParRed& rd, const uint64_t (&k)[R], uint32_t vmask) {
     constexpr uint32_t bmask = kFrontBkts - 1;
     uint32_t bk[R], slot[R];
 #pragma unroll
@@ -222,7 +235,7 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
     uint32_t pend = vmask, ins = 0, fol = 0;
     const int ln = threadIdx.x & 63;
     // phase A: find the key (flip it), or claim a slot (inserter), or find a claim of the same key (follower)
-    for (int it = 0; __syncthreads_or(pend != 0); ++it) {
+    for (int it = 0; rd.any(pend != 0); ++it) {
         if (it > 8 * (int)kFrontBkts) {  // cannot happen while the log precondition holds
             if (threadIdx.x == 0) PS.err = 11;
             break;
@@ -232,16 +245,18 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
             if (!((pend >> r) & 1u)) continue;
             const uint32_t fp = (uint32_t)k[r];
             const uint32_t bo = bk[r] * 8;
+            // the whole bucket in four independent 16-B reads (one LDS round trip)
+            const u64x2 q0 = *(const TDA_LDS u64x2*)&PS.idx[bo], q1 = *(const TDA_LDS u64x2*)&PS.idx[bo + 2];
+            const u64x2 q2 = *(const TDA_LDS u64x2*)&PS.idx[bo + 4], q3 = *(const TDA_LDS u64x2*)&PS.idx[bo + 6];
+            const uint64_t ev[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
             int found = -1, empty = -1;
             uint64_t fe = 0;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint64_t e = PS.idx[bo + u];
-                if (found < 0 && empty < 0) {
-                    if (e == 0) empty = u;
-                    else if ((uint32_t)(e >> 32) == fp) found = u, fe = e;
-                }
+            for (int u = 7; u >= 0; --u) {  // first empty / first match, branch-free selects
+                if (ev[u] == 0) empty = u;
+                if (ev[u] != 0 && (uint32_t)(ev[u] >> 32) == fp) found = u, fe = ev[u];
             }
+            if (empty >= 0 && found > empty) found = -1;  // slots fill in order: nothing lives past the first empty
             if (found >= 0) {
                 if ((uint32_t)fe == kReserved) {
                     fol |= 1u << r;
@@ -292,7 +307,7 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
         off += (uint32_t)__popcll(m[r]);
     }
     // phase C: followers flip the inserted entry
-    if (__syncthreads_or(fol != 0)) {
+    if (rd.any(fol != 0)) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!((fol >> r) & 1u)) continue;
@@ -350,7 +365,7 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
 // Append key k[r] to bucket bb[r] (bit r of vmask); chunks that start in this
 // pass and were never allocated by this workgroup are taken from the pool.
 template <int R>
-__device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint32_t (&bb)[R], uint32_t vmask, const ParBufs& P) {
+__device__ __forceinline__ void bucket_append(ParRed& rd, const uint64_t (&k)[R], const uint32_t (&bb)[R], uint32_t vmask, const ParBufs& P) {
     // slots: one LDS atomic per key, all R issued back to back (conflicting lanes serialise inside
     // the LDS, which is far cheaper than a round trip per distinct level)
     uint32_t slot[R];
@@ -369,7 +384,7 @@ __device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint
             need = true;
         }
     }
-    if (__syncthreads_or(need)) {
+    if (rd.any(need)) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if (!((vmask >> r) & 1u)) continue;
@@ -406,14 +421,23 @@ struct ParCol {
     uint64_t steps = 0, adds = 0;
 #ifdef TDA_PROFILE
     uint64_t ncompact = 0, nspill = 0;
+    uint64_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // keys, front toggle, bucket append, capacity, R adds, R entries, refill keys, load wait
 #endif
 };
+#ifdef TDA_PROFILE
+#define PAR_T0(v) const uint64_t v = clock64()
+#define PAR_ACC(i, v) C.q[i] += clock64() - (v)
+#else
+#define PAR_T0(v)
+#define PAR_ACC(i, v)
+#endif
 
 // Insert keys (bit r of vmask; all >= the current pivot) into the working
 // column: front levels toggle in LDS, the rest append to HBM buckets.
 template <int R>
 __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
     // room for R * T new log entries; compact, and spill front levels to HBM if too many keys are live
+    PAR_T0(tc0);
     if (PS.fcnt + R * kParT > kFrontLog) {
         uint32_t w = front_compact(C.rd, 33);
 #ifdef TDA_PROFILE
@@ -446,13 +470,14 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
                 const uint32_t e = e0 + threadIdx.x;
                 uint64_t x[1] = {e < w ? PS.log[e] : 0};
                 uint32_t b[1] = {e < w ? par_bucket((uint32_t)(x[0] >> 32), last) : 0};
-                bucket_append<1>(x, b, (e < w && b[0] > (uint32_t)keep) ? 1u : 0u, P);
+                bucket_append<1>(C.rd, x, b, (e < w && b[0] > (uint32_t)keep) ? 1u : 0u, P);
             }
             __syncthreads();
             if (threadIdx.x == 0) PS.kf = (uint32_t)keep;
             front_compact(C.rd, (uint32_t)keep);
         }
     }
+    PAR_ACC(3, tc0);
     const uint32_t last = PS.last, kf = PS.kf;
     uint32_t fm = 0, bm = 0, bb[R];
 #pragma unroll
@@ -463,8 +488,12 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
             else bm |= 1u << r;
         }
     }
-    front_toggle<R>(k, fm);
-    bucket_append<R>(k, bb, bm, P);
+    PAR_T0(tf0);
+    front_toggle<R>(C.rd, k, fm);
+    PAR_ACC(1, tf0);
+    PAR_T0(tb0);
+    bucket_append<R>(C.rd, k, bb, bm, P);
+    PAR_ACC(2, tb0);
 }
 
 // kParRegs keys per thread of bucket b at [e0, c), loads all in flight
@@ -481,8 +510,9 @@ __device__ __forceinline__ uint32_t bucket_batch(const ParBufs& P, uint32_t b, u
 
 // Front empty: redistribute the lowest non-empty bucket relative to its
 // minimum.  Returns false when the working column is zero.  A bucket of up
-// to kParT * kParRegs keys is read once into registers; larger ones stream
-// three times (minimum, level histogram, distribution), 8 loads in flight.
+// to kParRefill * kParT * kParRegs keys is read once into registers; larger
+// ones stream three times (minimum, level histogram, distribution), 8 loads
+// in flight per thread.
 __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     __syncthreads();
     int b = -1;
@@ -493,20 +523,27 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
         }
     if (b < 0) return false;
     const uint32_t c = PS.bcnt[b];
-    const bool inreg = c <= (uint32_t)(kParT * kParRegs);
+    constexpr uint32_t kPass = kParT * kParRegs;
+    const bool inreg = c <= kParRefill * kPass;
+#ifdef TDA_PROFILE
+    C.q[6] += c;
+#endif
     for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
     for (uint32_t q = threadIdx.x; q < 33; q += kParT) PS.hist[q] = 0;
     if (threadIdx.x == 0) PS.fcnt = 0;
-    uint64_t x[kParRegs];
-    uint32_t vm = 0;
+    uint64_t x[kParRefill][kParRegs];
+    uint32_t vm[kParRefill] = {};
     // pass 1: minimum (raw; a cancelled duplicate is still a lower bound of every live key)
     uint64_t mn = kEmpty64;
     if (inreg) {
-        vm = bucket_batch(P, (uint32_t)b, 0, c, x);
 #pragma unroll
-        for (int r = 0; r < kParRegs; ++r) mn = x[r] < mn ? x[r] : mn;
+        for (int h = 0; h < kParRefill; ++h) vm[h] = bucket_batch(P, (uint32_t)b, h * kPass, c, x[h]);
+#pragma unroll
+        for (int h = 0; h < kParRefill; ++h)
+#pragma unroll
+            for (int r = 0; r < kParRegs; ++r) mn = x[h][r] < mn ? x[h][r] : mn;
     } else {
-        for (uint32_t e0 = 0; e0 < c; e0 += kParT * kParRegs) {
+        for (uint32_t e0 = 0; e0 < c; e0 += kPass) {
             uint64_t y[kParRegs];
             (void)bucket_batch(P, (uint32_t)b, e0, c, y);
 #pragma unroll
@@ -518,10 +555,12 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     // pass 2: histogram of the new levels (all < b)
     if (inreg) {
 #pragma unroll
-        for (int r = 0; r < kParRegs; ++r)
-            if ((vm >> r) & 1u) atomicAdd(&PS.hist[par_bucket((uint32_t)(x[r] >> 32), nl)], 1u);
+        for (int h = 0; h < kParRefill; ++h)
+#pragma unroll
+            for (int r = 0; r < kParRegs; ++r)
+                if ((vm[h] >> r) & 1u) atomicAdd(&PS.hist[par_bucket((uint32_t)(x[h][r] >> 32), nl)], 1u);
     } else {
-        for (uint32_t e0 = 0; e0 < c; e0 += kParT * kParRegs) {
+        for (uint32_t e0 = 0; e0 < c; e0 += kPass) {
             uint64_t y[kParRegs];
             const uint32_t ym = bucket_batch(P, (uint32_t)b, e0, c, y);
 #pragma unroll
@@ -552,22 +591,35 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     }
     __syncthreads();
     // pass 3: distribute (front: toggles; below b: appends to empty lower buckets)
-    for (uint32_t e0 = 0; e0 < c; e0 += kParT * kParRegs) {
-        if (!inreg) vm = bucket_batch(P, (uint32_t)b, e0, c, x);
+    auto distribute = [&](const uint64_t (&y)[kParRegs], uint32_t ym) {
         // the front takes at most kFrontLive keys in all: compaction keeps room
         if (PS.fcnt + kParRegs * kParT > kFrontLog) front_compact(C.rd, 33);
         uint32_t fm = 0, bm = 0, bb[kParRegs];
 #pragma unroll
         for (int r = 0; r < kParRegs; ++r) {
-            bb[r] = par_bucket((uint32_t)(x[r] >> 32), nl);
-            if ((vm >> r) & 1u) {
+            bb[r] = par_bucket((uint32_t)(y[r] >> 32), nl);
+            if ((ym >> r) & 1u) {
                 if (bb[r] <= (uint32_t)keep) fm |= 1u << r;
                 else bm |= 1u << r;
             }
         }
-        front_toggle<kParRegs>(x, fm);
-        bucket_append<kParRegs>(x, bb, bm, P);
-        if (PS.err) return false;
+        front_toggle<kParRegs>(C.rd, y, fm);
+        bucket_append<kParRegs>(C.rd, y, bb, bm, P);
+    };
+    if (inreg) {
+#pragma unroll
+        for (int h = 0; h < kParRefill; ++h) {
+            if (h * kPass >= c) break;
+            distribute(x[h], vm[h]);
+            if (PS.err) return false;
+        }
+    } else {
+        for (uint32_t e0 = 0; e0 < c; e0 += kPass) {
+            uint64_t y[kParRegs];
+            const uint32_t ym = bucket_batch(P, (uint32_t)b, e0, c, y);
+            distribute(y, ym);
+            if (PS.err) return false;
+        }
     }
     __syncthreads();
     return true;
@@ -591,6 +643,7 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
                 db[q] = v < n ? ld_glb(D, (size_t)b * n + v) : 0.0f;
             }
         }
+        PAR_T0(tk0);
         uint64_t key[kParRV];
         uint32_t vm = 0;
 #pragma unroll
@@ -621,6 +674,14 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
             key[q] = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | tri_lo<PACKED>(x, y, z, f);
             vm |= 1u << q;
         }
+        PAR_ACC(0, tk0);
+#ifdef TDA_PROFILE
+        {  // how long the slowest wave's row loads keep the block waiting
+            PAR_T0(tw0);
+            __syncthreads();
+            PAR_ACC(7, tw0);
+        }
+#endif
         col_add<kParRV>(C, P, key, vm);
         if (PS.err) return;
     }
@@ -687,6 +748,10 @@ __device__ __forceinline__ void col_add_record(ParCol& C, const ParBufs& P, uint
     __syncthreads();
     const uint64_t off = PS.bc[2], len = PS.bc[3];
     __syncthreads();
+#ifdef TDA_PROFILE
+    C.q[4] += 1;
+    C.q[5] += len;
+#endif
     for (uint64_t e0 = 0; e0 < len; e0 += kParT * kParRegs) {
         uint64_t x[kParRegs];
         uint32_t vm = 0;
@@ -831,6 +896,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nref = 0, fsum = 0;
         const uint64_t t_col = clock64();
         C.ncompact = C.nspill = 0;
+        for (int q = 0; q < 8; ++q) C.q[q] = 0;
 #endif
         uint64_t step = 0;
         for (; !done; ++step) {
@@ -987,6 +1053,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             pf[6] = step;
             pf[7] = (fsum / (step ? step : 1)) | (nref << 16) | (C.ncompact << 32) | (C.nspill << 48);
             for (int q = 0; q < 8; ++q) stats[0].prof[2][q] = pf[q];
+            for (int q = 0; q < 8; ++q) stats[0].prof[3][q] = C.q[q];
         }
 #endif
         if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[1], (unsigned long long)adds);
