@@ -57,6 +57,12 @@ constexpr int kLdsMax = 160 * 1024;
 constexpr int kSmallN = 64;                  // one-wave H0 + LDS-resident reduction up to here
 constexpr int kAppLdsMaxN = 128;             // k_apparent stages the distance matrix in LDS up to here
 constexpr int kBigMinN = 256;                // large-N reducer above this N (global mode)
+constexpr unsigned kParGrid = 512;           // k_reduce_par workgroups: two 72-KB-LDS workgroups per CU
+unsigned par_grid_size() {
+    const char* g = getenv("TDA_PAR_GRID");
+    const unsigned v = g ? (unsigned)atoi(g) : kParGrid;
+    return v < 1 ? 1 : (v > kParGrid ? kParGrid : v);
+}
 
 // ------------------------------------------------------------------ plan
 struct Plan {
@@ -254,7 +260,8 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
             // bucket chunks: every workgroup keeps its peak bucket sizes (torus N=1024 needs ~2^26 keys
             // in all, N=2048 ~2^28); records: raw copies of the paired columns.  HBM is 288 GB.
             auto clampp = [](uint64_t x, int lo, int hi) { return std::min<uint64_t>(std::max<uint64_t>(next_pow2(x), 1ull << lo), 1ull << hi); };
-            p.bpool_cap = clampp(N * N * 128, 24, 30) << scale;
+            // + chunks 0..3 of the 33 buckets of every k_reduce_par workgroup
+            p.bpool_cap = (clampp(N * N * 128, 24, 30) << scale) + (uint64_t)kParGrid * 33 * 3840;
             p.rpool_cap = clampp(N * N * 64, 22, 29) << scale;
             p.rq_cap = 1ull << 16;
             p.o_pctl = take(sizeof(ParCtl));
@@ -978,7 +985,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 HIPC(hipGetLastError());
                 MARK("k_par_init");
                 // persistent workers: two 71-KB-LDS workgroups per CU; the surplus exits at once
-                static const unsigned par_grid = getenv("TDA_PAR_GRID") ? (unsigned)atoi(getenv("TDA_PAR_GRID")) : 512u;
+                const unsigned par_grid = par_grid_size();
                 if (p.packed)
                     hipLaunchKernelGGL(k_reduce_par<true>, dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], rb, pb);
                 else
@@ -1142,6 +1149,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         fprintf(stderr, "[tda-prof]   inside adds: keys %llu, capacity %llu, front toggles %llu, bucket appends %llu cycles; %llu record adds (%llu keys); refills moved %llu keys; waiting for the slowest wave's rows %llu\n",
                 (unsigned long long)u[0], (unsigned long long)u[3], (unsigned long long)u[1], (unsigned long long)u[2],
                 (unsigned long long)u[4], (unsigned long long)u[5], (unsigned long long)u[6], (unsigned long long)u[7]);
+        const uint64_t* v = w.hstats[0].prof[4];
+        fprintf(stderr, "[tda-prof]   record adds: room %llu, col_add %llu cycles, keys front %llu / all %llu; refill pass 3 %llu cycles\n",
+                (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2], (unsigned long long)v[3], (unsigned long long)v[5]);
     }
     if (p.big && !p.par)
         for (int d = 1; d <= p.maxdim; ++d) {

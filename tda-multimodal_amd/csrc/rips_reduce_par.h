@@ -37,7 +37,9 @@
 // visibility": record payloads are written with sc1 (agent-scope relaxed)
 // stores, every storing wave drains with s_waitcnt vmcnt(0) before the
 // workgroup barrier that precedes the publishing CAS, and every load of a
-// record is an sc1 load; map words and queue words are agent-scope atomics.
+// record header is an sc1 load, followed by one agent-scope acquire before
+// the payload's plain loads (cdna_hip_programming.md Guideline 16, R1); map
+// words and queue words are agent-scope atomics.
 // Any capacity overflow, step limit or spin limit aborts the launch and the
 // host re-runs the layer batch on k_reduce_big (the serial radix-heap kernel).
 #pragma once
@@ -115,7 +117,7 @@ __device__ __forceinline__ uint32_t par_bucket(uint32_t dbits, uint32_t last) {
     return x ? 32u - (uint32_t)__builtin_clz(x) : 0u;
 }
 __device__ __forceinline__ uint32_t chunk_of(uint32_t s) { return 31u - (uint32_t)__builtin_clz((s >> 8) + 1u); }
-__device__ __forceinline__ uint32_t chunk_start(uint32_t k) { return ((1u << k) - 1u) << 8; }
+__host__ __device__ constexpr uint32_t chunk_start(uint32_t k) { return ((1u << k) - 1u) << 8; }
 
 // triangle keys.  PACKED (N <= 1024): lo32 = ~(x << 22 | y << 12 | z << 2 | f)
 // with x > y > z the vertices and f the apparent facet (the vertex t[f] it
@@ -148,6 +150,20 @@ struct ParLds {
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup
+// release/acquire, which waits for ALL of the wave's outstanding global
+// memory operations (s_waitcnt vmcnt(0)) -- here the previous step's ~1000
+// scattered bucket stores and any row loads in flight.  The step loop only
+// exchanges LDS data across waves, so it waits for LDS (lgkmcnt) and leaves
+// global traffic in flight.  HBM bucket data written by other waves is read
+// only behind a full __syncthreads() (col_refill, col_save).
+__device__ __forceinline__ void lds_sync() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 struct ParRed {  // double-buffered block reductions: one barrier each
     uint32_t par = 0;
     // block-wide OR of p (HIP's OR-barrier builtin lowers to three barriers)
@@ -155,7 +171,7 @@ struct ParRed {  // double-buffered block reductions: one barrier each
         const uint64_t m = __ballot(p);
         const uint32_t b = par++ & 1;
         if ((threadIdx.x & 63) == 0) PS.anyf[b][threadIdx.x >> 6] = m != 0;
-        __syncthreads();
+        lds_sync();
         uint32_t r = 0;
 #pragma unroll
         for (int w = 0; w < kParW; ++w) r |= PS.anyf[b][w];
@@ -165,7 +181,7 @@ struct ParRed {  // double-buffered block reductions: one barrier each
         v = wave_min_u64(v);
         const uint32_t b = par++ & 1;
         if ((threadIdx.x & 63) == 0) PS.red[b][threadIdx.x >> 6] = v;
-        __syncthreads();
+        lds_sync();
         uint64_t m = PS.red[b][0];
 #pragma unroll
         for (int w = 1; w < kParW; ++w) m = PS.red[b][w] < m ? PS.red[b][w] : m;
@@ -175,7 +191,7 @@ struct ParRed {  // double-buffered block reductions: one barrier each
         v = wave_sum_u64(v);
         const uint32_t b = par++ & 1;
         if ((threadIdx.x & 63) == 0) PS.red[b][threadIdx.x >> 6] = v;
-        __syncthreads();
+        lds_sync();
         uint64_t m = 0;
 #pragma unroll
         for (int w = 0; w < kParW; ++w) m += PS.red[b][w];
@@ -193,7 +209,7 @@ struct ParRed {  // double-buffered block reductions: one barrier each
         }
         const uint32_t b = par++ & 1;
         if (ln == 63) PS.wsum[b][w] = x;
-        __syncthreads();
+        lds_sync();
         uint32_t before = 0, all = 0;
 #pragma unroll
         for (int q = 0; q < kParW; ++q) {
@@ -211,7 +227,6 @@ struct ParRed {  // double-buffered block reductions: one barrier each
 // CAS on the first empty slot (slots of a bucket fill in order and are only
 // cleared by a full reset), so a probe stops at the first empty slot.
 constexpr uint32_t kFrontBkts = kFrontIdx / 8;
-constexpr uint32_t kReserved = 0xFFFFFFFFu;  // slot claimed, log position not written yet
 
 __device__ __forceinline__ void front_reset() {
     for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
@@ -219,32 +234,53 @@ __device__ __forceinline__ void front_reset() {
     __syncthreads();
 }
 
-// Toggle up to R keys per thread (bit r of vmask) into the front.  Keys may
-// repeat within the pass (bucket refills and records are raw multisets): the
-// first claimant of a key inserts it live, every other copy flips its parity.
-// Precondition: fcnt + R * kParT <= kFrontLog.
+// Toggle up to R keys per thread (bit r of vmask) into the front, with NO
+// workgroup barrier: every key first gets its own log entry (one LDS atomic
+// per wave), written dead; a key found in the index flips the found entry; a
+// new key makes its entry live and claims an index slot by CAS.  Keys may
+// repeat within the pass (bucket refills and records are raw multisets): a
+// copy that loses the CAS to the same key kills its own entry and flips the
+// winner's.  The index only ever points at fully written log entries (a
+// wave's LDS operations complete in order).  Callers put a barrier between
+// this and the next read of the front.  Precondition: fcnt + R * kParT <= kFrontLog.
 template <int R>
-__device__ __forceinline__ void front_toggle(ParRed& rd, const uint64_t (&k)[R], uint32_t vmask) {
+__device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vmask) {
     constexpr uint32_t bmask = kFrontBkts - 1;
-    uint32_t bk[R], slot[R];
+    const int ln = threadIdx.x & 63;
+    // log entries for every key of the pass
+    uint64_t m[R];
+    uint32_t wtot = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        bk[r] = mix32((uint32_t)k[r]) & bmask;
-        slot[r] = 0;
+        m[r] = __ballot((vmask >> r) & 1u);
+        wtot += (uint32_t)__popcll(m[r]);
     }
-    uint32_t pend = vmask, ins = 0, fol = 0;
-    const int ln = threadIdx.x & 63;
-    // phase A: find the key (flip it), or claim a slot (inserter), or find a claim of the same key (follower)
-    for (int it = 0; rd.any(pend != 0); ++it) {
-        if (it > 8 * (int)kFrontBkts) {  // cannot happen while the log precondition holds
-            if (threadIdx.x == 0) PS.err = 11;
-            break;
-        }
+    if (!wtot) return;
+    uint32_t base = 0;
+    if (ln == 0) base = atomicAdd(&PS.fcnt, wtot);
+    base = __shfl(base, 0, 64);
+    uint32_t off = 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!((pend >> r) & 1u)) continue;
-            const uint32_t fp = (uint32_t)k[r];
-            const uint32_t bo = bk[r] * 8;
+    for (int r = 0; r < R; ++r) {
+        const uint32_t pos = base + off + lanes_below(m[r]);
+        off += (uint32_t)__popcll(m[r]);
+        if ((vmask >> r) & 1u) PS.log[pos < kFrontLog ? pos : kFrontLog - 1] = k[r] | kDead;
+    }
+    if (base + wtot > kFrontLog) {  // precondition violated (callers make room)
+        PS.err = 12;
+        return;
+    }
+    // the wave's keys now sit at log[base, base + wtot): lanes take them round
+    // robin, so every lane runs ceil(wtot / 64) probe chains whatever the
+    // spread of front keys over the lanes (a wave's LDS operations complete in
+    // order, so the entries written above are visible to every lane)
+    for (uint32_t pos = base + (uint32_t)ln; pos < base + wtot; pos += 64) {
+        const uint64_t kk = PS.log[pos] & ~kDead;
+        const uint32_t fp = (uint32_t)kk;
+        const uint64_t mine = ((uint64_t)fp << 32) | (pos + 1);
+        uint32_t bk = mix32(fp) & bmask;
+        for (uint32_t it = 0; it < 8 * kFrontBkts; ++it) {
+            const uint32_t bo = bk * 8;
             // the whole bucket in four independent 16-B reads (one LDS round trip)
             const u64x2 q0 = *(const TDA_LDS u64x2*)&PS.idx[bo], q1 = *(const TDA_LDS u64x2*)&PS.idx[bo + 2];
             const u64x2 q2 = *(const TDA_LDS u64x2*)&PS.idx[bo + 4], q3 = *(const TDA_LDS u64x2*)&PS.idx[bo + 6];
@@ -257,65 +293,24 @@ __device__ __forceinline__ void front_toggle(ParRed& rd, const uint64_t (&k)[R],
                 if (ev[u] != 0 && (uint32_t)(ev[u] >> 32) == fp) found = u, fe = ev[u];
             }
             if (empty >= 0 && found > empty) found = -1;  // slots fill in order: nothing lives past the first empty
-            if (found >= 0) {
-                if ((uint32_t)fe == kReserved) {
-                    fol |= 1u << r;
-                    slot[r] = bo + found;
-                } else {
-                    __hip_atomic_fetch_xor(&PS.log[(uint32_t)fe - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                pend &= ~(1u << r);
-            } else if (empty >= 0) {
-                const uint64_t mine = ((uint64_t)fp << 32) | kReserved;
-                const uint64_t old = atomicCAS((unsigned long long*)&PS.idx[bo + empty], 0ull, (unsigned long long)mine);
-                if (old == 0) {
-                    ins |= 1u << r;
-                    slot[r] = bo + empty;
-                    pend &= ~(1u << r);
-                } else if ((uint32_t)(old >> 32) == fp) {
-                    fol |= 1u << r;
-                    slot[r] = bo + empty;
-                    pend &= ~(1u << r);
-                }  // else: another key took the slot; probe this bucket again
-            } else {
-                bk[r] = (bk[r] + 1) & bmask;  // bucket full: next one
+            if (found >= 0) {  // present: flip it (this entry stays dead)
+                __hip_atomic_fetch_xor(&PS.log[(uint32_t)fe - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
             }
-        }
-    }
-    // phase B: inserters take log positions (one LDS atomic per wave) and publish them
-    uint32_t off = 0, wtot = 0;
-    uint64_t m[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        m[r] = __ballot((ins >> r) & 1u);
-        wtot += (uint32_t)__popcll(m[r]);
-    }
-    uint32_t base = 0;
-    if (ln == 0 && wtot) base = atomicAdd(&PS.fcnt, wtot);
-    base = __shfl(base, 0, 64);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if ((ins >> r) & 1u) {
-            const uint32_t pos = base + off + lanes_below(m[r]);
-            if (pos < kFrontLog) {
-                PS.log[pos] = k[r];
-                PS.idx[slot[r]] = ((uint64_t)(uint32_t)k[r] << 32) | (pos + 1);
-            } else {
-                PS.err = 12;
+            if (empty < 0) {  // bucket full: next one
+                bk = (bk + 1) & bmask;
+                continue;
             }
+            PS.log[pos] = kk;  // live, then publish
+            const uint64_t old = atomicCAS((unsigned long long*)&PS.idx[bo + empty], 0ull, (unsigned long long)mine);
+            if (old == 0) break;  // inserted
+            PS.log[pos] = kk | kDead;
+            if ((uint32_t)(old >> 32) == fp) {  // the same key, inserted by another copy of this pass
+                __hip_atomic_fetch_xor(&PS.log[(uint32_t)old - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+            }
+            // another key took the slot: probe this bucket again
         }
-        off += (uint32_t)__popcll(m[r]);
-    }
-    // phase C: followers flip the inserted entry
-    if (rd.any(fol != 0)) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!((fol >> r) & 1u)) continue;
-            const uint32_t pv = (uint32_t)PS.idx[slot[r]];
-            if (pv != kReserved && pv - 1 < kFrontLog)
-                __hip_atomic_fetch_xor(&PS.log[pv - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        __syncthreads();
     }
 }
 
@@ -364,49 +359,33 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
 // ------------------------------------------------------------------ HBM buckets
 // Append key k[r] to bucket bb[r] (bit r of vmask); chunks that start in this
 // pass and were never allocated by this workgroup are taken from the pool.
+// Append key k[r] to HBM bucket bb[r] (bit r of vmask), with NO workgroup
+// barrier: slots come from one LDS atomic per key; every bucket's chunks 0..3
+// are allocated when the workgroup starts, and the key that opens chunk c
+// allocates chunk c + 2, so a pass of up to 3072 keys per bucket never needs a
+// chunk that is not there yet (chunks c and c + 1 hold >= 3072 keys from c = 2
+// on).  Callers put a barrier between passes that may open new chunks.
 template <int R>
-__device__ __forceinline__ void bucket_append(ParRed& rd, const uint64_t (&k)[R], const uint32_t (&bb)[R], uint32_t vmask, const ParBufs& P) {
-    // slots: one LDS atomic per key, all R issued back to back (conflicting lanes serialise inside
-    // the LDS, which is far cheaper than a round trip per distinct level)
+__device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint32_t (&bb)[R], uint32_t vmask, const ParBufs& P) {
     uint32_t slot[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) slot[r] = ((vmask >> r) & 1u) ? atomicAdd(&PS.bcnt[bb[r]], 1u) : 0u;
-    bool need = false;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (!((vmask >> r) & 1u)) continue;
         const uint32_t kc = chunk_of(slot[r]);
-        if (kc >= (uint32_t)kParChunks) {
+        if (slot[r] == chunk_start(kc) && kc + 2 < (uint32_t)kParChunks && PS.cptr[bb[r]][kc + 2] == kNoChunk) {
+            const uint64_t sz = 256ull << (kc + 2);
+            const uint64_t o = aadd(&P.ctl->bpool_used, sz);
+            if (o + sz <= P.bpool_cap) PS.cptr[bb[r]][kc + 2] = (uint32_t)(o >> 8);
+            else PS.err = 22;
+        }
+        const uint32_t cp = kc < (uint32_t)kParChunks ? PS.cptr[bb[r]][kc] : kNoChunk;
+        if (cp == kNoChunk) {
             PS.err = 21;
-            need = true;  // takes the barrier below, so every thread sees the error
-            vmask &= ~(1u << r);
-        } else if (slot[r] == chunk_start(kc) && PS.cptr[bb[r]][kc] == kNoChunk) {
-            need = true;
+            continue;
         }
-    }
-    if (rd.any(need)) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!((vmask >> r) & 1u)) continue;
-            const uint32_t kc = chunk_of(slot[r]);
-            if (slot[r] == chunk_start(kc) && PS.cptr[bb[r]][kc] == kNoChunk) {
-                const uint64_t sz = 256ull << kc;
-                const uint64_t o = aadd(&P.ctl->bpool_used, sz);
-                if (o + sz <= P.bpool_cap)
-                    PS.cptr[bb[r]][kc] = (uint32_t)(o >> 8);
-                else
-                    PS.err = 22;
-            }
-        }
-        __syncthreads();
-        if (PS.err) return;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (!((vmask >> r) & 1u)) continue;
-        const uint32_t kc = chunk_of(slot[r]);
-        const uint64_t at = (uint64_t)PS.cptr[bb[r]][kc] * 256 + (slot[r] - chunk_start(kc));
-        st_glb(P.bpool, at, k[r]);
+        st_glb(P.bpool, (uint64_t)cp * 256 + (slot[r] - chunk_start(kc)), k[r]);
     }
 }
 
@@ -422,6 +401,7 @@ struct ParCol {
 #ifdef TDA_PROFILE
     uint64_t ncompact = 0, nspill = 0;
     uint64_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // keys, front toggle, bucket append, capacity, R adds, R entries, refill keys, load wait
+    uint64_t q2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // record: room, add, front keys, back keys; refill: passes 1-2, pass 3
 #endif
 };
 #ifdef TDA_PROFILE
@@ -432,52 +412,67 @@ struct ParCol {
 #define PAR_ACC(i, v)
 #endif
 
-// Insert keys (bit r of vmask; all >= the current pivot) into the working
-// column: front levels toggle in LDS, the rest append to HBM buckets.
-template <int R>
-__device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
-    // room for R * T new log entries; compact, and spill front levels to HBM if too many keys are live
+// Barrier, then room in the front for `need` more log entries: compact, and
+// spill the highest front levels to HBM if too many keys are live.
+__device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t need) {
+    lds_sync();
+    if (PS.fcnt + need <= kFrontLog) return;
     PAR_T0(tc0);
-    if (PS.fcnt + R * kParT > kFrontLog) {
-        uint32_t w = front_compact(C.rd, 33);
+    uint32_t w = front_compact(C.rd, 33);
 #ifdef TDA_PROFILE
-        ++C.ncompact;
+    ++C.ncompact;
 #endif
-        if (w > kFrontLive || w + R * kParT > kFrontLog) {
+    if (w > kFrontLive || w + need > kFrontLog) {
 #ifdef TDA_PROFILE
-            ++C.nspill;
+        ++C.nspill;
 #endif
-            // spill: histogram of the live front by level, keep the lowest levels up to kFrontFill
-            for (uint32_t q = threadIdx.x; q < 33; q += kParT) PS.hist[q] = 0;
-            __syncthreads();
-            const uint32_t last = PS.last;
-            for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket((uint32_t)(PS.log[e] >> 32), last)], 1u);
-            __syncthreads();
-            int keep = -1;
-            uint32_t cum = 0;
-            for (int q = 0; q <= (int)PS.kf; ++q) {
-                cum += PS.hist[q];
-                if (cum <= kFrontFill) keep = q;
-            }
-            if (keep < 0) {  // the exact-diameter level alone is too large for the front
-                if (PS.hist[0] + R * kParT <= kFrontLog) keep = 0;
-                else if (threadIdx.x == 0) PS.err = 31;
-            }
-            __syncthreads();
-            if (PS.err) return;
-            // move the levels above `keep` out to their HBM buckets, then drop them from the front
-            for (uint32_t e0 = 0; e0 < w; e0 += kParT) {
-                const uint32_t e = e0 + threadIdx.x;
-                uint64_t x[1] = {e < w ? PS.log[e] : 0};
-                uint32_t b[1] = {e < w ? par_bucket((uint32_t)(x[0] >> 32), last) : 0};
-                bucket_append<1>(C.rd, x, b, (e < w && b[0] > (uint32_t)keep) ? 1u : 0u, P);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) PS.kf = (uint32_t)keep;
-            front_compact(C.rd, (uint32_t)keep);
+        // histogram of the live front by level, keep the lowest levels up to kFrontFill
+        for (uint32_t q = threadIdx.x; q < 33; q += kParT) PS.hist[q] = 0;
+        __syncthreads();
+        const uint32_t last = PS.last;
+        for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket((uint32_t)(PS.log[e] >> 32), last)], 1u);
+        __syncthreads();
+        int keep = -1;
+        uint32_t cum = 0;
+        for (int q = 0; q <= (int)PS.kf; ++q) {
+            cum += PS.hist[q];
+            if (cum <= kFrontFill) keep = q;
         }
+        if (keep < 0) {  // the exact-diameter level alone is too large for the front
+            if (PS.hist[0] + need <= kFrontLog) keep = 0;
+            else if (threadIdx.x == 0) PS.err = 31;
+        }
+        __syncthreads();
+        if (PS.err) return;
+        // move the levels above `keep` out to their HBM buckets, then drop them from the front
+        for (uint32_t e0 = 0; e0 < w; e0 += kParT) {
+            const uint32_t e = e0 + threadIdx.x;
+            uint64_t x[1] = {e < w ? PS.log[e] : 0};
+            uint32_t b[1] = {e < w ? par_bucket((uint32_t)(x[0] >> 32), last) : 0};
+            bucket_append<1>(x, b, (e < w && b[0] > (uint32_t)keep) ? 1u : 0u, P);
+            __syncthreads();  // chunk pointers opened by this pass
+        }
+        if (threadIdx.x == 0) PS.kf = (uint32_t)keep;
+        front_compact(C.rd, (uint32_t)keep);
     }
     PAR_ACC(3, tc0);
+}
+
+// Insert keys (bit r of vmask; all >= the current pivot) into the working
+// column: front levels toggle in LDS, the rest append to HBM buckets.  No
+// barrier: the caller made room (front_room) for every key of the pass.
+// Back keys of one coboundary round kept in registers: appended to their HBM
+// buckets during the NEXT step, while that step's row loads are in flight
+// (they never affect the next pivot: every back key is above every front key).
+struct ParStash {
+    uint64_t k[kParRV];
+    uint32_t b[kParRV];
+    uint32_t m = 0;
+};
+
+template <int R>
+__device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask,
+                                        ParStash* stash = nullptr) {
     const uint32_t last = PS.last, kf = PS.kf;
     uint32_t fm = 0, bm = 0, bb[R];
 #pragma unroll
@@ -489,10 +484,25 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
         }
     }
     PAR_T0(tf0);
-    front_toggle<R>(C.rd, k, fm);
+    front_toggle<R>(k, fm);
     PAR_ACC(1, tf0);
+    if constexpr (R == kParRV) {
+        if (stash) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) stash->k[r] = k[r], stash->b[r] = bb[r];
+            stash->m = bm;
+            return;
+        }
+    }
     PAR_T0(tb0);
-    bucket_append<R>(C.rd, k, bb, bm, P);
+    bucket_append<R>(k, bb, bm, P);
+    PAR_ACC(2, tb0);
+}
+
+__device__ __forceinline__ void stash_flush(ParCol& C, const ParBufs& P, ParStash& st) {
+    PAR_T0(tb0);
+    bucket_append<kParRV>(st.k, st.b, st.m, P);
+    st.m = 0;
     PAR_ACC(2, tb0);
 }
 
@@ -590,9 +600,13 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
         PS.kf = (uint32_t)keep;
     }
     __syncthreads();
+#ifdef TDA_PROFILE
+    const uint64_t t3 = clock64();
+#endif
     // pass 3: distribute (front: toggles; below b: appends to empty lower buckets)
     auto distribute = [&](const uint64_t (&y)[kParRegs], uint32_t ym) {
         // the front takes at most kFrontLive keys in all: compaction keeps room
+        __syncthreads();  // chunk pointers opened by the previous pass
         if (PS.fcnt + kParRegs * kParT > kFrontLog) front_compact(C.rd, 33);
         uint32_t fm = 0, bm = 0, bb[kParRegs];
 #pragma unroll
@@ -603,33 +617,35 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
                 else bm |= 1u << r;
             }
         }
-        front_toggle<kParRegs>(C.rd, y, fm);
-        bucket_append<kParRegs>(C.rd, y, bb, bm, P);
+        front_toggle<kParRegs>(y, fm);
+        bucket_append<kParRegs>(y, bb, bm, P);
     };
     if (inreg) {
 #pragma unroll
         for (int h = 0; h < kParRefill; ++h) {
             if (h * kPass >= c) break;
             distribute(x[h], vm[h]);
-            if (PS.err) return false;
         }
     } else {
         for (uint32_t e0 = 0; e0 < c; e0 += kPass) {
             uint64_t y[kParRegs];
             const uint32_t ym = bucket_batch(P, (uint32_t)b, e0, c, y);
             distribute(y, ym);
-            if (PS.err) return false;
         }
     }
     __syncthreads();
-    return true;
+#ifdef TDA_PROFILE
+    C.q2[5] += clock64() - t3;
+#endif
+    return PS.err == 0;
 }
 
-// toggle the coboundary of edge (a > b), diameter sd, into the column.
+// toggle the coboundary of edge (a > b), diameter sd, into the column (no
+// barrier; the caller made room for n front keys: front_room(C, P, par_need(n))).
 // Round 0's rows may already be in registers (da0 / db0, prefetched with the pivot).
 template <bool PACKED>
 __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float* __restrict__ D, int n, float r, int a, int b, float sd,
-                        const float (&da0)[kParRV], const float (&db0)[kParRV]) {
+                        const float (&da0)[kParRV], const float (&db0)[kParRV], ParStash* stash = nullptr) {
     for (int v0 = 0; v0 < n; v0 += kParT * kParRV) {
         float da[kParRV], db[kParRV];
 #pragma unroll
@@ -675,21 +691,18 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
             vm |= 1u << q;
         }
         PAR_ACC(0, tk0);
-#ifdef TDA_PROFILE
-        {  // how long the slowest wave's row loads keep the block waiting
-            PAR_T0(tw0);
-            __syncthreads();
-            PAR_ACC(7, tw0);
-        }
-#endif
-        col_add<kParRV>(C, P, key, vm);
-        if (PS.err) return;
+        col_add<kParRV>(C, P, key, vm, v0 == 0 ? stash : nullptr);  // no barrier: the caller made room for all n keys
     }
+}
+
+__host__ __device__ __forceinline__ uint32_t par_need(int n) {  // log entries one coboundary can add
+    return (uint32_t)((n + kParT * kParRV - 1) / (kParT * kParRV)) * kParT * kParRV;
 }
 
 // Publish the working column as an immutable record (sc1 stores, drained).
 // Returns the record id (block-uniform), or -1 on overflow.
 __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_t pkey, uint64_t item) {
+    __syncthreads();  // full barrier: every wave's bucket stores are visible to the copy below
     const uint32_t c = PS.fcnt;
     uint32_t lv = 0;
     for (uint32_t e = threadIdx.x; e < c; e += kParT) lv += PS.log[e] < kDead;
@@ -741,9 +754,11 @@ __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_
 
 // add record `id` (sc1 loads) to the working column
 __device__ __forceinline__ void col_add_record(ParCol& C, const ParBufs& P, uint64_t id) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // header by sc1 loads, then ONE agent acquire: the payload reads are plain loads
         PS.bc[2] = ald(P.rec + id * 4 + 0);
         PS.bc[3] = ald(P.rec + id * 4 + 1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        drain_vm();
     }
     __syncthreads();
     const uint64_t off = PS.bc[2], len = PS.bc[3];
@@ -758,12 +773,30 @@ __device__ __forceinline__ void col_add_record(ParCol& C, const ParBufs& P, uint
 #pragma unroll
         for (int q = 0; q < kParRegs; ++q) {
             const uint64_t e = e0 + threadIdx.x + (uint64_t)q * kParT;
-            x[q] = e < len ? ald(P.rpool + off + e) : 0;
+            x[q] = e < len ? ld_glb(P.rpool, off + e) : 0;
             if (e < len) vm |= 1u << q;
         }
-        col_add<kParRegs>(C, P, x, vm);
+        PAR_T0(tr0);
+        front_room(C, P, kParT * kParRegs);
+#ifdef TDA_PROFILE
+        C.q2[0] += clock64() - tr0;
+        {
+            uint32_t nf = 0;
+#pragma unroll
+            for (int q = 0; q < kParRegs; ++q)
+                nf += ((vm >> q) & 1u) && par_bucket((uint32_t)(x[q] >> 32), PS.last) <= PS.kf;
+            C.q2[2] += C.rd.sum(nf);
+            C.q2[3] += C.rd.sum((uint32_t)__builtin_popcount(vm)) ;
+        }
+        const uint64_t ta0 = clock64();
+#endif
         if (PS.err) return;
+        col_add<kParRegs>(C, P, x, vm);
+#ifdef TDA_PROFILE
+        C.q2[1] += clock64() - ta0;
+#endif
     }
+    __syncthreads();
 }
 
 // owner-map probe (one lane): slot of pivot pidx, and its value (0 if absent: *slot = first empty)
@@ -807,6 +840,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
     if (tid == 0) PS.err = 0;
     __syncthreads();
     const uint64_t total = ald(&P.ctl->total);
+    bool prealloc = false;
     for (;;) {
         // ---------------- get work (lane 0): requeued columns first, then fresh ones.
         // A worker with nothing to take exits: every requeue push is made by a
@@ -869,6 +903,25 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             continue;
         }
         // ---------------- working column: reset (chunks stay), then the coboundary or the record
+        if (!prealloc) {  // chunks 0..3 of every bucket (bucket_append opens chunk c + 2 from chunk c)
+            if (tid == 0) {
+                constexpr uint64_t per = 33ull * chunk_start(4);
+                const uint64_t o = aadd(&P.ctl->bpool_used, per);
+                PS.bc[5] = o + per <= P.bpool_cap ? o : kEmpty64;
+            }
+            __syncthreads();
+            const uint64_t o = PS.bc[5];
+            if (o == kEmpty64) {
+                if (tid == 0) {
+                    acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)item << 16) | 22u);
+                    aadd(&P.ctl->abort, 1);
+                }
+                break;
+            }
+            for (uint32_t e = tid; e < 33u * 4u; e += kParT)
+                PS.cptr[e / 4][e % 4] = (uint32_t)((o + (e / 4) * chunk_start(4) + chunk_start(e % 4)) >> 8);
+            prealloc = true;
+        }
         for (uint32_t q = tid; q < 33; q += kParT) PS.bcnt[q] = 0;
         if (tid == 0) {
             PS.kf = 32;
@@ -896,11 +949,13 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nref = 0, fsum = 0;
         const uint64_t t_col = clock64();
         C.ncompact = C.nspill = 0;
-        for (int q = 0; q < 8; ++q) C.q[q] = 0;
+        for (int q = 0; q < 8; ++q) C.q[q] = C.q2[q] = 0;
 #endif
         uint64_t step = 0;
+        const uint32_t need = par_need(n);
+        ParStash stash;
         for (; !done; ++step) {
-            __syncthreads();
+            front_room(C, P, need);  // barrier: the previous step's toggles and appends are done
             if (PS.err) break;
             if (step > P.step_limit) {
                 if (tid == 0) PS.err = 61;
@@ -919,6 +974,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #ifdef TDA_PROFILE
                 ++nref;
 #endif
+                stash_flush(C, P, stash);  // the refill reads every bucket count
                 const bool more = col_refill(C, P);
 #ifdef TDA_PROFILE
                 pf[4] += clock64() - t0;
@@ -959,15 +1015,16 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 da[q] = v < n ? ld_glb(D, (size_t)fa * n + v) : 0.0f;
                 db[q] = v < n ? ld_glb(D, (size_t)fb * n + v) : 0.0f;
             }
-            if (tid == 0) PS.bc[5] = (ld_glb(pivg, pidx >> 5) >> (pidx & 31)) & 1u;
-            __syncthreads();
-            const bool app = PS.bc[5] != 0;
+            // every thread reads the pivot's bitmap word (one address per wave): no barrier
+            const uint32_t pw = ld_glb(pivg, pidx >> 5);
+            stash_flush(C, P, stash);  // the previous step's back keys, under this step's load latency
+            const bool app = (pw >> (pidx & 31)) & 1u;
 #ifdef TDA_PROFILE
             pf[2] += clock64() - t0;
             t0 = clock64();
 #endif
             if (app) {
-                col_cob<PACKED>(C, P, D, n, r, fa, fb, pd, da, db);
+                col_cob<PACKED>(C, P, D, n, r, fa, fb, pd, da, db, &stash);
                 ++adds;
 #ifdef TDA_PROFILE
                 pf[3] += clock64() - t0;
@@ -1054,6 +1111,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             pf[7] = (fsum / (step ? step : 1)) | (nref << 16) | (C.ncompact << 32) | (C.nspill << 48);
             for (int q = 0; q < 8; ++q) stats[0].prof[2][q] = pf[q];
             for (int q = 0; q < 8; ++q) stats[0].prof[3][q] = C.q[q];
+            for (int q = 0; q < 8; ++q) stats[0].prof[4][q] = C.q2[q];
         }
 #endif
         if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[1], (unsigned long long)adds);
