@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TDA_RIPS_ABI_VERSION 2
+#define TDA_RIPS_ABI_VERSION 3
 
 /* error codes */
 #define TDA_OK 0
@@ -73,6 +73,15 @@ typedef struct tda_rips_args {
      * shared by all L layers.  NULL / 0 = none. */
     const int32_t *labels;
     int32_t n_label_sets;
+    /* optional TwoNN intrinsic dimension per layer on the same distance
+     * matrices (ABI >= 3): the reference's compute_intrinsic_dimensionality
+     * (metrics.py:113-208: two nearest neighbours per point, mu = r2/r1,
+     * discard the largest `twonn_discard` fraction, slope of -log(1-F) on
+     * log(mu) through the origin).  0 = off. */
+    int32_t want_twonn;
+    float twonn_eps;       /* eps (reference default 1e-10; compared in f32)   */
+    double twonn_discard;  /* discard_fraction (reference default 0.1; f64 as
+                              in int(len * (1.0 - discard_fraction)))          */
 } tda_rips_args;
 
 /* per (layer, dim) emitted persistence pairs, in the reference's emission
@@ -110,6 +119,9 @@ typedef struct tda_rips_result {
     const float *stage_ms;
     /* [L][n_label_sets] silhouette scores when args.labels was given, else NULL */
     const double *silhouette;
+    /* [L] TwoNN intrinsic dimension when args.want_twonn (NaN where the
+     * reference returns NaN), else NULL (ABI >= 3) */
+    const float *twonn;
 } tda_rips_result;
 
 #define TDA_FLAG_STAGE_TIMES 1

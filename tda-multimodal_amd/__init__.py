@@ -7,7 +7,8 @@ include/tda_rips.h; no CPU fallback.
 """
 import sys as _sys
 
-from . import distributed, synthetic  # noqa: F401
+from . import distributed, metrics, synthetic  # noqa: F401
+from .metrics import compute_intrinsic_dimensionality  # noqa: F401
 from ._lib import EXPORTS, LIB_PATH, build, lib  # noqa: F401
 from .pipeline import get_max_persistence, get_persistence, layer_record, peak_layer, run_sweep, write_summary_stats  # noqa: F401
 from .ripser import LayerResult, persistence_pairs, ripser, ripser_batch, rips_dm, silhouette_score  # noqa: F401
@@ -27,6 +28,7 @@ __all__ = [
     "write_summary_stats",
     "peak_layer",
     "silhouette_score",
+    "compute_intrinsic_dimensionality",
     "build",
     "lib",
 ]

@@ -39,6 +39,9 @@ class RipsArgs(ctypes.Structure):
         ("flags", ctypes.c_int32),
         ("labels", ctypes.c_void_p),
         ("n_label_sets", ctypes.c_int32),
+        ("want_twonn", ctypes.c_int32),
+        ("twonn_eps", ctypes.c_float),
+        ("twonn_discard", ctypes.c_double),
     ]
 
 
@@ -70,6 +73,7 @@ class RipsResult(ctypes.Structure):
         ("stage_name", ctypes.POINTER(ctypes.c_char_p)),
         ("stage_ms", _f32p),
         ("silhouette", ctypes.POINTER(ctypes.c_double)),
+        ("twonn", _f32p),
     ]
 
 

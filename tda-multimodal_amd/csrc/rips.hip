@@ -57,6 +57,7 @@ constexpr int kLdsMax = 160 * 1024;
 constexpr int kSmallN = 64;                  // one-wave H0 + LDS-resident reduction up to here
 constexpr int kAppLdsMaxN = 128;             // k_apparent stages the distance matrix in LDS up to here
 constexpr int kBigMinN = 256;                // large-N reducer above this N (global mode)
+constexpr int64_t kDistMfmaMinD = 32;        // k_distance_mfma (FP64 MFMA Gram tiles) from this D up
 constexpr unsigned kParGrid = 512;           // k_reduce_par workgroups: two 72-KB-LDS workgroups per CU
 unsigned par_grid_size() {
     const char* g = getenv("TDA_PAR_GRID");
@@ -326,6 +327,9 @@ struct Workspace {
     char* hsil = nullptr;          // host-mapped: silhouette labels [S][N] i32, then scores [L][S] f64
     char* hsil_dev = nullptr;
     size_t hsil_cap = 0;
+    float* htn = nullptr;          // host-mapped: TwoNN estimates [L] (k_twonn writes them)
+    float* htn_dev = nullptr;
+    size_t htn_cap = 0;
     LayerStats* hstats_dev = nullptr;
     int64_t* houtoff_dev = nullptr;
     size_t hstats_cap = 0;
@@ -347,8 +351,9 @@ struct Workspace {
 // a single hipGraphLaunch when the same plan, input address and flags recur
 struct GraphKey {
     int64_t L, N, D;
-    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets, sil_K, no_par;
-    float thresh;
+    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets, sil_K, no_par, twonn;
+    float thresh, tn_eps;
+    double tn_discard;
     const void* x;
     uint64_t gen;
     bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
@@ -490,6 +495,7 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+    HIPC(hipFuncSetAttribute((const void*)k_twonn, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 4));
 #define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     TDA_ATTR_CHAIN(1, 0) TDA_ATTR_CHAIN(2, 0) TDA_ATTR_CHAIN(3, 0) TDA_ATTR_CHAIN(4, 0) TDA_ATTR_CHAIN(6, 0)
     TDA_ATTR_CHAIN(9, 0) TDA_ATTR_CHAIN(12, 0) TDA_ATTR_CHAIN(16, 0) TDA_ATTR_CHAIN(21, 0)
@@ -516,7 +522,7 @@ int set_lds_attrs(int dev) {
 struct ResultImpl {
     tda_rips_result pub;
     std::vector<int64_t> meta, num_edges, idx;
-    std::vector<float> bd, thresh, dist, stage_ms;
+    std::vector<float> bd, thresh, dist, stage_ms, tn;
     std::vector<double> sil;
     std::vector<const char*> stage_name;
 };
@@ -617,6 +623,17 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         std::memcpy(w.hsil, a.labels, (size_t)nls * n * 4);
     }
 
+    // TwoNN estimates -> host-mapped buffer (stable address: a graph source)
+    const bool want_tn = a.want_twonn != 0;
+    if (want_tn && w.htn_cap < (size_t)L) {
+        drop_graphs(w);
+        if (w.htn) HIPC(hipHostFree(w.htn));
+        w.htn = nullptr;
+        HIPC(hipHostMalloc((void**)&w.htn, sizeof(float) * std::max(L, 64), hipHostMallocMapped));
+        HIPC(hipHostGetDevicePointer((void**)&w.htn_dev, w.htn, 0));
+        w.htn_cap = std::max(L, 64);
+    }
+
     // TDA_FLAG_STAGE_SERIAL: every stage on the main stream, so each pair of
     // events brackets one kernel only (no time spent queued behind the side
     // streams' kernels); the side streams are restored on return
@@ -635,6 +652,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     StageTimer tm3{w.stage_ev3, w.stream3, tm.on, {}};
     StageTimer tm4{w.stage_ev4, w.stream4, tm.on, {}};
     if (serial_stages) tm2.fwd = tm3.fwd = tm4.fwd = &tm;
+    // D >= 32 (raw activations): Gram tiles on the FP64 matrix cores; TDA_DIST=scalar|mfma forces one (tests)
+    const bool dist_mfma = input_kind == 0 && (getenv_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !getenv_is("TDA_DIST", "scalar")));
     GraphKey gk;
     std::memset(&gk, 0, sizeof(gk));
     gk.L = p.L;
@@ -649,10 +668,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.scale = scale;
     gk.force_big = force_big;
     gk.no_par = no_par;
-    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0);
+    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
     gk.sil_K = sil_K;  // baked into the k_silhouette launch (argument K and its LDS size)
+    gk.twonn = want_tn;
+    gk.tn_discard = want_tn ? a.twonn_discard : 0.0;
+    gk.tn_eps = want_tn ? a.twonn_eps : 0.0f;
     gk.x = xsrc;
     gk.gen = w.gen;
     GraphEntry* ge = nullptr;
@@ -684,7 +706,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             x = B + p.o_x;
         }
         dim3 grid((n + 15) / 16, (n + 15) / 16, L);
-        if (p.dtype == TDA_F64)
+        const bool mfma = dist_mfma;
+        const unsigned nt = (unsigned)((n + kDmT - 1) / kDmT);
+        if (mfma && p.dtype == TDA_F64)
+            hipLaunchKernelGGL(k_distance_mfma<double>, dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const double*)x, n, (int)p.D,
+                               dist, rowmax);
+        else if (mfma)
+            hipLaunchKernelGGL(k_distance_mfma<float>, dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const float*)x, n, (int)p.D,
+                               dist, rowmax);
+        else if (p.dtype == TDA_F64)
             hipLaunchKernelGGL(k_distance<double>, grid, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax);
         else
             hipLaunchKernelGGL(k_distance<float>, grid, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax);
@@ -709,7 +739,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
     }
     HIPC(hipGetLastError());
-    MARK(input_kind == 0 ? "k_distance" : "k_square_dist");
+    MARK(input_kind != 0 ? "k_square_dist" : dist_mfma ? "k_distance_mfma" : "k_distance");
     HIPC(hipEventRecord(w.evf, s));  // fork point of the side streams
 
     DenseBufs dnb = {};
@@ -748,8 +778,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                                (double*)(w.hsil_dev + sil_out_off));
             HIPC(hipGetLastError());
             if (int rc = tm4.mark("k_silhouette")) return rc;
-            HIPC(hipEventRecord(w.evsil, s4));
         }
+        if (want_tn) {  // TwoNN intrinsic dimension on the same distance matrices
+            const int pw2 = (int)next_pow2((uint64_t)std::max(n, 64));
+            hipLaunchKernelGGL(k_twonn, dim3(L), dim3(kTnT), (size_t)pw2 * 4, s4, dist, n, a.twonn_discard, a.twonn_eps, pw2, w.htn_dev);
+            HIPC(hipGetLastError());
+            if (int rc = tm4.mark("k_twonn")) return rc;
+        }
+        if (nls || want_tn) HIPC(hipEventRecord(w.evsil, s4));
         if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
             dnb.recs = (EdgeRec*)(B + p.o_recs);
             dnb.cls = (uint32_t*)(B + p.o_cls);
@@ -1013,7 +1049,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
 
-    if (nls) HIPC(hipStreamWaitEvent(s, w.evsil, 0));  // join: silhouette scores
+    if (nls || want_tn) HIPC(hipStreamWaitEvent(s, w.evsil, 0));  // join: silhouette scores, TwoNN
     // ---- emission order, straight into host-mapped memory
     hipLaunchKernelGGL(k_emit, dim3(L), dim3(1024), kEmitLds, s, stats, L, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
                        (uint32_t*)(B + p.o_fv), p.sstride, w.houtoff_dev, w.hout_dev, (uint64_t)w.hout_cap, w.hstats_dev);
@@ -1245,6 +1281,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     } else {
         o.silhouette = nullptr;
     }
+    if (want_tn) {
+        R->tn.assign(w.htn, w.htn + L);
+        o.twonn = R->tn.data();
+    } else {
+        o.twonn = nullptr;
+    }
     o.device_ms = ms;
     for (size_t i = 0; i < tm.names.size(); ++i) {
         float t = 0.0f;
@@ -1291,6 +1333,8 @@ int validate(const tda_rips_args* a) {
     if (a->maxdim == 1 && a->N > 2900) return fail(TDA_E_UNSUPPORTED, "maxdim=1 requires N <= 2900");
     if (a->maxdim == 2 && a->N > 568) return fail(TDA_E_UNSUPPORTED, "maxdim=2 requires N <= 568");
     if (std::isnan(a->thresh)) return fail(TDA_E_INVALID, "thresh is NaN");
+    if (a->want_twonn && !(a->twonn_discard >= 0.0 && a->twonn_discard < 1.0 && a->twonn_eps >= 0.0f))
+        return fail(TDA_E_INVALID, "TwoNN needs 0 <= discard_fraction < 1 and eps >= 0");
     return 0;
 }
 

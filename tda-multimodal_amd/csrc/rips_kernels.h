@@ -134,6 +134,125 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
         atomicMax(&rm[bj * TS + threadIdx.x - 64], rmax_j[threadIdx.x - 64]);
 }
 
+// ------------------------------------------------------------------ distance, D >= 32: FP64 MFMA Gram tiles
+// Same arithmetic as k_distance (sklearn pairwise.py:582-653: f64 Gram
+// products of the upcast rows, d = (-2 g_ij + |x_i|^2) + |x_j|^2 for i < j,
+// round to f32, clamp, sqrt), with the dot products on the matrix cores:
+// v_mfma_f64_16x16x4_f64.  Products of upcast f32 values are exact in f64, so
+// only the summation order differs from the scalar kernel (and from sklearn's
+// BLAS dgemm, whose order is its own): the f32 results agree within the
+// north_star bound, and almost always bit for bit.
+//
+// One workgroup = one 64x64 tile of one layer's matrix, upper-triangle tile
+// pairs only (bi <= bj, enumerated linearly: no idle lower-triangle blocks).
+// 4 waves, each a 32x32 quadrant as 2x2 MFMA tiles (4 independent f64x4
+// accumulators hide the MFMA latency).  K is staged through LDS in chunks of
+// kDmKC, upcast to f64, row-major with a row stride of kDmS = kDmKC + 2
+// doubles: an MFMA operand read (lane -> row lane & 15, k = lane >> 4) maps
+// each half-wave's 32 lanes to 32 distinct 8-byte bank pairs (row r, k:
+// slot 2r + k mod 32), so the ds_read_b64 is conflict-free; each thread
+// stages 4 consecutive k of one row (coalesced global reads, 16-B aligned
+// LDS writes).
+// The squared norms accumulate (sequential k, FMA: the oracle's order) in the
+// same pass from the LDS tile, threads 0-63 for the i rows, 64-127 for j.
+constexpr int kDmT = 64, kDmKC = 32, kDmS = kDmKC + 2;
+typedef double dm_d4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, int n, int D, float* __restrict__ dist,
+                                                       uint32_t* __restrict__ rowmax) {
+    __shared__ double xs[2][kDmT][kDmS];  // [i/j tile][row][k]
+    __shared__ double nrm[2][kDmT];
+    __shared__ uint32_t rmx[2][kDmT];
+    const int l = blockIdx.y;
+    const int nt = (n + kDmT - 1) / kDmT;
+    // linear upper-triangle tile index -> (bi, bj), bi <= bj
+    int p = blockIdx.x, bi = 0;
+    while (p >= nt - bi) p -= nt - bi, ++bi;
+    const int bj = bi + p;
+    const T* Xl = X + (size_t)l * n * D;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    dm_d4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = dm_d4{0.0, 0.0, 0.0, 0.0};
+    double nacc = 0.0;  // threads < 128: squared norm of row (tid & 63) of tile (tid >> 6)
+    if (tid < 2 * kDmT) rmx[tid >> 6][tid & 63] = 0;
+    for (int k0 = 0; k0 < D; k0 += kDmKC) {
+        const int kc = min(kDmKC, D - k0);
+        // stage: 2 tiles x 64 rows x kDmKC k, upcast; coalesced along k
+#pragma unroll
+        for (int e = tid; e < 2 * kDmT * kDmKC / 4; e += 256) {
+            const int t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
+            const int g = (t ? bj : bi) * kDmT + r;
+            const T* src = Xl + (size_t)g * D + k0 + c0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xs[t][r][c0 + q] = (g < n && c0 + q < kc) ? (double)src[q] : 0.0;
+        }
+        __syncthreads();
+        if (tid < 2 * kDmT)
+            for (int c = 0; c < kc; ++c) {
+                const double v = xs[tid >> 6][tid & 63][c];
+                nacc = fma(v, v, nacc);
+            }
+#pragma unroll
+        for (int ks = 0; ks < kDmKC; ks += 4) {
+            const int k = ks + (lane >> 4);
+            double av[2], bv[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) av[a] = xs[0][wr * 32 + a * 16 + (lane & 15)][k];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) bv[b] = xs[1][wc * 32 + b * 16 + (lane & 15)][k];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    if (tid < 2 * kDmT) nrm[tid >> 6][tid & 63] = nacc;
+    __syncthreads();
+    float* Dl = dist + (size_t)l * n * n;
+    // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int ri = wr * 32 + a * 16 + (lane >> 4) + 4 * r, cj = wc * 32 + b * 16 + (lane & 15);
+                const int i = bi * kDmT + ri, j = bj * kDmT + cj;
+                if (i >= n || j >= n || j < i) continue;
+                if (i == j) {
+                    Dl[(size_t)i * n + i] = 0.0f;
+                    continue;
+                }
+                double d = (-2.0 * acc[a][b][r] + nrm[0][ri]) + nrm[1][cj];
+                float f;
+                if constexpr (sizeof(T) == 4) {
+                    f = (float)d;
+                    f = (f != f) ? f : fmaxf(f, 0.0f);
+                    f = sqrt_rn_f32(f);
+                } else {
+                    d = (d != d) ? d : fmax(d, 0.0);
+                    f = (float)__dsqrt_rn(d);
+                }
+                f = f + 0.0f;
+                Dl[(size_t)i * n + j] = f;
+                Dl[(size_t)j * n + i] = f;
+                atomicMax(&rmx[0][ri], __float_as_uint(f));
+                atomicMax(&rmx[1][cj], __float_as_uint(f));
+            }
+    __syncthreads();
+    uint32_t* rm = rowmax + (size_t)l * n;
+    if (tid < 2 * kDmT) {
+        const int t = tid >> 6, r = tid & 63, g = (t ? bj : bi) * kDmT + r;
+        if (g < n && rmx[t][r]) atomicMax(&rm[g], rmx[t][r]);
+    }
+}
+
 // row maxima of a square distance matrix (distance-matrix inputs): one wave per row
 __global__ __launch_bounds__(256) void k_rowmax(const float* __restrict__ dist, int n, uint32_t* __restrict__ rowmax) {
     const int l = blockIdx.y, w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, ln = threadIdx.x & 63;
@@ -895,6 +1014,131 @@ __global__ __launch_bounds__(kSilT) void k_silhouette(const float* __restrict__ 
         double m = 0.0;
         for (int w = 0; w < kSilT / 64; ++w) m += part[w];
         out[(size_t)l * S + s] = m / (double)n;
+    }
+}
+
+// ---------------------------------------------------------------- TwoNN
+// Intrinsic dimension of each layer's cloud on its distance matrix: the
+// reference's compute_intrinsic_dimensionality (metrics.py:113-208), which
+// runs torch.cdist (:143), diagonal -> inf (:146), topk(2, smallest) (:149),
+// mu = r2 / r1 where both exceed eps (:154-155), keeps the finite mu (:163),
+// sorts them and drops the largest discard fraction (:169-172,
+// n_keep = max(int(len * (1 - discard)), 5)), F_emp = i / n_samples over ALL
+// samples (:180-181), x = log(mu + eps), y = -log(1 - F + eps) (:184-187),
+// rejects var(x) or var(y) < eps (:190), slope = sum(xy) / sum(xx) (:195-201)
+// and returns it iff finite and in (0, 1000) (:204), else NaN.
+// Elementwise steps are f32 as in the reference; the sums and variances
+// accumulate in f64 and round to f32 (the reference's f32 reductions have
+// their own order), which is where the test tolerance comes from.
+// One 1024-thread block per layer: a wave per row finds the two smallest
+// off-diagonal distances (lane-strided, coalesced, DPP top-2 merge), the
+// finite ratios go to LDS, a bitonic sort orders them, block reductions do
+// the regression.  LDS: next_pow2(n) floats (n <= 8192).
+constexpr int kTnT = 1024;
+__device__ __forceinline__ void top2_insert(float v, float& a, float& b) {
+    if (v < a) {
+        b = a;
+        a = v;
+    } else if (v < b) {
+        b = v;
+    }
+}
+__device__ __forceinline__ double block_sum_f64(double v, double* part) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+    return s;
+}
+__global__ __launch_bounds__(kTnT) void k_twonn(const float* __restrict__ dist, int n, double discard, float eps, int pw2,
+                                                float* __restrict__ out) {
+    extern __shared__ __align__(16) unsigned char tn_lds[];
+    float* mu = (float*)tn_lds;  // [pw2]
+    __shared__ int cnt;
+    __shared__ double part[kTnT / 64];
+    const int l = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const float* D = dist + (size_t)l * n * n;
+    if (n <= 5) {  // metrics.py:136-137
+        if (t == 0) out[l] = __int_as_float(0x7fc00000);
+        return;
+    }
+    if (t == 0) cnt = 0;
+    __syncthreads();
+    for (int i = wv; i < n; i += kTnT / 64) {
+        float a = INFINITY, b = INFINITY;
+        const float* row = D + (size_t)i * n;
+        for (int j = lane; j < n; j += 64)
+            if (j != i) top2_insert(row[j], a, b);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float oa = __shfl_xor(a, o, 64), ob = __shfl_xor(b, o, 64);
+            top2_insert(oa, a, b);
+            top2_insert(ob, a, b);
+        }
+        if (lane == 0) {
+            const float m = (a > eps && b > eps) ? b / a : INFINITY;
+            if (isfinite(m)) mu[atomicAdd(&cnt, 1)] = m;
+        }
+    }
+    __syncthreads();
+    const int v = cnt;
+    if (v < 5) {  // :165-166
+        if (t == 0) out[l] = __int_as_float(0x7fc00000);
+        return;
+    }
+    for (int i = v + t; i < pw2; i += kTnT) mu[i] = INFINITY;
+    __syncthreads();
+    // bitonic sort, ascending
+    for (int k = 2; k <= pw2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < pw2; i += kTnT) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const float x = mu[i], y = mu[p];
+                    if (((i & k) == 0) == (x > y)) {
+                        mu[i] = y;
+                        mu[p] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    int keep = (int)((double)v * (1.0 - discard));  // Python float arithmetic (:170)
+    keep = keep < 5 ? 5 : (keep > v ? v : keep);
+    const float fn = (float)n;
+    double sx = 0.0, sy = 0.0;
+    for (int i = t; i < keep; i += kTnT) {
+        const float x = logf(mu[i] + eps);
+        const float f = (float)(i + 1) / fn;
+        const float y = -logf((1.0f - f) + eps);
+        sx += (double)x;
+        sy += (double)y;
+    }
+    const double mx = block_sum_f64(sx, part) / keep, my = block_sum_f64(sy, part) / keep;
+    double vx = 0.0, vy = 0.0, sxy = 0.0, sxx = 0.0;
+    for (int i = t; i < keep; i += kTnT) {
+        const float x = logf(mu[i] + eps);
+        const float f = (float)(i + 1) / fn;
+        const float y = -logf((1.0f - f) + eps);
+        vx += ((double)x - mx) * ((double)x - mx);
+        vy += ((double)y - my) * ((double)y - my);
+        sxy += (double)(x * y);
+        sxx += (double)(x * x);
+    }
+    const float varx = (float)(block_sum_f64(vx, part) / (keep - 1));
+    const float vary = (float)(block_sum_f64(vy, part) / (keep - 1));
+    const float num = (float)block_sum_f64(sxy, part);
+    const float den = (float)block_sum_f64(sxx, part);
+    if (t == 0) {
+        float r = __int_as_float(0x7fc00000);
+        if (!(varx < eps || vary < eps) && !(fabsf(den) < eps)) {
+            const float slope = num / den;
+            if (isfinite(slope) && slope > 0.0f && slope < 1000.0f) r = slope;
+        }
+        out[l] = r;
     }
 }
 

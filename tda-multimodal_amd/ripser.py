@@ -26,7 +26,7 @@ from . import _lib
 class _Batch:
     """Host copies of one batched call's outputs; LayerResults are views into it."""
 
-    __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist", "sil")
+    __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist", "sil", "tn")
 
 
 class LayerResult:
@@ -97,6 +97,12 @@ class LayerResult:
         return [] if self._b.sil is None else self._b.sil[self._l].tolist()
 
     @property
+    def twonn(self) -> float:
+        """TwoNN intrinsic dimension of the layer's cloud (``ripser_batch(twonn=True)``;
+        metrics.py:113-208 semantics, NaN where the reference gives NaN), or None."""
+        return None if self._b.tn is None else float(self._b.tn[self._l])
+
+    @property
     def dist(self):
         return None if self._b.dist is None else self._b.dist[self._l]
 
@@ -133,6 +139,7 @@ def _unpack(res_p, want_dist: bool, n_sets: int = 0) -> tuple[list, dict]:
     b.ne = _arr(r.num_edges, L, np.int64)
     b.dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N) if want_dist and bool(r.dist) else None
     b.sil = None
+    b.tn = _arr(r.twonn, L, np.float32) if bool(r.twonn) else None
     if bool(r.silhouette):
         b.sil = _arr(r.silhouette, L * n_sets, np.float64).reshape(L, n_sets)
     out = [LayerResult(b, l) for l in range(L)]
@@ -190,7 +197,7 @@ def encode_labels(label_sets, n: int) -> np.ndarray:
 
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
                  want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None,
-                 stage_serial: bool = False):
+                 stage_serial: bool = False, twonn: bool = False, discard_fraction: float = 0.1, eps: float = 1e-10):
     """Persistence of L layers in one call.
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
@@ -203,6 +210,9 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     layer); each layer's ``silhouette`` then holds sklearn's
     ``silhouette_score(cloud, labels)`` per set, computed on the GPU from the
     same distance matrix (debug_tda_pipeline.py:117-118).
+    twonn: also estimate each layer's TwoNN intrinsic dimension on the same
+    distance matrix (metrics.py:113-208, ``discard_fraction`` / ``eps`` as
+    there); read it from ``LayerResult.twonn``.
     """
     _check_common(maxdim, 2, False, None, "euclidean")
     a = _lib.RipsArgs()
@@ -250,6 +260,10 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
         lab = encode_labels(labels, N)
         a.labels = lab.ctypes.data
         a.n_label_sets = lab.shape[0]
+    if twonn:
+        a.want_twonn = 1
+        a.twonn_discard = float(discard_fraction)
+        a.twonn_eps = float(eps)
     out, info = _call_batch(a, want_dist)
     return (out, info) if return_time else out
 

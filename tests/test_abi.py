@@ -33,7 +33,7 @@ def test_library_is_gfx950_code_object(built_lib):
 
 def test_version_and_no_device_here(pkg, built_lib):
     L = pkg.lib()
-    assert L.tda_version() == 2  # ABI 2: silhouette labels / scores appended to args / result
+    assert L.tda_version() == 3  # ABI 3: TwoNN request / result appended to args / result (2: silhouettes)
     assert L.tda_device_ok(12345) == 0
 
 
@@ -83,11 +83,13 @@ def test_ctypes_structs_match_header_layout(pkg, tmp_path):
     src = tmp_path / "layout.c"
     src.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "tda_rips.h"\n'
-        'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(tda_rips_args), offsetof(tda_rips_args, labels),'
-        ' offsetof(tda_rips_args, n_label_sets), sizeof(tda_rips_result), offsetof(tda_rips_result, silhouette));return 0;}\n')
+        'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tda_rips_args), offsetof(tda_rips_args, labels),'
+        ' offsetof(tda_rips_args, n_label_sets), sizeof(tda_rips_result), offsetof(tda_rips_result, silhouette),'
+        ' offsetof(tda_rips_args, twonn_discard), offsetof(tda_rips_result, twonn));return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", lb.INCLUDE, str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [ctypes.sizeof(lb.RipsArgs), lb.RipsArgs.labels.offset, lb.RipsArgs.n_label_sets.offset,
-            ctypes.sizeof(lb.RipsResult), lb.RipsResult.silhouette.offset]
+            ctypes.sizeof(lb.RipsResult), lb.RipsResult.silhouette.offset, lb.RipsArgs.twonn_discard.offset,
+            lb.RipsResult.twonn.offset]
     assert got == want

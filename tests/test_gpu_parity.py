@@ -98,10 +98,10 @@ def test_grid144_maxdim2_vs_oracle(gpu, oracle, monkeypatch, reduce_kernel):
     compacted scans, and the 1024-thread radix-heap kernel) are forced via
     TDA_REDUCE and must agree bit-for-bit with the oracle."""
     monkeypatch.setenv("TDA_REDUCE", reduce_kernel)
-    X = gpu.synthetic.sweep144(3)
+    X = gpu.synthetic.sweep144(8)
     res = gpu.ripser_batch(X, maxdim=2)
     orc = oracle.rips_batch_f32(X, 2)
-    for l in range(3):
+    for l in range(8):
         assert_same(res[l], orc[l], 2, f"grid{l}")
 
 
@@ -316,6 +316,110 @@ def test_torus2048_maxdim1_invariants(gpu):
     assert np.all(np.diff(births) <= 0)  # emission order: decreasing birth
     pers = np.sort(a.dgms[1][:, 1] - a.dgms[1][:, 0])[::-1]
     assert pers[1] > 2.0 * pers[2]
+
+
+def _large_golden():
+    return np.load(os.path.join(GOLDEN, "large_cases.npz"))
+
+
+def assert_same_golden(res, z, name, l, maxdim):
+    """One layer against the committed oracle fixture (make_golden_large.py)."""
+    assert np.float32(res.thresh) == z[f"{name}__thresh"][l], (name, l)
+    assert res.num_edges == int(z[f"{name}__num_edges"][l]), (name, l)
+    for d in range(maxdim + 1):
+        bd, idx = z[f"{name}__l{l}_d{d}__bd"], z[f"{name}__l{l}_d{d}__idx"]
+        exp = [(float(b), float(e), int(bi), int(di)) for (b, e), (bi, di) in zip(bd, idx)]
+        assert _pairs(res, d) == exp, (name, l, d)
+        assert res.n_all_pairs[d] == int(z[f"{name}__n_all_pairs"][l][d]), (name, l, d)
+        assert res.checksum[d] == int(z[f"{name}__checksum"][l][d]), (name, l, d)
+
+
+@pytest.mark.parametrize("name", ["grid144", "torus1024", "torus2048"])
+def test_full_workload_vs_committed_oracle(gpu, name):
+    """Every BASELINE config's full workload against the committed oracle run:
+    configs[4] grid144 (all 32 layers, H0-H2), configs[3] torus1024 (C4) and
+    torus2048 (top of the north_star N range, H0-H1)."""
+    z = _large_golden()
+    X, md = z[f"{name}__X"], int(z[f"{name}__maxdim"])
+    res = gpu.ripser_batch(X, maxdim=md)
+    for l in range(X.shape[0]):
+        assert_same_golden(res[l], z, name, l, md)
+
+
+def test_distance_high_dim_vs_sklearn(gpu):
+    """D = 64 and 4096 (raw hidden size) against sklearn's f32-upcast
+    pairwise_distances.  sklearn's Gram products go through BLAS dgemm, whose
+    summation order is not ours, so the bound is north_star's 1e-5 (relative to
+    the distance, i.e. about one f32 ulp here); most entries are still
+    bit-identical after the f32 rounding."""
+    from golden.make_golden_large import HD_CASES, hd_cloud, sha
+
+    z = np.load(os.path.join(GOLDEN, "dist_hd.npz"))
+    for name, (n, d, seed) in HD_CASES.items():
+        X = hd_cloud(n, d, seed)
+        assert sha(X) == str(z[name + "__sha"]), f"{name}: input generator changed"
+        ref = z[name + "__condensed"]
+        res = gpu.ripser_batch(X[None], maxdim=0, want_dist=True)[0]
+        got = res.dist[np.triu_indices(n, 1)]
+        err = np.abs(got.astype(np.float64) - ref.astype(np.float64)) / np.maximum(1.0, ref.astype(np.float64))
+        assert err.max() <= TOL, (name, float(err.max()))
+        assert np.mean(got.view(np.uint32) == ref.view(np.uint32)) > 0.9, name
+        assert np.array_equal(res.dist, res.dist.T) and np.all(np.diag(res.dist) == 0)
+
+
+@pytest.mark.parametrize("dist_kernel", ["auto", "scalar", "mfma"])
+def test_distance_kernels_agree_with_oracle(gpu, oracle, monkeypatch, dist_kernel):
+    """The scalar FP64 kernel and the FP64-MFMA Gram kernel (forced both ways
+    with TDA_DIST) on ragged N (tile edges) and D (K-chunk edges), f32 and f64
+    inputs: within 1e-5 of the oracle, bit-exact on most entries; persistence
+    on top of them bit-exact where the distances are."""
+    monkeypatch.setenv("TDA_DIST", dist_kernel)
+    rng = np.random.default_rng(17)
+    for n, d in ((5, 33), (63, 64), (65, 100), (130, 37), (200, 3)):
+        X = (rng.standard_normal((2, n, d)) * 3 + 1).astype(np.float32)
+        for Xin in (X, X.astype(np.float64)):
+            res = gpu.ripser_batch(Xin, maxdim=1, want_dist=True)
+            for l in range(2):
+                ref = oracle.distances(Xin[l]).astype(np.float64)
+                got = res[l].dist.astype(np.float64)
+                assert np.max(np.abs(got - ref) / np.maximum(1.0, ref)) <= TOL, (n, d)
+                assert np.mean(got == ref) > 0.9, (n, d)
+                assert np.array_equal(res[l].dist, res[l].dist.T) and np.all(np.diag(res[l].dist) == 0)
+                if np.array_equal(got, ref):
+                    assert_same(res[l], oracle.rips_dm(res[l].dist, 1), 1, f"n{n}d{d}")
+
+
+TWONN_TOL = 1e-4  # relative: the reference runs torch.cdist's f32 Gram form and f32 sums; we use f64 sums
+
+
+def test_twonn_vs_reference_goldens_and_oracle(gpu):
+    """TwoNN intrinsic dimension (metrics.py:113-208) from the GPU distance
+    matrices: within TWONN_TOL of the reference's own outputs
+    (tests/golden/twonn.json), NaN exactly where the reference gives NaN, and
+    within 1e-5 of the restatement (oracle/twonn.py) on the same GPU distances."""
+    import torch
+
+    from golden.make_golden_twonn import sha, twonn_inputs
+
+    from oracle import twonn
+
+    with open(os.path.join(GOLDEN, "twonn.json")) as f:
+        g = json.load(f)
+    for name, (X, disc, eps) in twonn_inputs().items():
+        assert g[name]["sha"] == sha(X), name
+        want = g[name]["twonn"]
+        got = gpu.compute_intrinsic_dimensionality(torch.from_numpy(X).to("cuda:0"), disc, eps)
+        assert got.device.type == "cuda" and got.dtype == torch.float32 and got.shape == (X.shape[0],)
+        got = got.cpu().numpy()
+        if X.shape[1] > 5:
+            res = gpu.ripser_batch(X, maxdim=0, want_dist=True, twonn=True, discard_fraction=disc, eps=eps)
+        for b, w in enumerate(want):
+            if w is None:
+                assert np.isnan(got[b]), (name, b)
+                continue
+            assert abs(got[b] - w) <= TWONN_TOL * abs(w), (name, b, float(got[b]), w)
+            o = twonn.twonn_from_dist(res[b].dist, disc, eps)
+            assert abs(res[b].twonn - o) <= 1e-5 * abs(o), (name, b)
 
 
 @pytest.mark.parametrize("n,maxdim", [(180, 1), (324, 2)])

@@ -134,3 +134,61 @@ def test_oracle_silhouette_matches_sklearn_goldens(oracle, ref_clouds):
     for c in g["synthetic"]:
         D = oracle.distances(np.asarray(c["X"], dtype=np.float32))
         assert abs(oracle.silhouette(D, c["labels"]) - c["score"]) < 1e-6, c["name"]
+
+
+def test_large_fixtures_match_generators_and_oracle(oracle):
+    """tests/golden/large_cases.npz (made by make_golden_large.py): its inputs are
+    what the synthetic generators produce, and the oracle still reproduces the
+    torus1024 (C4) and the first grid144 layers' outputs."""
+    syn = load_pkg().synthetic
+    z = np.load(os.path.join(GOLDEN, "large_cases.npz"))
+    assert np.array_equal(z["grid144__X"], syn.sweep144(32))
+    assert np.array_equal(z["torus1024__X"][0], syn.torus(1024, seed=0))
+    assert np.array_equal(z["torus2048__X"][0], syn.torus(2048, seed=3))
+    for name, X, md in (("torus1024", z["torus1024__X"], 1), ("grid144", z["grid144__X"][:4], 2)):
+        res = oracle.rips_batch_f32(X, md)
+        for l, r in enumerate(res):
+            assert r["checksum"] == [int(c) for c in z[f"{name}__checksum"][l]], (name, l)
+            for d in range(md + 1):
+                got = np.stack([r["birth_idx"][d], r["death_idx"][d]], 1).reshape(-1, 2)
+                assert np.array_equal(got, z[f"{name}__l{l}_d{d}__idx"]), (name, l, d)
+                assert np.array_equal(r["dgms"][d].astype(np.float32).reshape(-1, 2), z[f"{name}__l{l}_d{d}__bd"])
+
+
+def test_oracle_distance_high_dim_within_tolerance_of_sklearn(oracle):
+    """D = 64 / 4096: sklearn sums the Gram products through BLAS dgemm, the
+    oracle sequentially; after rounding to f32 they agree within north_star's
+    1e-5 (relative) and mostly bit for bit."""
+    from golden.make_golden_large import HD_CASES, hd_cloud, sha
+
+    z = np.load(os.path.join(GOLDEN, "dist_hd.npz"))
+    for name, (n, d, seed) in HD_CASES.items():
+        X = hd_cloud(n, d, seed)
+        assert sha(X) == str(z[name + "__sha"])
+        ref = z[name + "__condensed"].astype(np.float64)
+        got = oracle.distances(X)[np.triu_indices(n, 1)]
+        err = np.abs(got - ref) / np.maximum(1.0, ref)
+        assert err.max() <= 1e-5, (name, err.max())
+
+
+TWONN_TOL = 1e-4  # relative; the reference sums in f32 on torch.cdist's f32 Gram form, the restatement in f64
+
+
+def test_twonn_restatement_matches_reference_goldens(oracle):
+    """oracle/twonn.py (restatement of metrics.py:113-208 on a given distance
+    matrix) on the oracle's distances against the reference's own outputs
+    (tests/golden/twonn.json, made by importing /root/reference/metrics.py)."""
+    from golden.make_golden_twonn import sha, twonn_inputs
+
+    from oracle import twonn
+
+    with open(os.path.join(GOLDEN, "twonn.json")) as f:
+        g = json.load(f)
+    for name, (X, disc, eps) in twonn_inputs().items():
+        assert g[name]["sha"] == sha(X), name
+        for b, want in enumerate(g[name]["twonn"]):
+            got = twonn.twonn_from_dist(oracle.distances(X[b]), disc, eps)
+            if want is None:
+                assert np.isnan(got), (name, b)
+            else:
+                assert abs(got - want) <= TWONN_TOL * abs(want), (name, b, got, want)
