@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (vendor spec; v_mfma_f64_16x16x4_f64)
 METRIC = "layers/sec (pairwise-dist + VR persistence H0-H2) at 1/2/4/8 MI355X"
 
 WORKLOADS = {
@@ -41,13 +42,18 @@ WORKLOADS = {
     "sweep48": (32, 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2", 50, 5),
     "grid144": (32, 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2", 10, 2),
     "torus1024": (1, 1, "S1xS1 torus N=1024 (configs[3]), D=3, H0-H1", 5, 2),
+    # raw hidden states (no UMAP): distance on the FP64 matrix cores + TwoNN + H0
+    "raw4096": (32, 0, "32 layers x 144 tokens x 4096 raw hidden-state features: distance (FP64 MFMA) + H0 + TwoNN "
+                       "intrinsic dimension (metrics.py:113-208)", 20, 3),
 }
 DATA = {
     "sweep48": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
     "grid144": "synthetic: 12x12 grid on the torus + N(0, 0.02^2) + random rotation per layer",
     "torus1024": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 0",
+    "raw4096": "synthetic: activation-like f32 clouds (heavy-tailed feature scales, offsets, outlier features)",
 }
-NPOINTS = {"sweep48": 48, "grid144": 144, "torus1024": 1024}
+NPOINTS = {"sweep48": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
+CALL_KW = {"raw4096": {"twonn": True}}
 
 
 def algo_bytes_per_layer(n: int, d: int, maxdim: int) -> int:
@@ -64,6 +70,8 @@ def make_workload(name: str, layers: int | None = None):
         return syn.sweep144(L)
     if name == "torus1024":
         return syn.torus(1024)[None].repeat(L, 0)
+    if name == "raw4096":
+        return syn.activations(L, 144, 4096)
     raise ValueError(name)
 
 
@@ -81,7 +89,13 @@ def _cpu_layers(task):
     X = _WORKER_CACHE[name]
     oracle.lib()
     if hi > lo:
-        oracle.rips_batch_f32(X[lo:hi], maxdim)
+        if name in CALL_KW:  # distances + TwoNN restatement (H0 is negligible next to them)
+            from oracle import twonn
+
+            for x in X[lo:hi]:
+                twonn.twonn_from_dist(oracle.distances(x))
+        else:
+            oracle.rips_batch_f32(X[lo:hi], maxdim)
     return hi - lo
 
 
@@ -114,10 +128,11 @@ def cpu_baseline(pool, P: int, name: str, X, maxdim: int, seconds: float) -> dic
 
     oracle.lib()
     L = X.shape[0]
+    _WORKER_CACHE[name] = X
     done, t1 = 0, 0.0
     t0 = time.perf_counter()
     while t1 < seconds and done < 100000:
-        oracle.rips_batch_f32(X[done % L:done % L + 1], maxdim)
+        _cpu_layers((name, done % L, done % L + 1, maxdim))
         done += 1
         t1 = time.perf_counter() - t0
     one = done / t1
@@ -140,12 +155,13 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     X = torch.from_numpy(X_host).to(dev)  # resident in HBM before the timed region
     torch.cuda.synchronize()
     dev_ms = []
+    kw = CALL_KW.get(name, {})
     for _ in range(warmup):
-        pkg.ripser_batch(X, maxdim=maxdim)
+        pkg.ripser_batch(X, maxdim=maxdim, **kw)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        _, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True)
+        _, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, **kw)
         dev_ms.append(info["device_ms"])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -154,7 +170,7 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     # after the timed region; the dominant kernel has the largest mean
     acc: dict = {}
     for _ in range(max(1, min(steps, 10))):
-        _, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, stage_times=True, stage_serial=True)
+        _, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, stage_times=True, stage_serial=True, **kw)
         for k, ms in info["stages"]:
             acc.setdefault(k, []).append(ms)
     stages = {k: sum(v) / len(v) for k, v in acc.items()}
@@ -162,6 +178,11 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     dom = max(kern, key=kern.get)
     bpl = algo_bytes_per_layer(n, d, maxdim)
     achieved = bpl * L / (kern[dom] * 1e-3) / 1e9
+    bound, peak, unit, per_layer = "hbm", HBM_PEAK_GBS, "GB/s", {"algo_bytes_per_layer": bpl}
+    if dom == "k_distance_mfma":  # 2 N^2 D FP64 FLOPs per layer (Gram) against the FP64 MFMA peak
+        fpl = 2 * n * n * d
+        achieved = fpl * L / (kern[dom] * 1e-3) / 1e12
+        bound, peak, unit, per_layer = "mfma", FP64_MFMA_PEAK_TFS, "TFLOP/s", {"algo_flops_per_layer": fpl}
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
     if os.path.exists(pmc_path):
@@ -171,8 +192,8 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
         "value": L * steps / el, "unit": "layers/s", "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warmup,
         "device_ms_per_step": sum(dev_ms) / len(dev_ms), "X_host": X_host, "maxdim": maxdim,
         "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algo_bytes_per_layer": bpl,
+        "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
+                     "frac": achieved / peak, "traffic": traffic, **per_layer,
                      "layers_per_launch": L, "kernel_avg_ms": kern[dom],
                      "kernel_timing": "HIP events around each kernel on its stream, all stages serialised on one "
                                       "stream, after the timed region (same batch)"},
@@ -187,7 +208,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
-    ap.add_argument("--extra", default="grid144,torus1024",
+    ap.add_argument("--extra", default="grid144,torus1024,raw4096",
                     help="secondary workloads measured at N=1 (comma list, '' for none)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")

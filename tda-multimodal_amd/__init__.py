@@ -10,7 +10,8 @@ import sys as _sys
 from . import distributed, metrics, synthetic  # noqa: F401
 from .metrics import compute_intrinsic_dimensionality  # noqa: F401
 from ._lib import EXPORTS, LIB_PATH, build, lib  # noqa: F401
-from .pipeline import get_max_persistence, get_persistence, layer_record, peak_layer, run_sweep, write_summary_stats  # noqa: F401
+from .pipeline import (get_max_persistence, get_persistence, layer_record, layer_record_adversarial, peak_layer,  # noqa: F401
+                       run_adversarial_condition, run_sweep, write_layer_stats, write_summary_stats)
 from .ripser import LayerResult, persistence_pairs, ripser, ripser_batch, rips_dm, silhouette_score  # noqa: F401
 
 _sys.modules.setdefault("tda_multimodal_amd", _sys.modules[__name__])
@@ -24,6 +25,8 @@ __all__ = [
     "get_persistence",
     "get_max_persistence",
     "layer_record",
+    "layer_record_adversarial",
+    "run_adversarial_condition",
     "run_sweep",
     "write_summary_stats",
     "peak_layer",

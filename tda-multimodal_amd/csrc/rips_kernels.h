@@ -180,20 +180,32 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
         for (int b = 0; b < 2; ++b) acc[a][b] = dm_d4{0.0, 0.0, 0.0, 0.0};
     double nacc = 0.0;  // threads < 128: squared norm of row (tid & 63) of tile (tid >> 6)
     if (tid < 2 * kDmT) rmx[tid >> 6][tid & 63] = 0;
-    for (int k0 = 0; k0 < D; k0 += kDmKC) {
+    // register double buffer: chunk k0 + kDmKC is in flight while chunk k0 feeds the MFMAs
+    T pre[4][4];
+    auto load = [&](int k0) {
         const int kc = min(kDmKC, D - k0);
-        // stage: 2 tiles x 64 rows x kDmKC k, upcast; coalesced along k
 #pragma unroll
-        for (int e = tid; e < 2 * kDmT * kDmKC / 4; e += 256) {
-            const int t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
+        for (int u = 0; u < 4; ++u) {  // 2 tiles x 64 rows x kDmKC / 4 groups of 4 consecutive k
+            const int e = tid + 256 * u, t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
             const int g = (t ? bj : bi) * kDmT + r;
             const T* src = Xl + (size_t)g * D + k0 + c0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) xs[t][r][c0 + q] = (g < n && c0 + q < kc) ? (double)src[q] : 0.0;
+            for (int q = 0; q < 4; ++q) pre[u][q] = (g < n && c0 + q < kc) ? src[q] : (T)0;
+        }
+    };
+    load(0);
+    for (int k0 = 0; k0 < D; k0 += kDmKC) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = tid + 256 * u, t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xs[t][r][c0 + q] = (double)pre[u][q];
         }
         __syncthreads();
-        if (tid < 2 * kDmT)
-            for (int c = 0; c < kc; ++c) {
+        if (k0 + kDmKC < D) load(k0 + kDmKC);
+        if (tid < 2 * kDmT)  // zero padding adds exact zeros
+#pragma unroll 8
+            for (int c = 0; c < kDmKC; ++c) {
                 const double v = xs[tid >> 6][tid & 63][c];
                 nacc = fma(v, v, nacc);
             }

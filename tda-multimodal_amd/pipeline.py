@@ -15,6 +15,12 @@ sweep produces records identical to ``tda-output/summary_stats.json``:
   scores (:117-118) come from the same call's distance matrices.
 * ``write_summary_stats``  -- debug_tda_pipeline.py:154-156 (json, indent=2).
 * ``peak_layer``           -- debug_tda_pipeline.py:195 (argmax of the shape score).
+* ``layer_record_adversarial`` / ``run_adversarial_condition`` -- the
+  adversarial experiment's per-condition loop
+  (experiments/adversarial_compositional_binding/analyze_adversarial_tda.py:
+  81-122, minus UMAP and plotting): its record keys (:113-122) with four
+  silhouettes (image / text x color / shape labels, :108-111) from one
+  batched call, and ``write_layer_stats`` (:131-134).
 """
 from __future__ import annotations
 
@@ -91,6 +97,41 @@ def run_sweep(clouds, maxdim: int = 1, thresh: float = np.inf, layer_ids=None, d
             col = sil[q]
         recs.append(layer_record(int(i), r.dgms, shp, col))
     return recs, res
+
+
+ADVERSARIAL_LABELS = ("img_color", "img_shape", "txt_color", "txt_shape")
+
+
+def layer_record_adversarial(layer: int, dgms: list, silhouettes) -> dict:
+    """analyze_adversarial_tda.py:102-122: the per-layer record of the
+    adversarial experiment's layer_stats.json (key order as written there).
+    silhouettes: the four scores in ADVERSARIAL_LABELS order (:108-111)."""
+    _, max_h0 = get_persistence(dgms[0])
+    h1_pers, max_h1 = get_persistence(dgms[1])
+    rec = {
+        "layer": layer,
+        "n_h1_features": len(h1_pers),
+        "max_h1_persistence": float(max_h1),
+        "max_h0_persistence": float(max_h0),
+    }
+    for name, v in zip(ADVERSARIAL_LABELS, silhouettes):
+        rec[f"silhouette_{name}"] = float(v)
+    return rec
+
+
+def run_adversarial_condition(clouds, img_colors, img_shapes, txt_colors, txt_shapes, maxdim: int = 1,
+                              device: int = 0):
+    """One condition of analyze_adversarial_tda.py:60-134 for a stack of
+    per-layer clouds (L, N, D): persistence and the four silhouette scores of
+    every layer in ONE batched call (the reference calls ripser once and
+    silhouette_score four times per layer, :100-111).  Returns (records, results)."""
+    res = ripser_batch(clouds, maxdim=maxdim, device=device, labels=[img_colors, img_shapes, txt_colors, txt_shapes])
+    return [layer_record_adversarial(i, r.dgms, r.silhouette) for i, r in enumerate(res)], res
+
+
+def write_layer_stats(path: str, records: list) -> None:
+    """analyze_adversarial_tda.py:131-134: ``json.dump(all_stats, f, indent=2)``."""
+    write_summary_stats(path, records)
 
 
 def write_summary_stats(path: str, records: list) -> None:

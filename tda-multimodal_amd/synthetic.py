@@ -57,3 +57,17 @@ def grid144(l: int) -> np.ndarray:
 
 def sweep144(n_layers: int = 32) -> np.ndarray:
     return np.stack([grid144(l) for l in range(n_layers)])
+
+
+def activations(n_layers: int = 32, n: int = 144, d: int = 4096, seed: int = 0) -> np.ndarray:
+    """Raw hidden-state-like clouds (n tokens x d features per layer, the
+    Qwen-VL hidden size analyze_adversarial_tda.py:77 stacks): heavy-tailed
+    per-feature scales, a shared offset and a few outlier features."""
+    rng = np.random.default_rng(seed)
+    out = np.empty((n_layers, n, d), dtype=np.float32)
+    for l in range(n_layers):
+        scale = np.exp(rng.normal(0.0, 1.0, d))
+        X = rng.standard_normal((n, d)) * scale + rng.normal(0.0, 2.0, d)
+        X[:, rng.integers(0, d, max(1, d // 64))] *= 20.0
+        out[l] = X
+    return out

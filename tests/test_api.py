@@ -2,6 +2,8 @@
 import numpy as np
 import pytest
 
+from conftest import load_pkg
+
 
 def test_ripser_signature_errors_match_reference_behaviour(pkg):
     X = np.random.default_rng(0).standard_normal((10, 3)).astype(np.float32)
@@ -137,3 +139,19 @@ def test_summary_stats_writer_and_peak_layer(pkg, tmp_path):
     pipe = __import__("importlib").import_module("tda-multimodal_amd.pipeline")
     back = pipe.unpack_record(pipe.pack_record(recs[1], 1), 1)
     assert back["silhouette_shape"] == 0.7 and back["silhouette_color"] == -0.7
+
+
+def test_adversarial_record_keys_and_values(oracle):
+    """analyze_adversarial_tda.py:113-122: key order, no all_h1 list, no
+    n_h0_features; values from get_persistence of the oracle's diagrams."""
+    pipe = load_pkg().pipeline
+    X = load_pkg().synthetic.torus(60, seed=2)
+    o = oracle.rips(X, maxdim=1)
+    rec = pipe.layer_record_adversarial(3, o["dgms"], [0.1, 0.2, 0.3, 0.4])
+    assert list(rec) == ["layer", "n_h1_features", "max_h1_persistence", "max_h0_persistence", "silhouette_img_color",
+                         "silhouette_img_shape", "silhouette_txt_color", "silhouette_txt_shape"]
+    h1 = o["dgms"][1]
+    fin = np.isfinite(h1[:, 1])
+    assert rec["n_h1_features"] == int(fin.sum())
+    assert rec["max_h1_persistence"] == float(np.max(h1[fin, 1] - h1[fin, 0]))
+    assert rec["silhouette_txt_shape"] == 0.4

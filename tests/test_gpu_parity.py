@@ -442,3 +442,27 @@ def test_silhouette_graph_replay_with_different_class_counts(gpu, oracle):
     for lab in (np.arange(48) % 2, np.arange(48) % 6, np.arange(48) // 24, np.arange(48) % 6):
         got = gpu.silhouette_score(X, lab)
         assert abs(got - oracle.silhouette(Dm, lab)) < 1e-9, int(lab.max()) + 1
+
+
+@pytest.mark.parametrize("n", [180, 324])
+def test_adversarial_condition_records(gpu, oracle, n):
+    """analyze_adversarial_tda.py:81-122 at the experiment's point counts: the
+    record of every layer from one batched call with the four label sets
+    (image / text x color / shape) equals the record built from the oracle's
+    diagrams and silhouettes."""
+    rng = np.random.default_rng(n)
+    X = np.stack([gpu.synthetic.torus(n, seed=n + l) for l in range(3)])
+    colors, shapes = np.array(["red", "green", "blue", "cyan", "pink", "gray"]), np.arange(6)
+    img_c, img_s = colors[rng.integers(0, 6, n)], shapes[rng.integers(0, 6, n)]
+    txt_c, txt_s = colors[rng.integers(0, 6, n)], shapes[rng.integers(0, 6, n)]
+    recs, _ = gpu.run_adversarial_condition(X, img_c, img_s, txt_c, txt_s)
+    for l in range(3):
+        o = oracle.rips(X[l], maxdim=1)
+        sil = [oracle.silhouette(o["dperm2all"], lab) for lab in (img_c, img_s, txt_c, txt_s)]
+        want = gpu.layer_record_adversarial(l, o["dgms"], sil)
+        got = recs[l]
+        for k in want:
+            if k.startswith("silhouette"):
+                assert abs(got[k] - want[k]) < 1e-9, (n, l, k)
+            else:
+                assert got[k] == want[k], (n, l, k)
