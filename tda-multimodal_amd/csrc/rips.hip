@@ -262,8 +262,10 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
             // in all, N=2048 ~2^28); records: raw copies of the paired columns.  HBM is 288 GB.
             auto clampp = [](uint64_t x, int lo, int hi) { return std::min<uint64_t>(std::max<uint64_t>(next_pow2(x), 1ull << lo), 1ull << hi); };
             // + chunks 0..3 of the 33 buckets of every k_reduce_par workgroup
-            p.bpool_cap = (clampp(N * N * 128, 24, 30) << scale) + (uint64_t)kParGrid * 33 * 3840;
-            p.rpool_cap = clampp(N * N * 64, 22, 29) << scale;
+            // above N = 1024 start at 4x (torus N=2048 overflows 2x: measured r02, 3 attempts per call)
+            const int big4 = N > 1024 ? 2 : 0;
+            p.bpool_cap = (clampp(N * N * 128, 24, 30) << (scale + big4)) + (uint64_t)kParGrid * 33 * 3840;
+            p.rpool_cap = clampp(N * N * 64, 22, 29) << (scale + big4);
             p.rq_cap = 1ull << 16;
             p.o_pctl = take(sizeof(ParCtl));
             p.o_pitem = take((L + 1) * 8);
@@ -344,6 +346,16 @@ struct Workspace {
     size_t hin_cap = 0;
     uint64_t gen = 0;                  // bumped whenever a buffer baked into graphs moves
     std::vector<struct GraphEntry> graphs;
+    // the configuration a retry ended on (larger pools / another reducer), per
+    // (N, maxdim, input kind): later calls of that shape start there instead of
+    // failing the same way first
+    struct Retry {
+        int64_t N;
+        int maxdim, input_kind;
+        bool force_global, force_big, no_par;
+        int scale;
+    };
+    std::vector<Retry> retry;
     std::mutex mu;
 };
 
@@ -1211,6 +1223,19 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 #endif
 
+    if (force_global || scale || force_big || no_par) {  // remember what this shape needed
+        bool seen = false;
+        for (auto& m : w.retry)
+            if (m.N == p.N && m.maxdim == p.maxdim && m.input_kind == input_kind) {
+                m.force_global = m.force_global || force_global;
+                m.force_big = m.force_big || force_big;
+                m.no_par = m.no_par || no_par;
+                m.scale = std::max(m.scale, scale);
+                seen = true;
+            }
+        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale});
+    }
+
     // ---- result
     auto* R = new ResultImpl();
     const int nd = p.maxdim + 1;
@@ -1319,6 +1344,26 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     return 0;
 }
 
+// entry: start from the configuration an earlier call of this shape ended on
+int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_result** out) {
+    bool fg = false, fb = false, np = false;
+    int sc = 0;
+    // not when a test forces a reducer (the memo would override what it asks for)
+    if (!getenv_is("TDA_RETRY_MEMO", "0") && !getenv("TDA_REDUCE") && !getenv("TDA_PAR") && !getenv("TDA_PAR_STRICT") &&
+        !getenv("TDA_CHAIN")) {
+        Workspace& w = *get_ws(a.device);
+        std::lock_guard<std::mutex> g(w.mu);
+        for (const auto& m : w.retry)
+            if (m.N == a.N && m.maxdim == a.maxdim && m.input_kind == input_kind) {
+                fg = m.force_global;
+                fb = m.force_big;
+                np = m.no_par;
+                sc = m.scale;
+            }
+    }
+    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np);
+}
+
 int validate(const tda_rips_args* a) {
     if (!a) return fail(TDA_E_INVALID, "args is NULL");
     if (!a->x && a->L * a->N > 0) return fail(TDA_E_INVALID, "x is NULL");
@@ -1347,7 +1392,7 @@ int tda_rips_batch(const tda_rips_args* args, tda_rips_result** out) {
     *out = nullptr;
     if (int rc = validate(args)) return rc;
     if (!tda_device_ok(args->device)) return fail(TDA_E_NODEVICE, "no gfx950 device at ordinal " + std::to_string(args->device));
-    return run_pipeline(*args, args->is_dist ? 1 : 0, args->x, out);
+    return run_entry(*args, args->is_dist ? 1 : 0, args->x, out);
 }
 
 int tda_rips_dm(const float* D, int64_t n_entries, int32_t modulus, int32_t dim_max, float threshold, int32_t do_cocycles,
@@ -1373,7 +1418,7 @@ int tda_rips_dm(const float* D, int64_t n_entries, int32_t modulus, int32_t dim_
     a.device = 0;
     if (int rc = validate(&a)) return rc;
     if (!tda_device_ok(0)) return fail(TDA_E_NODEVICE, "no gfx950 device");
-    return run_pipeline(a, 2, D, out);
+    return run_entry(a, 2, D, out);
 }
 
 void tda_rips_free(tda_rips_result* r) {
