@@ -911,6 +911,17 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // on a third stream beside the H1 chain; they only need apparent<1>'s
     // pivot bitmap, and the chain records its residual pivots separately
     const bool split2 = p.dense && p.maxdim >= 2;
+    // H2 phase 1 (its early exits read the chain's residual H1 pivots as they
+    // appear); in the one-stream timing mode it runs right after the chain,
+    // so it sees what it sees when it runs beside it
+    auto launch_phase1 = [&](hipStream_t st) -> int {
+        hipLaunchKernelGGL(k_h2_phase1, dim3(L, kP1Grid), dim3(64), p.p1_lds, st, dist, n, stats, db[2], sb, (const uint16_t*)dnb.cls2,
+                           p.n2p, p.bm_words, (const uint32_t*)dnb.res1, (uint32_t)p.piv_words[1], step_limit());
+        HIPC(hipGetLastError());
+        if (int rc = (st == s && serial_stages ? tm : tm3).mark("k_h2_phase1")) return rc;
+        HIPC(hipEventRecord(w.evp, st));
+        return 0;
+    };
     // capture order of the launches (the graph executor dispatches in it):
     // TDA_ORDER=0 apparent<1> first; 1 side streams first; 2 side streams
     // first and the H2 branch after the triangle ranks; 3 side streams first,
@@ -941,12 +952,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipGetLastError());
             if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
             HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));  // edge classes (k_prep_*)
-            hipLaunchKernelGGL(k_h2_phase1, dim3(L, kP1Grid), dim3(64), p.p1_lds, w.stream3, dist, n, stats, db[2], sb,
-                               (const uint16_t*)dnb.cls2, p.n2p, p.bm_words, (const uint32_t*)dnb.res1, (uint32_t)p.piv_words[1],
-                               step_limit());
-            HIPC(hipGetLastError());
-            if (int rc = tm3.mark("k_h2_phase1")) return rc;
-            HIPC(hipEventRecord(w.evp, w.stream3));
+            if (!serial_stages)
+                if (int rc = launch_phase1(w.stream3)) return rc;
             if (order != 3) {
                 launch_sort(1, 1, s);
                 HIPC(hipGetLastError());
@@ -994,6 +1001,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipGetLastError());
             MARK("k_h1_chain");
             if (p.maxdim >= 2) {
+                if (serial_stages)
+                    if (int rc = launch_phase1(s)) return rc;
                 HIPC(hipStreamWaitEvent(s, w.evp, 0));  // phase-1 results
                 MARK("wait:phase1");
                 hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[1], db[2], rb, rc, sb,
