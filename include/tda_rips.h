@@ -122,6 +122,14 @@ typedef struct tda_rips_result {
     /* [L] TwoNN intrinsic dimension when args.want_twonn (NaN where the
      * reference returns NaN), else NULL (ABI >= 3) */
     const float *twonn;
+    /* ABI >= 3: count .. n_adds, num_edges, birth_idx / death_idx, thresh
+     * (padded to 8 bytes) and birth / death, in this order, are ONE
+     * allocation of blob_bytes bytes starting at blob (8-byte aligned
+     * blocks), so a binding copies every per-pair array in one read;
+     * n_pairs = total pairs over all layers and dims. */
+    const void *blob;
+    int64_t blob_bytes;
+    int64_t n_pairs;
 } tda_rips_result;
 
 #define TDA_FLAG_STAGE_TIMES 1

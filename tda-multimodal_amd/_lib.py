@@ -74,6 +74,9 @@ class RipsResult(ctypes.Structure):
         ("stage_ms", _f32p),
         ("silhouette", ctypes.POINTER(ctypes.c_double)),
         ("twonn", _f32p),
+        ("blob", ctypes.c_void_p),
+        ("blob_bytes", ctypes.c_int64),
+        ("n_pairs", ctypes.c_int64),
     ]
 
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -533,8 +534,8 @@ int set_lds_attrs(int dev) {
 // and birth_idx/death_idx are each one allocation too (tda_rips.h).
 struct ResultImpl {
     tda_rips_result pub;
-    std::vector<int64_t> meta, num_edges, idx;
-    std::vector<float> bd, thresh, dist, stage_ms, tn;
+    std::vector<uint64_t> blob;  // meta | num_edges | birth_idx, death_idx | thresh (padded) | birth, death
+    std::vector<float> dist, stage_ms, tn;
     std::vector<double> sil;
     std::vector<const char*> stage_name;
 };
@@ -555,6 +556,7 @@ std::string err_flags(int e) {
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
                  bool force_global = false, int scale = 0, bool force_big = false, bool no_par = false) {
+    const auto h_entry = std::chrono::steady_clock::now();
     Plan p;
     p.L = a.L;
     p.N = a.N;
@@ -1079,6 +1081,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(rec_t(w.ev1));
     return 0;
     };  // enqueue
+    // TDA_HOST_PROF=1: host-side time of the call's parts (stderr, every 200 calls)
+    static const bool host_prof = getenv_is("TDA_HOST_PROF", "1");
+    using hclk = std::chrono::steady_clock;
+    const auto h0 = hclk::now();
     if (ge) {
         HIPC(hipEventRecord(w.ev0, s));
         HIPC(hipGraphLaunch(ge->exec, s));
@@ -1106,7 +1112,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     } else {
         if (int rc = enqueue()) return rc;
     }
-    HIPC(hipStreamSynchronize(s));
+    const auto h1 = hclk::now();
+    HIPC(hipStreamSynchronize(s));  // (an event sync or a busy-polled end event measured the same, r02)
+    const auto h2 = hclk::now();
 
     int errs = 0;
     for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
@@ -1249,21 +1257,27 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     auto* R = new ResultImpl();
     const int nd = p.maxdim + 1;
     const size_t S = (size_t)L * nd;
-    R->meta.resize(7 * S);
-    int64_t* m_count = R->meta.data();
+    size_t total = 0;
+    for (int l = 0; l < L; ++l)
+        for (int d = 0; d < nd; ++d) total += (size_t)std::min<int64_t>(w.hstats[l].count[d], (int64_t)p.pcap[d]);
+    // one allocation (tda_rips.h layout guarantee): a binding copies it in one read
+    const size_t o_ne = 7 * S, o_idx = o_ne + L, o_thr = o_idx + 2 * total, o_bd = o_thr + (L + 1) / 2;
+    R->blob.assign(o_bd + total, 0);
+    int64_t* m_count = (int64_t*)R->blob.data();
     int64_t* m_off = m_count + S;
     uint64_t* m_cs = (uint64_t*)(m_count + 2 * S);
     int64_t* m_all = m_count + 3 * S;
     int64_t* m_cols = m_count + 4 * S;
     int64_t* m_res = m_count + 5 * S;
     int64_t* m_add = m_count + 6 * S;
-    R->thresh.resize(L);
-    R->num_edges.resize(L);
-    size_t total = 0;
+    float* r_thr = (float*)(R->blob.data() + o_thr);
+    int64_t* r_ne = (int64_t*)(R->blob.data() + o_ne);
+    int64_t* r_idx = (int64_t*)(R->blob.data() + o_idx);
+    float* r_bd = (float*)(R->blob.data() + o_bd);
     for (int l = 0; l < L; ++l) {
         const LayerStats& st = w.hstats[l];
-        R->thresh[l] = st.thresh;
-        R->num_edges[l] = st.num_edges;
+        r_thr[l] = st.thresh;
+        r_ne[l] = st.num_edges;
         for (int d = 0; d < nd; ++d) {
             int64_t c = std::min<int64_t>(st.count[d], (int64_t)p.pcap[d]);
             m_count[l * nd + d] = c;
@@ -1273,17 +1287,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             m_cols[l * nd + d] = st.n_columns[d];
             m_res[l * nd + d] = st.n_residual[d] - st.nskip[d];
             m_add[l * nd + d] = st.n_adds[d];
-            total += (size_t)c;
         }
     }
-    R->bd.resize(2 * total);
-    R->idx.resize(2 * total);
     for (size_t e = 0; e < total; ++e) {
         const OutPair q = w.hout[e];
-        R->bd[e] = q.birth;
-        R->bd[total + e] = q.death;
-        R->idx[e] = q.birth_idx;
-        R->idx[total + e] = q.death_idx;
+        r_bd[e] = q.birth;
+        r_bd[total + e] = q.death;
+        r_idx[e] = q.birth_idx;
+        r_idx[total + e] = q.death_idx;
     }
     if (a.want_dist) {
         R->dist.resize((size_t)L * n * n);
@@ -1297,12 +1308,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     o.N = n;
     o.count = m_count;
     o.offset = m_off;
-    o.birth = R->bd.data();
-    o.death = R->bd.data() + total;
-    o.birth_idx = R->idx.data();
-    o.death_idx = R->idx.data() + total;
-    o.thresh = R->thresh.data();
-    o.num_edges = R->num_edges.data();
+    o.birth = r_bd;
+    o.death = r_bd + total;
+    o.birth_idx = r_idx;
+    o.death_idx = r_idx + total;
+    o.thresh = r_thr;
+    o.num_edges = r_ne;
+    o.blob = R->blob.data();
+    o.blob_bytes = (int64_t)(R->blob.size() * 8);
+    o.n_pairs = (int64_t)total;
     o.checksum = m_cs;
     o.n_all_pairs = m_all;
     o.n_columns = m_cols;
@@ -1347,6 +1361,22 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         R->stage_name.push_back(tm3.names[i]);
     }
     o.n_stages = (int32_t)R->stage_name.size();
+    if (host_prof) {
+        static double acc[5] = {0, 0, 0, 0, 0};
+        static int calls = 0;
+        const auto h3 = hclk::now();
+        auto us = [](hclk::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
+        acc[0] += us(h1 - h0);
+        acc[1] += us(h2 - h1);
+        acc[2] += us(h3 - h2);
+        acc[3] += ms * 1e3;
+        acc[4] += us(h0 - h_entry);
+        if (++calls % 200 == 0) {
+            fprintf(stderr, "[tda-host] per call: setup %.1f us, launch %.1f us, sync %.1f us (device %.1f us), result %.1f us\n",
+                    acc[4] / 200, acc[0] / 200, acc[1] / 200, acc[3] / 200, acc[2] / 200);
+            acc[0] = acc[1] = acc[2] = acc[3] = acc[4] = 0;
+        }
+    }
     o.stage_name = R->stage_name.data();
     o.stage_ms = R->stage_ms.data();
     *out = &R->pub;

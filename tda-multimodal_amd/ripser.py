@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import warnings
+from itertools import repeat
 
 import numpy as np
 
@@ -26,85 +27,94 @@ from . import _lib
 class _Batch:
     """Host copies of one batched call's outputs; LayerResults are views into it."""
 
-    __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist", "sil", "tn")
+    __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist", "sil",
+                 "tn", "dg")
 
 
-class LayerResult:
+class LayerResult(tuple):
     """Persistence of one layer (all arrays on the host).
 
     ``dgms`` (list of (n_k, 2) float64 arrays, ripser's emission order) and
     the other fields are views into the batch's shared arrays, made on first
-    access.
+    access.  (A (batch, layer) tuple: one batched call makes L of them.)
     """
 
-    __slots__ = ("_dgms", "_b", "_l")
+    __slots__ = ()
 
-    def __init__(self, batch, layer):
-        self._dgms = None
-        self._b = batch
-        self._l = layer
+    @property
+    def _b(self):
+        return self[0]
+
+    @property
+    def _l(self):
+        return self[1]
 
     def _seg(self, arr):
-        b = self._b
-        return [arr[o:o + c] for o, c in zip(b.off[self._l].tolist(), b.cnt[self._l].tolist())]
+        b, l = self
+        return [arr[o:o + c] for o, c in zip(b.off[l].tolist(), b.cnt[l].tolist())]
 
     @property
     def dgms(self) -> list:
-        if self._dgms is None:
-            self._dgms = self._seg(self._b.pairs)
-        return self._dgms
+        b, l = self
+        d = b.dg[l]
+        if d is None:
+            d = b.dg[l] = self._seg(b.pairs)
+        return d
 
     @property
     def birth_idx(self):
-        return self._seg(self._b.bidx)
+        return self._seg(self[0].bidx)
 
     @property
     def death_idx(self):
-        return self._seg(self._b.didx)
+        return self._seg(self[0].didx)
 
     @property
     def num_edges(self) -> int:
-        return int(self._b.ne[self._l])
+        return int(self[0].ne[self[1]])
 
     @property
     def thresh(self) -> float:
-        return float(self._b.thr[self._l])
+        return float(self[0].thr[self[1]])
 
     @property
     def checksum(self) -> list:
-        return self._b.cs[self._l].tolist()
+        return self[0].cs[self[1]].tolist()
 
     @property
     def n_all_pairs(self) -> list:
-        return self._b.na[self._l].tolist()
+        return self[0].na[self[1]].tolist()
 
     @property
     def n_columns(self) -> list:
-        return self._b.nc[self._l].tolist()
+        return self[0].nc[self[1]].tolist()
 
     @property
     def n_residual(self) -> list:
-        return self._b.nr[self._l].tolist()
+        return self[0].nr[self[1]].tolist()
 
     @property
     def n_adds(self) -> list:
-        return self._b.nadd[self._l].tolist()
+        return self[0].nadd[self[1]].tolist()
 
     @property
     def silhouette(self) -> list:
         """Silhouette score per label set passed to ``ripser_batch(labels=...)``
         (sklearn.metrics.silhouette_score semantics), or [] when none."""
-        return [] if self._b.sil is None else self._b.sil[self._l].tolist()
+        b = self[0]
+        return [] if b.sil is None else b.sil[self[1]].tolist()
 
     @property
     def twonn(self) -> float:
         """TwoNN intrinsic dimension of the layer's cloud (``ripser_batch(twonn=True)``;
         metrics.py:113-208 semantics, NaN where the reference gives NaN), or None."""
-        return None if self._b.tn is None else float(self._b.tn[self._l])
+        b = self[0]
+        return None if b.tn is None else float(b.tn[self[1]])
 
     @property
     def dist(self):
-        return None if self._b.dist is None else self._b.dist[self._l]
+        b = self[0]
+        return None if b.dist is None else b.dist[self[1]]
 
 
 def _arr(ptr, n, dtype):
@@ -116,35 +126,39 @@ def _arr(ptr, n, dtype):
 
 def _unpack(res_p, want_dist: bool, n_sets: int = 0) -> tuple[list, dict]:
     r = res_p.contents
-    L, md, N = int(r.L), int(r.maxdim), int(r.N)
+    L, md, N = r.L, r.maxdim, r.N
     nd = md + 1
     S = L * nd
+    total = r.n_pairs
     b = _Batch()
     b.L, b.nd, b.N = L, nd, N
-    # count .. n_adds: seven consecutive [L][nd] blocks (tda_rips.h layout guarantee)
-    meta = _arr(r.count, 7 * S, np.int64).reshape(7, L, nd)
+    # one copy of the result blob (tda_rips.h): meta | num_edges | idx | thresh | birth, death
+    raw = ctypes.string_at(r.blob, r.blob_bytes)
+    w = np.frombuffer(raw, dtype=np.int64)
+    meta = w[:7 * S].reshape(7, L, nd)
     b.cnt, b.off = meta[0], meta[1]
     b.cs = meta[2].view(np.uint64)
     b.na, b.nc, b.nr, b.nadd = meta[3], meta[4], meta[5], meta[6]
-    total = int(b.cnt.sum())
-    # birth | death -> one (total, 2) float64 block; every diagram is a view into it
-    bd = _arr(r.birth, 2 * total, np.float32)
-    pairs = np.empty((total, 2), dtype=np.float64)
+    o = 7 * S
+    b.ne = w[o:o + L]
+    o += L
+    b.bidx, b.didx = w[o:o + total], w[o + total:o + 2 * total]
+    o += 2 * total
+    b.thr = np.frombuffer(raw, dtype=np.float32, count=L, offset=8 * o)
+    o += (L + 1) // 2
+    bd = np.frombuffer(raw, dtype=np.float32, count=2 * total, offset=8 * o) if total else np.zeros(0, np.float32)
+    pairs = np.empty((total, 2), dtype=np.float64)  # every diagram is a view into it
     pairs[:, 0] = bd[:total]
     pairs[:, 1] = bd[total:]
     b.pairs = pairs
-    idx = _arr(r.birth_idx, 2 * total, np.int64)
-    b.bidx, b.didx = idx[:total], idx[total:]
-    b.thr = _arr(r.thresh, L, np.float32)
-    b.ne = _arr(r.num_edges, L, np.int64)
+    b.dg = [None] * L
     b.dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N) if want_dist and bool(r.dist) else None
-    b.sil = None
     b.tn = _arr(r.twonn, L, np.float32) if bool(r.twonn) else None
-    if bool(r.silhouette):
-        b.sil = _arr(r.silhouette, L * n_sets, np.float64).reshape(L, n_sets)
-    out = [LayerResult(b, l) for l in range(L)]
-    stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(int(r.n_stages))]
-    return out, {"device_ms": float(r.device_ms), "stages": stages}
+    b.sil = _arr(r.silhouette, L * n_sets, np.float64).reshape(L, n_sets) if bool(r.silhouette) else None
+    out = list(map(LayerResult, zip(repeat(b, L), range(L))))
+    ns = r.n_stages
+    stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(ns)] if ns else []
+    return out, {"device_ms": r.device_ms, "stages": stages}
 
 
 def _call_batch(args: _lib.RipsArgs, want_dist: bool):
@@ -227,7 +241,9 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
         a.x = keep.data_ptr()
         a.x_on_device = 1
         device = keep.device.index if keep.device.index is not None else torch.cuda.current_device()
-        a.stream = torch.cuda.current_stream(keep.device).cuda_stream
+        # torch's current stream on that device (raw handle: no Stream object per call)
+        raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        a.stream = raw_stream(device) if raw_stream else torch.cuda.current_stream(keep.device).cuda_stream
         dtype_is64 = keep.dtype == torch.float64
     else:
         if _is_torch(X):
