@@ -76,6 +76,9 @@ struct Plan {
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
     bool par = false;  // H1 on k_reduce_par (many columns in flight), k_reduce_big for H2 / fallback
     bool packed = false;  // k_reduce_par keys carry packed vertices + apparent facet (N <= 1024)
+    bool wide = false;    // H2 on k_reduce_big with edge-code keys (tetrahedron indices > 32 bits)
+    uint64_t ecap = 0;    // per-layer stride of the sorted edge lengths
+    size_t o_dsort = 0, o_dtmp = 0, o_dcode = 0;
     bool serial_tables = false;  // HBM working tables of k_reduce_all (global mode) / k_reduce_big
     uint64_t ostride = 0, rec_cap = 0, rpool_cap = 0, bpool_cap = 0, rq_cap = 0;
     size_t o_pctl = 0, o_pitem = 0, o_pokey = 0, o_poval = 0, o_colpiv = 0, o_prec = 0, o_prpool = 0, o_pbpool = 0, o_prq = 0;
@@ -170,6 +173,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
         // TDA_PAR=0: H1 on the serial k_reduce_big as well (comparison / debugging)
         p.par = p.big && p.maxdim >= 1 && !no_par && !getenv_is("TDA_PAR", "0");
         p.packed = p.N <= 1024;
+        // C(N, 4) >= 2^32 (N > 568): the 32-bit index word of the H2 pivot keys
+        // overflows; TDA_H2_WIDE=1 forces the wide keys on any big-path N (tests)
+        p.wide = p.big && p.maxdim >= 2 && (binom(N, 4) >= (1ull << 32) || getenv_is("TDA_H2_WIDE", "1"));
         p.dense = p.lds_mode && p.maxdim >= 1 && p.N <= kDenseMaxN && p.N >= 3 && !want_wave;
     }
     if (p.dense) {  // carve of rips_reduce_small.h (h1_chain / h2_phase1), mirrored here
@@ -254,6 +260,12 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
             p.o_wl = take(L * p.wcap_g * 2 * 8);   // u64 index, 2 * wcap slots
             p.o_wp = take(L * p.wcap_g / 4 * 4);   // bucket fill counters
             if (p.big) p.o_bref = take(L * kNB * p.wcap_g * 4);  // radix-heap bucket references
+        }
+        if (p.wide) {
+            p.ecap = align_up(std::max<uint64_t>(binom(N, 2), 1), 32);
+            p.o_dsort = take(L * p.ecap * 8);
+            p.o_dtmp = take(L * p.ecap * 8);
+            p.o_dcode = take(L * N * N * 4);
         }
         if (p.par) {
             // k_reduce_par: owner maps, final pivots, records, bucket chunks, requeue slots
@@ -507,6 +519,7 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_edge_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEdgeSortLds));
     HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
     HIPC(hipFuncSetAttribute((const void*)k_twonn, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 4));
 #define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -682,7 +695,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.scale = scale;
     gk.force_big = force_big;
     gk.no_par = no_par;
-    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0);
+    gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0) |
+                 (p.wide ? 1 << 10 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
     gk.sil_K = sil_K;  // baked into the k_silhouette launch (argument K and its LDS size)
@@ -1021,6 +1035,21 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             gb.cap = p.wcap_g;
             gb.bcap = p.wcap_g;
             gb.step_limit = step_limit();
+            gb.wide = p.wide ? 1 : 0;
+            gb.dcode = (const uint32_t*)(B + p.o_dcode);
+            gb.dsort = (const uint64_t*)(B + p.o_dsort);
+            gb.ecap = p.ecap;
+            if (p.wide) {  // edge codes of the wide H2 keys (thresholds are known: after the H0 join)
+                hipLaunchKernelGGL(k_edge_sort, dim3(L), dim3(1024), kEdgeSortLds, s, dist, n, (uint64_t*)(B + p.o_dsort),
+                                   (uint64_t*)(B + p.o_dtmp), p.ecap);
+                HIPC(hipGetLastError());
+                MARK("k_edge_sort");
+                const unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
+                hipLaunchKernelGGL(k_edge_codes, dim3(gx, L), dim3(256), 0, s, dist, n, stats, (const uint64_t*)(B + p.o_dsort), p.ecap,
+                                   (uint32_t*)(B + p.o_dcode));
+                HIPC(hipGetLastError());
+                MARK("k_edge_codes");
+            }
             int start_dim = 1;
             if (p.par) {
                 ParBufs pb;
@@ -1413,9 +1442,10 @@ int validate(const tda_rips_args* a) {
     if (a->modulus != 2) return fail(TDA_E_UNSUPPORTED, "only coeff=2 (Z/2) is supported");
     if (a->maxdim < 0 || a->maxdim > 2) return fail(TDA_E_UNSUPPORTED, "maxdim must be 0, 1 or 2");
     if (a->N > 8192) return fail(TDA_E_UNSUPPORTED, "N > 8192 is not supported");
-    // filtration keys pack a 32-bit row-simplex index: C(N, maxdim+2) < 2^32
+    // H1 filtration keys pack a 32-bit row-simplex index: C(N, 3) < 2^32.  H2
+    // above N = 568 uses edge-code keys (21-bit code + 42-bit index): C(N, 2) < 2^21
     if (a->maxdim == 1 && a->N > 2900) return fail(TDA_E_UNSUPPORTED, "maxdim=1 requires N <= 2900");
-    if (a->maxdim == 2 && a->N > 568) return fail(TDA_E_UNSUPPORTED, "maxdim=2 requires N <= 568");
+    if (a->maxdim == 2 && a->N > 2048) return fail(TDA_E_UNSUPPORTED, "maxdim=2 requires N <= 2048");
     if (std::isnan(a->thresh)) return fail(TDA_E_INVALID, "thresh is NaN");
     if (a->want_twonn && !(a->twonn_discard >= 0.0 && a->twonn_discard < 1.0 && a->twonn_eps >= 0.0f))
         return fail(TDA_E_INVALID, "TwoNN needs 0 <= discard_fraction < 1 and eps >= 0");

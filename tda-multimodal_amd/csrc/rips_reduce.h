@@ -359,6 +359,23 @@ struct PivMap {
         else
             insert_t<false>(lo, val);
     }
+    // full 64-bit row keys (H2 above N = 568: tetrahedron indices exceed 32
+    // bits); HBM tables only.  A key never equals kEmpty64 (indices < 2^42).
+    __device__ int64_t find64(uint64_t key, int ln) const {
+        for (uint64_t h0 = mix64(key);; h0 += 64) {
+            const uint64_t kk = ld_glb(k, (h0 + ln) & mask);
+            const uint64_t mhit = __ballot(kk == key), mend = __ballot(kk == kEmpty64);
+            const uint64_t below_end = mend ? ((mend & (~mend + 1)) - 1) : ~0ull;
+            if (mhit & below_end) return (int64_t)ld_glb(v, (h0 + __builtin_ctzll(mhit & below_end)) & mask);
+            if (mend) return -1;
+        }
+    }
+    __device__ void insert64(uint64_t key, uint32_t val) const {  // one lane
+        uint64_t h = mix64(key) & mask;
+        while (ld_glb(k, h) != kEmpty64) h = (h + 1) & mask;
+        st_glb(k, h, key);
+        st_glb(v, h, val);
+    }
 };
 
 struct ReduceCtx {

@@ -29,7 +29,75 @@ struct BigBufs {
     uint32_t* bref;      // [L][kNB][bcap] log positions per radix bucket
     uint64_t cap, bcap;
     uint64_t step_limit;  // pivots per column before giving up (exit guarantee)
+    // wide H2 keys (N > 568: tetrahedron indices need up to 42 bits): the
+    // diameter is replaced by its edge code (rank of the first occurrence of
+    // the value among the layer's sorted edge lengths, k_edge_codes)
+    const uint32_t* dcode;  // [L][N][N] edge codes, kCodeInf above the threshold
+    const uint64_t* dsort;  // [L][ecap] sorted edge-length bits: dsort[code] = bits of the value
+    uint64_t ecap;
+    int wide;
 };
+
+// wide key = code << 42 | (2^42 - 1 - idx): 21-bit edge code (C(2048, 2) <
+// 2^21), 42-bit inverted index, bit 63 stays free for kDead
+constexpr int kWideIdxBits = 42;
+constexpr uint64_t kWideIdxMask = (1ull << kWideIdxBits) - 1;
+constexpr uint32_t kCodeInf = (1u << 21) - 1;
+
+// ---- wide H2 keys: per-layer edge codes
+// k_edge_sort: one workgroup per layer sorts the f32 bits of its C(N,2) edge
+// lengths (row-major strict upper triangle) ascending: LDS bitonic chunks of
+// 16384 keys, then merge-path passes in HBM (block_sort).
+constexpr int kEdgeSortLog2 = 14;
+constexpr size_t kEdgeSortLds = size_t(8) << kEdgeSortLog2;
+__global__ __launch_bounds__(1024) void k_edge_sort(const float* __restrict__ dist, int n, uint64_t* __restrict__ dsort,
+                                                    uint64_t* __restrict__ tmp, uint64_t ecap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x;
+    const float* D = dist + (size_t)l * n * n;
+    uint64_t* keys = dsort + (size_t)l * ecap;
+    const uint32_t nn = (uint32_t)n * (uint32_t)n;
+    for (uint32_t q = threadIdx.x; q < nn; q += blockDim.x) {
+        const uint32_t i = q / (uint32_t)n, j = q - i * (uint32_t)n;
+        if (j > i) st_glb(keys, (size_t)i * (2 * (size_t)n - i - 1) / 2 + (j - i - 1), (uint64_t)__float_as_uint(ld_glb(D, q)));
+    }
+    __syncthreads();
+    block_sort<false>(keys, nullptr, binom((uint64_t)n, 2), tmp + (size_t)l * ecap, nullptr, (uint64_t*)smem, nullptr, kEdgeSortLog2);
+}
+
+// k_edge_codes: code(i, j) = position of the first occurrence of d(i, j) in
+// the sorted lengths (monotone in the value, equal values share a code, and
+// dsort[code] gives the value back); kCodeInf above the layer's threshold.
+__global__ __launch_bounds__(256) void k_edge_codes(const float* __restrict__ dist, int n, const LayerStats* __restrict__ stats,
+                                                    const uint64_t* __restrict__ dsort, uint64_t ecap, uint32_t* __restrict__ dcode) {
+    const int l = blockIdx.y;
+    const float r = stats[l].thresh;
+    const float* D = dist + (size_t)l * n * n;
+    const uint64_t* S = dsort + (size_t)l * ecap;
+    const uint64_t E = binom((uint64_t)n, 2);
+    const uint32_t nn = (uint32_t)n * (uint32_t)n;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nn; q += gridDim.x * blockDim.x) {
+        const uint32_t i = q / (uint32_t)n, j = q - i * (uint32_t)n;
+        const float d = ld_glb(D, q);
+        uint32_t c = 0;
+        if (i != j) {
+            c = kCodeInf;
+            if (d <= r) {
+                const uint64_t b = __float_as_uint(d);
+                uint64_t lo = 0, hi = E;
+                while (lo < hi) {
+                    const uint64_t mid = (lo + hi) >> 1;
+                    if (ld_glb(S, mid) < b)
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                c = (uint32_t)lo;
+            }
+        }
+        st_glb(dcode, (size_t)l * nn + q, c);
+    }
+}
 
 struct BigShared {  // block-uniform state in LDS
     uint32_t cnt;           // log length
@@ -91,6 +159,7 @@ struct BigHeap {
     uint32_t* bref;  // [kNB][bcap]
     uint64_t cap, bcap;
     uint32_t imask;
+    bool wide;  // fingerprints (low 32 key bits) are not unique: verify hits against the log
     BigShared* S;
 
     // append log position pos (key k) to its radix bucket; wave-aggregated
@@ -115,12 +184,14 @@ struct BigHeap {
         }
     }
 
-    // slot of a logged key in the bucketed index (the key is present)
-    __device__ __forceinline__ uint32_t slot_of(uint32_t fp) const {
+    // slot of the key logged at position pos in the bucketed index (exact
+    // entry match, so fingerprints need not be unique)
+    __device__ __forceinline__ uint32_t slot_of(uint32_t fp, uint32_t pos) const {
+        const uint64_t want = ((uint64_t)fp << 32) | (pos + 1);
         uint32_t h = (mix32(fp) & (imask >> 3)) * 8;
         for (;;) {
             const uint64_t cur = index[h];
-            if (cur == 0 || (uint32_t)(cur >> 32) == fp) return h;
+            if (cur == 0 || cur == want) return h;
             h = (h + 1) & imask;
         }
     }
@@ -132,7 +203,7 @@ struct BigHeap {
     __device__ void compact() {
         __syncthreads();
         const uint32_t c = S->cnt < cap ? S->cnt : (uint32_t)cap;
-        for (uint32_t e = threadIdx.x; e < c; e += kBigT) bref[e] = slot_of((uint32_t)log[e]);
+        for (uint32_t e = threadIdx.x; e < c; e += kBigT) bref[e] = slot_of((uint32_t)log[e], e);
         __syncthreads();
         for (uint32_t e = threadIdx.x; e < c; e += kBigT) {
             const uint32_t h = bref[e];
@@ -201,7 +272,7 @@ struct BigHeap {
                 bool full = true;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    if (e[u] != 0 && (uint32_t)(e[u] >> 32) == fp) eh = e[u];
+                    if (e[u] != 0 && (uint32_t)(e[u] >> 32) == fp && (!wide || (log[(uint32_t)e[u] - 1] & ~kDead) == k)) eh = e[u];
                     full &= e[u] != 0;
                 }
                 if (eh) {
@@ -297,7 +368,7 @@ struct BigHeap {
     __device__ void reset() {
         const uint32_t c = S->cnt;
         for (uint32_t e = threadIdx.x; e < c; e += kBigT)
-            log[e] = (uint64_t)slot_of((uint32_t)log[e]);  // stash the slot (the log is rebuilt anyway)
+            log[e] = (uint64_t)slot_of((uint32_t)log[e], e);  // stash the slot (the log is rebuilt anyway)
         __syncthreads();
         for (uint32_t e = threadIdx.x; e < c; e += kBigT) {
             const uint32_t h = (uint32_t)log[e];
@@ -344,26 +415,6 @@ __device__ __forceinline__ float apparent_facet(const float* __restrict__ D, int
     return fd;
 }
 
-// toggle the coboundary of vs (diam sd) into H -- one thread per new vertex
-template <int DIM>
-__device__ __forceinline__ void big_cob(BigHeap& H, const float* __restrict__ D, int n, float r, const int (&vs)[DIM + 1], float sd) {
-    for (int v0 = 0; v0 < n; v0 += kBigT) {
-        const int v = v0 + (int)threadIdx.x;
-        bool ok = v < n;
-#pragma unroll
-        for (int i = 0; i <= DIM; ++i) ok &= (vs[i] != v);
-        float cd = sd;
-        uint64_t key = 0;
-        if (ok) {
-#pragma unroll
-            for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, ld_glb(D, (size_t)vs[i] * n + v));
-            ok = cd <= r;
-            key = filt_key(cd, cofacet_index<DIM>(vs, v));
-        }
-        H.toggle_pass(key, ok);
-    }
-}
-
 template <int DIM>
 __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, LayerStats* st, int l, const DimBufs& b,
                                const Reduce2Bufs& rb, const BigBufs& gb, BigShared& S, PivMap& map, const PivMap* prev,
@@ -390,7 +441,20 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
     H.cap = gb.cap;
     H.bcap = gb.bcap;
     H.imask = (uint32_t)(2 * gb.cap - 1);
+    const bool wide = DIM == 2 && gb.wide;
+    H.wide = wide;
     H.S = &S;
+    const uint32_t* dcode = wide ? gb.dcode + (size_t)l * n * n : nullptr;
+    const uint64_t* dsort = wide ? gb.dsort + (size_t)l * gb.ecap : nullptr;
+    // edge code of a simplex (max over its edges; codes are monotone in the diameter)
+    auto scode = [&](const int (&vs)[DIM + 1]) -> uint32_t {
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i <= DIM; ++i)
+#pragma unroll
+            for (int k = i + 1; k <= DIM; ++k) c = max(c, ld_glb(dcode, (size_t)vs[i] * n + vs[k]));
+        return c;
+    };
     const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
     uint64_t* roff = rb.roff + (size_t)l * b.rcap;
     uint32_t* rlen = rb.rlen + (size_t)l * b.rcap;
@@ -410,16 +474,22 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
     }
     __syncthreads();
 
-    // toggle the coboundary of vs (diam sd) -- one thread per new vertex
-    auto cob = [&](const int (&vs)[DIM + 1], float sd) {
+    // toggle the coboundary of vs (diam sd, wide: edge code sc) -- one thread per new vertex
+    auto cob = [&](const int (&vs)[DIM + 1], float sd, uint32_t sc) {
         for (int v0 = 0; v0 < n; v0 += kBigT) {
             const int v = v0 + tid;
             bool ok = v < n;
 #pragma unroll
             for (int i = 0; i <= DIM; ++i) ok &= (vs[i] != v);
-            float cd = sd;
             uint64_t key = 0;
-            if (ok) {
+            if (ok && wide) {
+                uint32_t cc = sc;
+#pragma unroll
+                for (int i = 0; i <= DIM; ++i) cc = max(cc, ld_glb(dcode, (size_t)vs[i] * n + v));
+                ok = cc < kCodeInf;
+                key = ((uint64_t)cc << kWideIdxBits) | (kWideIdxMask - cofacet_index<DIM>(vs, v));
+            } else if (ok) {
+                float cd = sd;
 #pragma unroll
                 for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, ld_glb(D, (size_t)vs[i] * n + v));
                 ok = cd <= r;
@@ -449,10 +519,11 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             if (tid == 0) rlen[j] = 0;
             continue;
         }
-        if (tid == 0) S.last = __float_as_uint(sdm + 0.0f);
+        const uint32_t sc = wide ? scode(vs) : 0u;
+        if (tid == 0) S.last = wide ? (uint32_t)(((uint64_t)sc << kWideIdxBits) >> 32) : __float_as_uint(sdm + 0.0f);
         __syncthreads();
         TDA_STAMP(t_c0);
-        cob(vs, sdm);
+        cob(vs, sdm, sc);
         TDA_ACC(0, t_c0);
         for (uint64_t step = 0;; ++step) {
             TDA_STAMP(t_p0);
@@ -478,10 +549,10 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                 }
                 break;
             }
-            const uint64_t pidx = 0xFFFFFFFFull - (pk & 0xFFFFFFFFull);
-            const float pd = __uint_as_float((uint32_t)(pk >> 32));
+            const uint64_t pidx = wide ? kWideIdxMask - (pk & kWideIdxMask) : 0xFFFFFFFFull - (pk & 0xFFFFFFFFull);
+            const float pd = wide ? __uint_as_float((uint32_t)ld_glb(dsort, pk >> kWideIdxBits)) : __uint_as_float((uint32_t)(pk >> 32));
             const bool app = (ld_glb((const uint32_t*)pivg, pidx >> 5) >> (pidx & 31)) & 1u;
-            const int64_t owner = app ? map.find((uint32_t)pidx, ln) : -1;
+            const int64_t owner = !app ? -1 : wide ? map.find64(pidx, ln) : map.find((uint32_t)pidx, ln);
             TDA_STAMP(t_a0);
             if (owner >= 0) {
                 const uint64_t o0 = ld_glb((const uint64_t*)roff, owner);
@@ -498,7 +569,7 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
             } else if (app) {
                 int fv[DIM + 1];
                 const float fd = apparent_facet<DIM>(D, n, pidx, fv);
-                cob(fv, fd);
+                cob(fv, fd, wide ? scode(fv) : 0u);
                 ++nadds;
                 TDA_ACC(3, t_a0);
             } else {
@@ -511,7 +582,10 @@ __device__ void big_reduce_dim(const float* __restrict__ D, int n, float r, Laye
                         else
                             atomicOr(&st->err, ERR_PAIR_CAP);
                     }
-                    map.insert((uint32_t)pidx, (uint32_t)j);
+                    if (wide)
+                        map.insert64(pidx, (uint32_t)j);
+                    else
+                        map.insert((uint32_t)pidx, (uint32_t)j);
                     atomicOr(&pivg[pidx >> 5], 1u << (pidx & 31));
                 }
                 cs += pair_hash(sidx, pidx);

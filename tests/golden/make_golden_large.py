@@ -17,7 +17,12 @@ the GPU tests read the committed files and never run the oracle at this size).
   stacks), N = 36 and 144.  The inputs are regenerated from a seed in the test
   (4096-wide clouds would be MBs); a SHA-256 of the bytes pins them.
 
-Usage: python tests/golden/make_golden_large.py [--dist-only]
+* large_h2.npz -- the oracle on H0-H2 above N = 568, where tetrahedron
+  indices no longer fit 32 bits (the GPU's wide edge-code keys): torus600
+  (seed 0, ~18 s of oracle) and torus1024 (configs[3]'s cloud at maxdim 2,
+  ~90 s).  Same layout as large_cases.npz.
+
+Usage: python tests/golden/make_golden_large.py [--dist-only | --h2-only]
 """
 from __future__ import annotations
 
@@ -97,7 +102,25 @@ def large_golden():
     np.savez_compressed(os.path.join(HERE, "large_cases.npz"), **out)
 
 
+def h2_golden():
+    from oracle import oracle
+
+    syn = __import__("importlib").import_module("tda-multimodal_amd.synthetic")
+    out = {}
+    for name, n in (("torus600", 600), ("torus1024", 1024)):
+        X = syn.torus(n, seed=0)[None]
+        t0 = time.time()
+        res = oracle.rips_batch_f32(X, 2)
+        print(f"{name} H0-H2: {time.time() - t0:.1f} s", flush=True)
+        out.update(case_arrays(name, X, 2, res))
+    np.savez_compressed(os.path.join(HERE, "large_h2.npz"), **out)
+
+
 if __name__ == "__main__":
+    if "--h2-only" in sys.argv:
+        h2_golden()
+        sys.exit(0)
     dist_golden()
     if "--dist-only" not in sys.argv:
         large_golden()
+        h2_golden()

@@ -346,6 +346,31 @@ def test_full_workload_vs_committed_oracle(gpu, name):
         assert_same_golden(res[l], z, name, l, md)
 
 
+@pytest.mark.parametrize("name", ["torus600", "torus1024"])
+def test_h2_above_568_vs_committed_oracle(gpu, name):
+    """H0-H2 where tetrahedron indices exceed 32 bits (C(N,4) >= 2^32 above
+    N = 568): the radix-heap H2 reduction on wide edge-code keys against the
+    committed oracle runs (make_golden_large.py --h2-only); torus1024 is C4's
+    cloud at maxdim 2 (S^1 x S^1: one dominant H2 class)."""
+    z = np.load(os.path.join(GOLDEN, "large_h2.npz"))
+    X = z[f"{name}__X"]
+    res = gpu.ripser_batch(X, maxdim=2)
+    assert_same_golden(res[0], z, name, 0, 2)
+    pers = np.sort(res[0].dgms[2][:, 1] - res[0].dgms[2][:, 0])[::-1]
+    assert pers[0] > 2.0 * pers[1]
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_h2_wide_keys_forced_vs_oracle(gpu, oracle, monkeypatch, wide):
+    """The wide edge-code keys forced below N = 568 (TDA_H2_WIDE=1) must give
+    what the 32-bit keys give: the same pairs, indices and checksums as the
+    oracle, on the big-path H2 reduction (N = 300)."""
+    monkeypatch.setenv("TDA_H2_WIDE", wide)
+    X = gpu.synthetic.torus(300, seed=0)
+    res = gpu.ripser_batch(X[None], maxdim=2)[0]
+    assert_same(res, oracle.rips(X, maxdim=2), 2, f"torus300 wide={wide}")
+
+
 def test_distance_high_dim_vs_sklearn(gpu):
     """D = 64 and 4096 (raw hidden size) against sklearn's f32-upcast
     pairwise_distances.  sklearn's Gram products go through BLAS dgemm, whose
