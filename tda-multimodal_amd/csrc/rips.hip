@@ -75,6 +75,7 @@ struct Plan {
     bool lds_mode = false;
     bool big = false;  // k_reduce_big (1024-thread radix-heap reduction) instead of one wave per layer
     bool par = false;  // H1 on k_reduce_par (many columns in flight), k_reduce_big for H2 / fallback
+    bool par2 = false;    // H2 on k_reduce_par as well (N <= 568: 32-bit tetrahedron indices)
     bool packed = false;  // k_reduce_par keys carry packed vertices + apparent facet (N <= 1024)
     bool wide = false;    // H2 on k_reduce_big with edge-code keys (tetrahedron indices > 32 bits)
     uint64_t ecap = 0;    // per-layer stride of the sorted edge lengths
@@ -168,14 +169,16 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
         const char* m = getenv("TDA_REDUCE");
         // measured (r01): one wave per layer wins up to N = 256 (grid144 md2
         // 20.6 vs 26.8 ms, torus256 md2 64 vs 91 ms); the radix heap above
-        const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big");
-        p.big = !p.lds_mode && (force_big || want_big || (!want_wave && p.N > kBigMinN));
+        const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big"), want_par = m && !strcmp(m, "par");
+        p.big = !p.lds_mode && (force_big || want_big || want_par || (!want_wave && p.N > kBigMinN));
         // TDA_PAR=0: H1 on the serial k_reduce_big as well (comparison / debugging)
         p.par = p.big && p.maxdim >= 1 && !no_par && !getenv_is("TDA_PAR", "0");
         p.packed = p.N <= 1024;
         // C(N, 4) >= 2^32 (N > 568): the 32-bit index word of the H2 pivot keys
         // overflows; TDA_H2_WIDE=1 forces the wide keys on any big-path N (tests)
         p.wide = p.big && p.maxdim >= 2 && (binom(N, 4) >= (1ull << 32) || getenv_is("TDA_H2_WIDE", "1"));
+        // TDA_PAR2=0: H2 on the serial radix-heap kernel after a parallel H1
+        p.par2 = p.par && p.maxdim >= 2 && !p.wide && !getenv_is("TDA_PAR2", "0");
         p.dense = p.lds_mode && p.maxdim >= 1 && p.N <= kDenseMaxN && p.N >= 3 && !want_wave;
     }
     if (p.dense) {  // carve of rips_reduce_small.h (h1_chain / h2_phase1), mirrored here
@@ -254,7 +257,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
         if (!p.big) p.o_wt = take(L * wmax * 8 * 2);  // slot scratch + compaction keys
         // global working tables of the one-wave / serial radix-heap kernels (not needed when
         // k_reduce_par takes H1 and there is no H2)
-        p.serial_tables = !p.lds_mode && !(p.par && p.maxdim < 2);
+        p.serial_tables = !p.lds_mode && !(p.par && (p.maxdim < 2 || p.par2));
         if (p.serial_tables) {
             p.o_wk = take(L * p.wcap_g * 8);       // key log
             p.o_wl = take(L * p.wcap_g * 2 * 8);   // u64 index, 2 * wcap slots
@@ -269,8 +272,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
         }
         if (p.par) {
             // k_reduce_par: owner maps, final pivots, records, bucket chunks, requeue slots
-            p.ostride = next_pow2(2 * p.rcap[1] + 16);
-            p.rec_cap = 2 * (uint64_t)L * p.rcap[1] + 4096;
+            const uint64_t prc = p.par2 ? std::max(p.rcap[1], p.rcap[2]) : p.rcap[1];
+            p.ostride = next_pow2(2 * prc + 16);
+            p.rec_cap = 2 * (uint64_t)L * prc + 4096;
             // bucket chunks: every workgroup keeps its peak bucket sizes (torus N=1024 needs ~2^26 keys
             // in all, N=2048 ~2^28); records: raw copies of the paired columns.  HBM is 288 GB.
             auto clampp = [](uint64_t x, int lo, int hi) { return std::min<uint64_t>(std::max<uint64_t>(next_pow2(x), 1ull << lo), 1ull << hi); };
@@ -278,13 +282,14 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
             // above N = 1024 start at 4x (torus N=2048 overflows 2x: measured r02, 3 attempts per call)
             const int big4 = N > 1024 ? 2 : 0;
             p.bpool_cap = (clampp(N * N * 128, 24, 30) << (scale + big4)) + (uint64_t)kParGrid * 33 * 3840;
-            p.rpool_cap = clampp(N * N * 64, 22, 29) << (scale + big4);
+            // H2 records as well: grid144 (32 layers) stores ~4.4 M keys of reduced H2 columns
+            p.rpool_cap = clampp(std::max<uint64_t>(N * N * 64, p.par2 ? L * N * N * 8 : 0), 22, 29) << (scale + big4);
             p.rq_cap = 1ull << 16;
             p.o_pctl = take(sizeof(ParCtl));
             p.o_pitem = take((L + 1) * 8);
             p.o_pokey = take(L * p.ostride * 8);
             p.o_poval = take(L * p.ostride * 8);
-            p.o_colpiv = take(L * p.rcap[1] * 8);
+            p.o_colpiv = take(L * prc * 8);
             p.o_prec = take(p.rec_cap * 32);
             p.o_prpool = take(p.rpool_cap * 8);
             p.o_pbpool = take(p.bpool_cap * 8);
@@ -516,8 +521,10 @@ int set_lds_attrs(int dev) {
     TDA_ATTR_RED(false, true, false);
     TDA_ATTR_RED(false, false, false);
 #undef TDA_ATTR_RED
-    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
-    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_edge_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEdgeSortLds));
     HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
@@ -1069,21 +1076,43 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 pb.rq_cap = p.rq_cap;
                 pb.step_limit = step_limit();
                 HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
-                hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb);
+                hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);
                 HIPC(hipGetLastError());
                 MARK("k_par_init");
                 // persistent workers: two 71-KB-LDS workgroups per CU; the surplus exits at once
                 const unsigned par_grid = par_grid_size();
+                const uint32_t* no_clr = nullptr;
                 if (p.packed)
-                    hipLaunchKernelGGL(k_reduce_par<true>, dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], rb, pb);
+                    hipLaunchKernelGGL((k_reduce_par<1, true>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], no_clr,
+                                       (uint64_t)0, rb, pb);
                 else
-                    hipLaunchKernelGGL(k_reduce_par<false>, dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], rb, pb);
+                    hipLaunchKernelGGL((k_reduce_par<1, false>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], no_clr,
+                                       (uint64_t)0, rb, pb);
                 HIPC(hipGetLastError());
                 MARK("k_reduce_par");
-                hipLaunchKernelGGL(k_par_emit, dim3(L), dim3(1024), 0, s, stats, db[1], rb, pb, pairs1, p.pcap[1], p.maxdim >= 2 ? 1 : 0);
+                // H2 next: residual H1 pivots into the dim-1 bitmap (k_reduce_par<2>) or map (k_reduce_big)
+                hipLaunchKernelGGL(k_par_emit<1>, dim3(L), dim3(1024), 0, s, stats, db[1], rb, pb, pairs1, p.pcap[1],
+                                   p.maxdim < 2 ? 0 : p.par2 ? 2 : 1);
                 HIPC(hipGetLastError());
                 MARK("k_par_emit");
                 start_dim = 2;
+                if (p.par2) {  // H2 columns on the same workers (an H1 abort skips it: k_par_init keeps the flag)
+                    HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
+                    hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[2], pb, 2);
+                    HIPC(hipGetLastError());
+                    if (n <= kPar2PackedMaxN)
+                        hipLaunchKernelGGL((k_reduce_par<2, true>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[2],
+                                           (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb);
+                    else
+                        hipLaunchKernelGGL((k_reduce_par<2, false>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[2],
+                                           (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb);
+                    HIPC(hipGetLastError());
+                    MARK("k_reduce_par<2>");
+                    hipLaunchKernelGGL(k_par_emit<2>, dim3(L), dim3(1024), 0, s, stats, db[2], rb, pb, pairs2, p.pcap[2], 0);
+                    HIPC(hipGetLastError());
+                    MARK("k_par_emit<2>");
+                    start_dim = 3;
+                }
             }
             if (start_dim <= p.maxdim)
                 hipLaunchKernelGGL(k_reduce_big, dim3(L), dim3(kBigT), 0, s, dist, n, p.maxdim, stats, db[1], db[2], rb, gb, pairs1,
@@ -1095,7 +1124,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         }
 #undef TDA_LAUNCH_RED
         HIPC(hipGetLastError());
-        if (!p.dense && !(p.par && p.maxdim < 2)) MARK(p.big ? "k_reduce_big" : "k_reduce_all");
+        if (!p.dense && !(p.par && (p.maxdim < 2 || p.par2))) MARK(p.big ? "k_reduce_big" : "k_reduce_all");
     } else {
         HIPC(hipStreamWaitEvent(s, w.evh, 0));
         HIPC(hipStreamWaitEvent(s, w.evj, 0));

@@ -695,6 +695,74 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
     }
 }
 
+// tetrahedron keys (H2 columns' cofacets).  PACKED (N <= 400, C(N,4) < 2^30):
+// lo32 = ~(index << 2 | f), f the position (in descending vertex order) of the
+// vertex its apparent facet omits -- the facet apparent_facet<2> picks: max
+// diameter, first on ties.  Otherwise (N <= 568) lo32 = ~index.
+constexpr int kPar2PackedMaxN = 400;
+template <bool PACKED>
+__device__ __forceinline__ uint32_t tet_lo(uint64_t idx, int f) {
+    if (PACKED) return 0xFFFFFFFFu - (((uint32_t)idx << 2) | (uint32_t)f);
+    return 0xFFFFFFFFu - (uint32_t)idx;
+}
+
+// toggle the coboundary of triangle (a > b > c), diameter sd, into the column
+// (no barrier; the caller made room).  Round 0's rows may be prefetched (r0).
+template <bool PACKED>
+__device__ __forceinline__ void col_cob2(ParCol& C, const ParBufs& P, const float* __restrict__ D, int n, float r, int a, int b, int c,
+                                         float sd, const float (&r0)[3][kParRV], ParStash* stash = nullptr) {
+    // the triangle's own edges (facet diameters of its cofacets)
+    const float eab = ld_glb(D, (size_t)a * n + b), eac = ld_glb(D, (size_t)a * n + c), ebc = ld_glb(D, (size_t)b * n + c);
+    const int vs[3] = {a, b, c};
+    for (int v0 = 0; v0 < n; v0 += kParT * kParRV) {
+        float da[kParRV], db[kParRV], dc[kParRV];
+#pragma unroll
+        for (int q = 0; q < kParRV; ++q) {
+            const int v = v0 + (int)threadIdx.x + q * kParT;
+            if (v0 == 0) {
+                da[q] = r0[0][q];
+                db[q] = r0[1][q];
+                dc[q] = r0[2][q];
+            } else {
+                da[q] = v < n ? ld_glb(D, (size_t)a * n + v) : 0.0f;
+                db[q] = v < n ? ld_glb(D, (size_t)b * n + v) : 0.0f;
+                dc[q] = v < n ? ld_glb(D, (size_t)c * n + v) : 0.0f;
+            }
+        }
+        PAR_T0(tk0);
+        uint64_t key[kParRV];
+        uint32_t vm = 0;
+#pragma unroll
+        for (int q = 0; q < kParRV; ++q) {
+            const int v = v0 + (int)threadIdx.x + q * kParT;
+            key[q] = 0;
+            if (v >= n || v == a || v == b || v == c) continue;
+            const float cd = fmaxf(fmaxf(sd, da[q]), fmaxf(db[q], dc[q]));
+            if (!(cd <= r)) continue;
+            // facet diameters: omitting v -> sd; a -> (b,c,v); b -> (a,c,v); c -> (a,b,v)
+            const float oa = fmaxf(ebc, fmaxf(db[q], dc[q]));
+            const float ob = fmaxf(eac, fmaxf(da[q], dc[q]));
+            const float oc = fmaxf(eab, fmaxf(da[q], db[q]));
+            // in descending vertex order of the cofacet
+            const int pv = v > a ? 0 : v > b ? 1 : v > c ? 2 : 3;  // position of v
+            float ex[4];
+            ex[0] = pv == 0 ? sd : oa;
+            ex[1] = pv == 0 ? oa : pv == 1 ? sd : ob;
+            ex[2] = pv <= 1 ? ob : pv == 2 ? sd : oc;
+            ex[3] = pv <= 2 ? oc : sd;
+            int f = 0;
+            float fd = ex[0];
+#pragma unroll
+            for (int u = 1; u < 4; ++u)
+                if (ex[u] > fd) f = u, fd = ex[u];
+            key[q] = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | tet_lo<PACKED>(cofacet_index<2>(vs, v), f);
+            vm |= 1u << q;
+        }
+        PAR_ACC(0, tk0);
+        col_add<kParRV>(C, P, key, vm, v0 == 0 ? stash : nullptr);
+    }
+}
+
 __host__ __device__ __forceinline__ uint32_t par_need(int n) {  // log entries one coboundary can add
     return (uint32_t)((n + kParT * kParRV - 1) / (kParT * kParRV)) * kParT * kParRV;
 }
@@ -831,9 +899,14 @@ __device__ __forceinline__ uint64_t par_omask(uint64_t nres, uint64_t ostride) {
     return (m > ostride ? ostride : m) - 1;
 }
 
-template <bool PACKED>
+// DIM 1: edge columns, triangle rows (PACKED: N <= 1024).  DIM 2: triangle
+// columns, tetrahedron rows (PACKED: N <= 400); a triangle is cleared when it
+// is any H1 pivot: `clr` is the dim-1 pivot bitmap, which k_par_emit<1> has
+// completed with the residual H1 pivots.
+template <int DIM, bool PACKED>
 __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ dist, int n, int L, LayerStats* __restrict__ stats,
-                                                      DimBufs b1, Reduce2Bufs rb, ParBufs P) {
+                                                      DimBufs b1, const uint32_t* __restrict__ clr, uint64_t clr_words, Reduce2Bufs rb,
+                                                      ParBufs P) {
     ParCol C;
     const int tid = threadIdx.x;
     for (uint32_t e = tid; e < 33u * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
@@ -896,9 +969,10 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         const uint64_t ckey = ld_glb(resid, j);
         const uint64_t sidx = key_idx(ckey);
         const float sdm = key_diam(ckey);
-        int sv[2];
-        decode<1>(sidx, n, sv);
-        if (!rec0 && ((ld_glb(mst, sidx >> 5) >> (sidx & 31)) & 1u)) {  // cleared: an H0 death
+        int sv[DIM + 1];
+        decode<DIM>(sidx, n, sv);
+        const uint32_t* cbits = DIM == 1 ? mst : clr + (size_t)l * clr_words;
+        if (!rec0 && ((ld_glb(cbits, sidx >> 5) >> (sidx & 31)) & 1u)) {  // cleared: an H_{DIM-1} death
             if (tid == 0) ast(colpiv + j, kParSkip);
             continue;
         }
@@ -928,15 +1002,18 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             PS.last = __float_as_uint(sdm + 0.0f);
         }
         front_reset();
-        float z0[kParRV], z1[kParRV];
         if (!rec0) {
+            float z[DIM + 1][kParRV];
 #pragma unroll
             for (int q = 0; q < kParRV; ++q) {
                 const int v = tid + q * kParT;
-                z0[q] = v < n ? ld_glb(D, (size_t)sv[0] * n + v) : 0.0f;
-                z1[q] = v < n ? ld_glb(D, (size_t)sv[1] * n + v) : 0.0f;
+#pragma unroll
+                for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(D, (size_t)sv[i] * n + v) : 0.0f;
             }
-            col_cob<PACKED>(C, P, D, n, r, sv[0], sv[1], sdm, z0, z1);
+            if constexpr (DIM == 1)
+                col_cob<PACKED>(C, P, D, n, r, sv[0], sv[1], sdm, z[0], z[1]);
+            else
+                col_cob2<PACKED>(C, P, D, n, r, sv[0], sv[1], sv[2], sdm, z);
         } else {
             if (tid == 0) PS.last = (uint32_t)(ald(P.rec + (rec0 - 1) * 4 + 2) >> 32);
             __syncthreads();
@@ -986,34 +1063,46 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 }
                 continue;
             }
-            // pivot: vertices, index, apparent facet
-            int t[3], fa, fb;
+            // pivot: vertices, index, apparent facet fv
+            int fv[DIM + 1];
             uint64_t pidx;
             const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
             const float pd = __uint_as_float((uint32_t)(pk >> 32));
-            if (PACKED) {
-                t[0] = (int)(plo >> 22);
-                t[1] = (int)((plo >> 12) & 1023u);
-                t[2] = (int)((plo >> 2) & 1023u);
-                const int f = (int)(plo & 3u);
-                fa = f == 0 ? t[1] : t[0];
-                fb = f == 2 ? t[1] : t[2];
-                pidx = encode<2>(t);
+            if constexpr (DIM == 1) {
+                int t[3];
+                if (PACKED) {
+                    t[0] = (int)(plo >> 22);
+                    t[1] = (int)((plo >> 12) & 1023u);
+                    t[2] = (int)((plo >> 2) & 1023u);
+                    const int f = (int)(plo & 3u);
+                    fv[0] = f == 0 ? t[1] : t[0];
+                    fv[1] = f == 2 ? t[1] : t[2];
+                    pidx = encode<2>(t);
+                } else {
+                    pidx = plo;
+                    (void)apparent_facet<1>(D, n, pidx, fv);
+                }
             } else {
-                pidx = plo;
-                decode<2>(pidx, n, t);
-                int fv[2];
-                (void)apparent_facet<1>(D, n, pidx, fv);
-                fa = fv[0];
-                fb = fv[1];
+                if (PACKED) {
+                    pidx = plo >> 2;
+                    const int f = (int)(plo & 3u);
+                    int t[4];
+                    decode<3>(pidx, n, t);
+#pragma unroll
+                    for (int u = 0, q = 0; u < 4; ++u)
+                        if (u != f) fv[q++] = t[u];
+                } else {
+                    pidx = plo;
+                    (void)apparent_facet<2>(D, n, pidx, fv);
+                }
             }
-            // one round trip: the pivot's bitmap word and the facet's two rows
-            float da[kParRV], db[kParRV];
+            // one round trip: the pivot's bitmap word and the facet's rows
+            float z[DIM + 1][kParRV];
 #pragma unroll
             for (int q = 0; q < kParRV; ++q) {
                 const int v = tid + q * kParT;
-                da[q] = v < n ? ld_glb(D, (size_t)fa * n + v) : 0.0f;
-                db[q] = v < n ? ld_glb(D, (size_t)fb * n + v) : 0.0f;
+#pragma unroll
+                for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(D, (size_t)fv[i] * n + v) : 0.0f;
             }
             // every thread reads the pivot's bitmap word (one address per wave): no barrier
             const uint32_t pw = ld_glb(pivg, pidx >> 5);
@@ -1024,7 +1113,10 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             t0 = clock64();
 #endif
             if (app) {
-                col_cob<PACKED>(C, P, D, n, r, fa, fb, pd, da, db, &stash);
+                if constexpr (DIM == 1)
+                    col_cob<PACKED>(C, P, D, n, r, fv[0], fv[1], pd, z[0], z[1], &stash);
+                else
+                    col_cob2<PACKED>(C, P, D, n, r, fv[0], fv[1], fv[2], pd, z, &stash);
                 ++adds;
 #ifdef TDA_PROFILE
                 pf[3] += clock64() - t0;
@@ -1114,7 +1206,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             for (int q = 0; q < 8; ++q) stats[0].prof[4][q] = C.q2[q];
         }
 #endif
-        if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[1], (unsigned long long)adds);
+        if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)adds);
         if (PS.err) {
             if (tid == 0) {
                 acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)item << 16) | (uint64_t)PS.err);  // first error: item, code
@@ -1126,9 +1218,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 }
 
 // per-layer residual counts -> item prefix, control block, owner maps cleared
-__global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats, int L, uint64_t rcap, ParBufs P) {
+__global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats, int L, uint64_t rcap, ParBufs P, int dim) {
     const int l = blockIdx.y;
-    uint64_t nres = (uint64_t)stats[l].n_residual[1];
+    uint64_t nres = (uint64_t)stats[l].n_residual[dim];
     if (nres > rcap) nres = rcap;
     const uint64_t m = par_omask(nres, P.ostride) + 1;
     uint64_t* ok = P.okey + (size_t)l * P.ostride;
@@ -1138,10 +1230,14 @@ __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats
         ov[e] = 0;
     }
     if (blockIdx.x == 0 && l == 0 && threadIdx.x == 0) {
+        if (dim > 1 && P.ctl->abort) {  // the H1 launch aborted: keep its flag and error, run nothing
+            P.ctl->total = 0;
+            return;
+        }
         uint64_t s = 0;
         for (int q = 0; q < L; ++q) {
             P.item_base[q] = s;
-            uint64_t c = (uint64_t)stats[q].n_residual[1];
+            uint64_t c = (uint64_t)stats[q].n_residual[dim];
             s += c > rcap ? rcap : c;
         }
         P.item_base[L] = s;
@@ -1152,7 +1248,10 @@ __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats
 }
 
 // Pairs from the final owners (one block per layer): emission buffer, stats,
-// and the dim-1 residual pivot map that the H2 reduction clears with.
+// and (DIM 1, H2 next) the residual H1 pivots that the H2 reduction clears
+// with: fill_map 1 -> the dim-1 pivot map (k_reduce_big), 2 -> OR'ed into the
+// dim-1 pivot bitmap (k_reduce_par<2>).
+template <int DIM>
 __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stats, DimBufs b1, Reduce2Bufs rb, ParBufs P,
                                                    Pair* __restrict__ pairs, uint64_t pcap, int fill_map) {
     __shared__ uint64_t red[3][16];
@@ -1185,7 +1284,7 @@ __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stat
                 continue;
             }
             if (cp == kParEss) {
-                const uint64_t pos = atomicAdd((unsigned long long*)&st->count[1], 1ull);
+                const uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
                 if (pos < pcap) store_pair(Pp, pos, sdm, INFINITY, (int64_t)sidx, -1);
                 else atomicOr(&st->err, ERR_PAIR_CAP);
                 continue;
@@ -1193,13 +1292,14 @@ __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stat
             const uint64_t pidx = 0xFFFFFFFFull - (cp & 0xFFFFFFFFull);
             const float pd = __uint_as_float((uint32_t)(cp >> 32));
             if (pd > sdm) {
-                const uint64_t pos = atomicAdd((unsigned long long*)&st->count[1], 1ull);
+                const uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
                 if (pos < pcap) store_pair(Pp, pos, sdm, pd, (int64_t)sidx, (int64_t)pidx);
                 else atomicOr(&st->err, ERR_PAIR_CAP);
             }
             cs += pair_hash(sidx, pidx);
             ++np;
-            if (fill_map) map.insert_par_t<false>((uint32_t)pidx, (uint32_t)j);
+            if (fill_map == 1) map.insert_par_t<false>((uint32_t)pidx, (uint32_t)j);
+            if (fill_map == 2) atomicOr(&b1.pivbits[(size_t)l * b1.piv_words + (pidx >> 5)], 1u << (pidx & 31));
         }
     }
     cs = wave_sum_u64(cs);
@@ -1217,10 +1317,10 @@ __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stat
         if (failed) {
             atomicOr(&st->err, ERR_PAR);
         } else {
-            atomicAdd((unsigned long long*)&st->checksum[1], (unsigned long long)a);
-            atomicAdd((unsigned long long*)&st->all_pairs[1], (unsigned long long)b);
-            atomicAdd((unsigned long long*)&st->n_columns[1], (unsigned long long)(0ull - c));
-            st->nskip[1] = c;
+            atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)a);
+            atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)b);
+            atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)(0ull - c));
+            st->nskip[DIM] = c;
         }
     }
 }

@@ -17,7 +17,8 @@ the GPU tests read the committed files and never run the oracle at this size).
   stacks), N = 36 and 144.  The inputs are regenerated from a seed in the test
   (4096-wide clouds would be MBs); a SHA-256 of the bytes pins them.
 
-* large_h2.npz -- the oracle on H0-H2 above N = 568, where tetrahedron
+* large_h2.npz -- the oracle on H0-H2 at N = 500 (the unpacked-key parallel
+  H2 reduction) and above N = 568, where tetrahedron
   indices no longer fit 32 bits (the GPU's wide edge-code keys): torus600
   (seed 0, ~18 s of oracle) and torus1024 (configs[3]'s cloud at maxdim 2,
   ~90 s).  Same layout as large_cases.npz.
@@ -107,7 +108,7 @@ def h2_golden():
 
     syn = __import__("importlib").import_module("tda-multimodal_amd.synthetic")
     out = {}
-    for name, n in (("torus600", 600), ("torus1024", 1024)):
+    for name, n in (("torus500", 500), ("torus600", 600), ("torus1024", 1024)):
         X = syn.torus(n, seed=0)[None]
         t0 = time.time()
         res = oracle.rips_batch_f32(X, 2)

@@ -346,7 +346,26 @@ def test_full_workload_vs_committed_oracle(gpu, name):
         assert_same_golden(res[l], z, name, l, md)
 
 
-@pytest.mark.parametrize("name", ["torus600", "torus1024"])
+@pytest.mark.parametrize("case", ["grid144", "torus256", "adv324"])
+def test_parallel_h2_reduction_vs_oracle(gpu, oracle, monkeypatch, case):
+    """H1 and H2 both on k_reduce_par (every residual column in flight, owner
+    map by CAS), forced at N <= 256 with TDA_REDUCE=par; TDA_PAR_STRICT=1 makes
+    an abort of the parallel path a failure instead of a serial re-run."""
+    monkeypatch.setenv("TDA_REDUCE", "par")
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")
+    if case == "grid144":
+        X = gpu.synthetic.sweep144(6)
+    elif case == "torus256":
+        X = gpu.synthetic.torus(256, seed=1)[None]
+    else:
+        X = np.random.default_rng(324).normal(size=(2, 324, 3)).astype(np.float32)
+    res = gpu.ripser_batch(X, maxdim=2)
+    orc = oracle.rips_batch_f32(X, 2)
+    for l in range(X.shape[0]):
+        assert_same(res[l], orc[l], 2, f"{case} layer {l}")
+
+
+@pytest.mark.parametrize("name", ["torus500", "torus600", "torus1024"])
 def test_h2_above_568_vs_committed_oracle(gpu, name):
     """H0-H2 where tetrahedron indices exceed 32 bits (C(N,4) >= 2^32 above
     N = 568): the radix-heap H2 reduction on wide edge-code keys against the

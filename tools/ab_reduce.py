@@ -1,0 +1,38 @@
+"""A/B of the residual reducers (TDA_REDUCE=wave|par) over N, maxdim and
+batch size: median device ms over a few replays (dev aid)."""
+import importlib
+import os
+import statistics
+import subprocess
+import sys
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+if len(sys.argv) > 1:  # child: one configuration
+    import numpy as np
+    import torch
+
+    pkg = importlib.import_module("tda-multimodal_amd")
+    n, md, L, kind = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    if kind == "torus":
+        X = np.stack([pkg.synthetic.torus(n, seed=s) for s in range(L)])
+    else:
+        X = np.random.default_rng(n).normal(size=(L, n, 3)).astype(np.float32)
+    Xd = torch.from_numpy(X).to("cuda:0")
+    ms = []
+    for i in range(6):
+        _, info = pkg.ripser_batch(Xd, maxdim=md, return_time=True)
+        if i >= 2:
+            ms.append(info["device_ms"])
+    print(f"{statistics.median(ms):.3f}")
+    sys.exit(0)
+for kind in ("torus", "gauss"):
+    for n in (80, 100, 144, 200, 256):
+        for md in (1, 2):
+            for L in (1, 32):
+                row = []
+                for red in ("wave", "par"):
+                    env = dict(os.environ, TDA_REDUCE=red)
+                    r = subprocess.run([sys.executable, __file__, str(n), str(md), str(L), kind], env=env, capture_output=True,
+                                       text=True, timeout=120)
+                    row.append(r.stdout.strip() or ("ERR " + r.stderr.strip()[-200:]))
+                print(f"{kind} N={n} md={md} L={L}: wave {row[0]} ms, par {row[1]} ms", flush=True)
