@@ -167,10 +167,14 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
     p.wcap_g = (N <= 256 ? 1ull << 17 : (N <= 640 ? 1ull << 21 : 1ull << 23)) << (2 * scale);
     {
         const char* m = getenv("TDA_REDUCE");
-        // measured (r01): one wave per layer wins up to N = 256 (grid144 md2
-        // 20.6 vs 26.8 ms, torus256 md2 64 vs 91 ms); the radix heap above
+        // measured (r01): one wave per layer beats the serial radix heap up to
+        // N = 256 (grid144 md2 20.6 vs 26.8 ms); measured (r02): the parallel
+        // reducer k_reduce_par beats both at every N > 64, H1 and H2, L = 1 and
+        // 32 (tools/ab_reduce.py: grid144 md2 L=32 24.1 -> 6.8 ms, torus256
+        // md2 L=32 926 -> 50 ms).  After a parallel abort (no_par) the old rule.
         const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big"), want_par = m && !strcmp(m, "par");
-        p.big = !p.lds_mode && (force_big || want_big || want_par || (!want_wave && p.N > kBigMinN));
+        const bool par_ok = !no_par && p.maxdim >= 1 && !getenv_is("TDA_PAR", "0");
+        p.big = !p.lds_mode && (force_big || want_big || want_par || (!want_wave && (p.N > kBigMinN || par_ok)));
         // TDA_PAR=0: H1 on the serial k_reduce_big as well (comparison / debugging)
         p.par = p.big && p.maxdim >= 1 && !no_par && !getenv_is("TDA_PAR", "0");
         p.packed = p.N <= 1024;
