@@ -7,11 +7,12 @@ include/tda_rips.h; no CPU fallback.
 """
 import sys as _sys
 
-from . import distributed, metrics, synthetic  # noqa: F401
+from . import distributed, metrics, synthetic, umap  # noqa: F401
 from .metrics import compute_intrinsic_dimensionality  # noqa: F401
 from ._lib import EXPORTS, LIB_PATH, build, lib  # noqa: F401
 from .pipeline import (get_max_persistence, get_persistence, layer_record, layer_record_adversarial, peak_layer,  # noqa: F401
                        run_adversarial_condition, run_sweep, write_layer_stats, write_summary_stats)
+from .umap import UMAP, umap_batch  # noqa: F401
 from .ripser import LayerResult, persistence_pairs, ripser, ripser_batch, rips_dm, silhouette_score  # noqa: F401
 
 _sys.modules.setdefault("tda_multimodal_amd", _sys.modules[__name__])
@@ -32,6 +33,8 @@ __all__ = [
     "peak_layer",
     "silhouette_score",
     "compute_intrinsic_dimensionality",
+    "UMAP",
+    "umap_batch",
     "build",
     "lib",
 ]

@@ -1541,3 +1541,6 @@ int tda_device_ok(int32_t device) {
 }
 
 }  // extern "C"
+
+// UMAP embedding (include/tda_umap.h): same library, same error state
+#include "umap_host.h"

@@ -158,7 +158,10 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
 constexpr int kDmT = 64, kDmKC = 32, kDmS = kDmKC + 2;
 typedef double dm_d4 __attribute__((ext_vector_type(4)));
 
-template <typename T>
+// METRIC 1: cosine distance instead (UMAP input, umap.distances.cosine:
+// 1 - <x,y> / sqrt(|x|^2 |y|^2), 0 for two zero rows, 1 for one), from the
+// same Gram tiles; clamped at 0.
+template <typename T, int METRIC = 0>
 __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, int n, int D, float* __restrict__ dist,
                                                        uint32_t* __restrict__ rowmax) {
     __shared__ double xs[2][kDmT][kDmS];  // [i/j tile][row][k]
@@ -243,7 +246,11 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
                 }
                 double d = (-2.0 * acc[a][b][r] + nrm[0][ri]) + nrm[1][cj];
                 float f;
-                if constexpr (sizeof(T) == 4) {
+                if constexpr (METRIC == 1) {
+                    const double ni = nrm[0][ri], nj = nrm[1][cj];
+                    d = (ni == 0.0 && nj == 0.0) ? 0.0 : (ni == 0.0 || nj == 0.0) ? 1.0 : 1.0 - acc[a][b][r] / sqrt(ni * nj);
+                    f = fmaxf((float)d, 0.0f);
+                } else if constexpr (sizeof(T) == 4) {
                     f = (float)d;
                     f = (f != f) ? f : fmaxf(f, 0.0f);
                     f = sqrt_rn_f32(f);

@@ -11,9 +11,12 @@ from conftest import ROOT
 
 
 def _declared_functions():
-    src = open(os.path.join(ROOT, "include", "tda_rips.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(tda_[a-z_]+)\s*\(", src)))
+    names = set()
+    for h in ("tda_rips.h", "tda_umap.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(tda_[a-z_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_header_and_binding_agree(pkg):
@@ -94,3 +97,36 @@ def test_ctypes_structs_match_header_layout(pkg, tmp_path):
             ctypes.sizeof(lb.RipsResult), lb.RipsResult.silhouette.offset, lb.RipsArgs.twonn_discard.offset,
             lb.RipsResult.twonn.offset, lb.RipsResult.n_pairs.offset]
     assert got == want
+
+
+def test_umap_struct_matches_header_layout(pkg, tmp_path):
+    import subprocess
+
+    from importlib import import_module
+
+    lb = import_module("tda-multimodal_amd._lib")
+    src = tmp_path / "ulayout.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "tda_umap.h"\n'
+        'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(tda_umap_args), offsetof(tda_umap_args, a),'
+        ' offsetof(tda_umap_args, seed), offsetof(tda_umap_args, out), offsetof(tda_umap_args, graph_out)); return 0;}\n')
+    exe = tmp_path / "ulayout"
+    subprocess.run(["gcc", "-I", lb.INCLUDE, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    U = lb.UmapArgs
+    assert got == [ctypes.sizeof(U), U.a.offset, U.seed.offset, U.out.offset, U.graph_out.offset]
+
+
+def test_umap_invalid_arguments_rejected_before_device(pkg, built_lib):
+    L = pkg.lib()
+    U = pkg._lib.UmapArgs()
+    X = np.zeros((1, 8, 3), np.float32)
+    out = np.zeros((1, 8, 2), np.float32)
+    U.x, U.out, U.dtype, U.L, U.N, U.D = X.ctypes.data, out.ctypes.data, 0, 1, 8, 3
+    U.metric, U.n_neighbors, U.n_components, U.n_epochs, U.a, U.b = 0, 4, 2, 10, 1.5, 0.9
+    U.metric = 5
+    assert L.tda_umap_batch(ctypes.byref(U)) == -2
+    U.metric, U.n_neighbors = 1, 9  # > N
+    assert L.tda_umap_batch(ctypes.byref(U)) == -1
+    U.n_neighbors = 4
+    assert L.tda_umap_batch(ctypes.byref(U)) == -5  # valid, but no gfx950 here
