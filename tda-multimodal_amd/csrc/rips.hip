@@ -876,10 +876,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     auto launch_apparent = [&](int d, hipStream_t st) {
         uint64_t blocks = (p.ncand[d] + 255) / 256;
         // total blocks over all layers: measured (r01, sweep48) 1024 beats 4096,
-        // whose grid holds every CU while the critical small kernels wait
-        static const uint64_t app_total = getenv("TDA_APP_GRID") ? strtoull(getenv("TDA_APP_GRID"), nullptr, 10) : 1024;
+        // whose grid holds every CU while the critical small kernels wait; off
+        // the dense path the apparent kernels run alone: 4096 (r02, grid144:
+        // apparent<2> 1.08 -> 0.87 ms; staging the 83-KB matrix in LDS: 2.25 ms)
+        static const char* app_env = getenv("TDA_APP_GRID");
+        const uint64_t app_total = app_env ? strtoull(app_env, nullptr, 10) : (p.dense ? 1024 : 4096);
         unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, app_total / L)));
-        const bool dl = n <= kAppLdsMaxN;
+        static const int app_lds_max = getenv("TDA_APP_LDS_MAXN") ? atoi(getenv("TDA_APP_LDS_MAXN")) : kAppLdsMaxN;
+        const bool dl = n <= app_lds_max && 16 + (size_t)n * n * 4 <= (size_t)kLdsMax;
         const size_t alds = 16 + (dl ? (size_t)n * n * 4 : 0);
         if (d == 1) {
             if (dl)
