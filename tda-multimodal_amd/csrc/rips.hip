@@ -59,10 +59,14 @@ constexpr int kSmallN = 64;                  // one-wave H0 + LDS-resident reduc
 constexpr int kAppLdsMaxN = 128;             // k_apparent stages the distance matrix in LDS up to here
 constexpr int kBigMinN = 256;                // large-N reducer above this N (global mode)
 constexpr int64_t kDistMfmaMinD = 32;        // k_distance_mfma (FP64 MFMA Gram tiles) from this D up
-constexpr unsigned kParGrid = 512;           // k_reduce_par workgroups: two 72-KB-LDS workgroups per CU
+constexpr unsigned kParGrid = 512;           // k_reduce_par workgroups at most (pool sizing): two 72-KB-LDS workgroups per CU
+// default: one per CU -- the longest column is the critical path and runs
+// faster without a second workgroup on its CU (r02, tools/ab_pargrid.sh:
+// grid144 10.5 -> 8.5 ms, torus1024 61 -> 58.5 ms at 256 vs 512)
+constexpr unsigned kParGridDefault = 256;
 unsigned par_grid_size() {
     const char* g = getenv("TDA_PAR_GRID");
-    const unsigned v = g ? (unsigned)atoi(g) : kParGrid;
+    const unsigned v = g ? (unsigned)atoi(g) : kParGridDefault;
     return v < 1 ? 1 : (v > kParGrid ? kParGrid : v);
 }
 
@@ -1087,7 +1091,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);
                 HIPC(hipGetLastError());
                 MARK("k_par_init");
-                // persistent workers: two 71-KB-LDS workgroups per CU; the surplus exits at once
+                // persistent workers (one 71-KB-LDS workgroup per CU by default); the surplus exits at once
                 const unsigned par_grid = par_grid_size();
                 const uint32_t* no_clr = nullptr;
                 if (p.packed)
