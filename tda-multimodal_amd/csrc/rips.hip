@@ -102,7 +102,7 @@ struct Plan {
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_epos = 0, o_cobt = 0, o_lenr = 0, o_clsr = 0, o_q0t = 0, o_eM = 0, o_cpos = 0, o_necnt = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_epos = 0, o_cobt = 0, o_lenr = 0, o_eM = 0, o_cpos = 0, o_necnt = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -310,8 +310,6 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
             p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
             p.o_epos = take(L * binom(N, 2) * 4);
             p.o_lenr = take(L * (binom(N, 2) + 8) * 4);
-            p.o_clsr = take(L * (binom(N, 2) + 8) * 4);
-            p.o_q0t = take(L * (binom(N, 2) + 8) * 4);
             p.o_eM = take(L * binom(N, 2) * 8);
             p.o_cpos = take(L * (binom(N, 2) + 8) * 4);
             if (p.fast) {
@@ -844,8 +842,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             dnb.K = p.dK;
             dnb.epos = (uint32_t*)(B + p.o_epos);
             dnb.lenr = (uint32_t*)(B + p.o_lenr);
-            dnb.clsr = (uint32_t*)(B + p.o_clsr);
-            dnb.q0t = (uint32_t*)(B + p.o_q0t);
             dnb.cobt = (uint16_t*)(B + p.o_cobt);
             dnb.cob_stride = p.cob_stride;
             dnb.eM = (uint64_t*)(B + p.o_eM);
@@ -855,10 +851,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             hipLaunchKernelGGL(k_prep_edges, pg, dim3(256), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_edges")) return rc;
-            hipLaunchKernelGGL(k_prep_scan, dim3(L), dim3(256), 0, s2, dnb, stats);
-            HIPC(hipGetLastError());
-            if (int rc = tm2.mark("k_prep_scan")) return rc;
-            hipLaunchKernelGGL(k_prep_tables, dim3(L, kPrepTabBlocks), dim3(kPrepTabT), prep_tables_lds(n), s2, dist, n, dnb, p.cmode);
+            hipLaunchKernelGGL(k_prep_tables, dim3(L, kPrepTabBlocks), dim3(kPrepTabT), prep_tables_lds(n), s2, dist, n, dnb, p.cmode, stats);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_tables")) return rc;
         }
@@ -877,6 +870,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         db[d].rcap = p.rcap[d];
         db[d].ncand = p.ncand[d];
     }
+    // N <= 64 with H2: the H2 columns (apparent<2>, their sort, phase 1) run
+    // on a third stream beside the H1 chain; they only need apparent<1>'s
+    // pivot bitmap, and the chain records its residual pivots separately
+    const bool split2 = p.dense && p.maxdim >= 2;
     auto launch_apparent = [&](int d, hipStream_t st) {
         uint64_t blocks = (p.ncand[d] + 255) / 256;
         // total blocks over all layers: measured (r01, sweep48) 1024 beats 4096,
@@ -942,10 +939,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         sb.p1_used = (unsigned long long*)(B + p.o_p1used);
         sb.p1_wcap = kP1WCap;
     }
-    // N <= 64 with H2: the H2 columns (apparent<2>, their sort, phase 1) run
-    // on a third stream beside the H1 chain; they only need apparent<1>'s
-    // pivot bitmap, and the chain records its residual pivots separately
-    const bool split2 = p.dense && p.maxdim >= 2;
     // H2 phase 1 (its early exits read the chain's residual H1 pivots as they
     // appear); in the one-stream timing mode it runs right after the chain,
     // so it sees what it sees when it runs beside it
@@ -964,6 +957,16 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     static const int order = getenv("TDA_ORDER") ? atoi(getenv("TDA_ORDER")) : 3;  // 3: measured best (r01)
     if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
+    auto launch_h2_columns = [&]() -> int {  // apparent<2> + their sort on the third stream
+        if (int rc = tm3.begin()) return rc;
+        launch_apparent(2, w.stream3);
+        HIPC(hipGetLastError());
+        if (int rc = tm3.mark("k_apparent<2>")) return rc;
+        launch_sort(2, 1, w.stream3);
+        HIPC(hipGetLastError());
+        if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
+        return 0;
+    };
     if (p.maxdim >= 1) {
         launch_apparent(1, s);
         HIPC(hipGetLastError());
@@ -979,13 +982,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             }
             HIPC(hipStreamWaitEvent(w.stream3, w.evs, 0));
             if (order == 2) HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));
-            if (int rc = tm3.begin()) return rc;
-            launch_apparent(2, w.stream3);
-            HIPC(hipGetLastError());
-            if (int rc = tm3.mark("k_apparent<2>")) return rc;
-            launch_sort(2, 1, w.stream3);
-            HIPC(hipGetLastError());
-            if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
+            if (int rc = launch_h2_columns()) return rc;
             HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));  // edge classes (k_prep_*)
             if (!serial_stages)
                 if (int rc = launch_phase1(w.stream3)) return rc;

@@ -45,7 +45,7 @@ struct LayerStats {  // zeroed every call; copied to the host result
     int64_t n_adds[4];     // column additions in the serial reduction
     int64_t nskip[4];      // residual columns cleared by the serial reduction (host: n_residual - nskip)
     uint64_t rmask[4];     // residual pivot map mask used by the dim's reducer (HBM map consumers)
-    int64_t ntri;          // N <= 64: triangles <= thresh (k_prep_scan)
+    int64_t ntri;          // N <= 64: triangles <= thresh (k_prep_tables)
     uint64_t prof[5][8];   // -DTDA_PROFILE builds: cycle counters (per dim; [3]: k_h0_wave, [4]: k_prep_layer)
 };
 enum : int32_t { ERR_RESID_CAP = 1, ERR_PAIR_CAP = 2, ERR_WORK_CAP = 4, ERR_VPOOL_CAP = 8, ERR_OUT_CAP = 16 };

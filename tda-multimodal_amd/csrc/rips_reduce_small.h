@@ -115,10 +115,8 @@ struct DenseBufs {
     uint32_t* res1;     // [L][piv_words1] colex bitmap of residual H1 pivots (H2 clearing; zeroed per call)
     uint32_t* epos;     // [L][E] rank of the edge among edges <= thresh (kNoRank above)
     uint32_t* lenr;     // [L][E + 8] length bits by rank
-    uint32_t* clsr;     // [L][E + 8] by rank: the class's triangle ranks: cs | ce << 16
-    uint32_t* q0t;      // [L][E + 8] by rank: first edge rank of the class | tie << 16
     uint64_t* eM;       // [L][E] block masks
-    uint32_t* cpos;     // [L][E + 8] block sizes by rank, then their exclusive scan
+    uint32_t* cpos;     // [L][E + 8] block sizes by rank (k_prep_tables scans them in LDS)
     uint32_t* necnt;    // [L] edges <= thresh (zeroed per call)
     uint16_t* cobt;     // [L][cob_stride] TABLE chain: rank of {a, b, v} at e * n + v
     uint32_t cob_stride;
@@ -132,8 +130,6 @@ struct DenseBufs {
 //   k_prep_edges   rank of each edge <= thresh in (length, index) order by
 //                  counting smaller 64-bit keys; its block mask M_e; by rank:
 //                  the block size and the length bits
-//   k_prep_scan    per layer: exclusive scan of the block sizes in rank
-//                  order, and each rank's length class [q0, q1]
 //   k_prep_tables  recs / cls / cls2 and the rank tables: inv16[rank] = edge
 //                  | first | tie; FAST and TABLE: inv32[rank] = a | b << 6 |
 //                  w << 12 | first << 18 | tie << 19; FAST: rank_of[triangle]
@@ -237,55 +233,6 @@ __global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ di
     }
 }
 
-// per layer: exclusive scan of the block sizes in rank order (cpos, in
-// place) and the length class of each rank: clsr[q] = first rank of the
-// class's triangles | end << 16, q0t[q] = first edge rank of the class |
-// tie << 16 (the class holds more than one edge)
-__global__ __launch_bounds__(256) void k_prep_scan(DenseBufs db, LayerStats* __restrict__ stats) {
-    __shared__ uint32_t wsum[4];
-    __shared__ uint32_t offs[2048 + 8];
-    __shared__ uint32_t lens[2048 + 8];
-    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
-    const uint32_t nE = db.necnt[l];
-    uint32_t* c = db.cpos + (size_t)l * (db.E + 8);
-    const uint32_t* lr = db.lenr + (size_t)l * (db.E + 8);
-    for (uint32_t q = t; q < nE; q += 256) lens[q] = ld_glb(lr, q);
-    const uint32_t per = (nE + 255) / 256, q0 = t * per;
-    uint32_t loc = 0;
-    for (uint32_t q = q0; q < min(nE, q0 + per); ++q) loc += ld_glb(c, q);
-    uint32_t x = loc;  // inclusive wave scan
-    for (int s = 1; s < 64; s <<= 1) {
-        const uint32_t y = __shfl_up(x, s, 64);
-        if (ln >= s) x += y;
-    }
-    if (ln == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int w = 0; w < wv; ++w) base += wsum[w];
-    uint32_t run = base + x - loc;  // exclusive prefix of this thread's chunk
-    for (uint32_t q = q0; q < min(nE, q0 + per); ++q) {
-        const uint32_t v = ld_glb(c, q);
-        offs[q] = run;
-        st_glb(c, q, run);
-        run += v;
-    }
-    if (t == 255) {
-        const uint32_t tot = base + x;
-        offs[nE] = tot;
-        st_glb(c, nE, tot);
-        stats[l].ntri = tot;
-    }
-    __syncthreads();
-    for (uint32_t q = t; q < nE; q += 256) {
-        const uint32_t len = lens[q];
-        uint32_t a = q, b = q;  // classes are short except on lattice-like inputs
-        while (a > 0 && lens[a - 1] == len) --a;
-        while (b + 1 < nE && lens[b + 1] == len) ++b;
-        st_glb(db.clsr + (size_t)l * (db.E + 8), (size_t)q, offs[a] | (offs[b + 1] << 16));
-        st_glb(db.q0t + (size_t)l * (db.E + 8), (size_t)q, a | ((uint32_t)(b > a) << 16));
-    }
-}
-
 // tables: kPrepTabBlocks blocks of 1024 threads per layer.  Every block
 // stages the layer's per-edge words (rank, block mask) and per-rank words
 // (first triangle rank, class range, class start) in LDS, so the
@@ -295,9 +242,15 @@ __global__ __launch_bounds__(256) void k_prep_scan(DenseBufs db, LayerStats* __r
 constexpr int kPrepTabBlocks = 4;
 constexpr int kPrepTabT = 1024;
 __host__ __device__ constexpr size_t prep_tables_lds(int n) {
-    return 16 + (((size_t)4 * n * n + 15) & ~(size_t)15) + (size_t)(n * (n - 1) / 2 + 8) * (8 + 4 + 4 + 4 + 4);
+    return 16 + (((size_t)4 * n * n + 15) & ~(size_t)15) + (size_t)(n * (n - 1) / 2 + 8) * (8 + 4 + 4 + 4 + 4 + 4) + 64;
 }
-__global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restrict__ dist, int n, DenseBufs db, int cmode) {
+// The per-layer scan (block sizes in rank order -> first triangle rank of
+// every block, and each rank's length class) is folded in: every block of the
+// layer redoes it in LDS from k_prep_edges' raw sizes and lengths (at most
+// C(64,2) = 2016 ranks), which takes one launch and one dependency hop off the
+// critical path (it was k_prep_scan).
+__global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restrict__ dist, int n, DenseBufs db, int cmode,
+                                                           LayerStats* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
     constexpr int NW = kPrepTabT / 64;
@@ -309,14 +262,53 @@ __global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restri
     uint32_t* fr = ep + ES;                                                          // [nE + 1] rank -> first triangle rank
     uint32_t* cl = fr + ES;                                                          // [nE] rank -> class triangle range
     uint32_t* qt = cl + ES;                                                          // [nE] rank -> class start | tie << 16
+    uint32_t* lens = qt + ES;                                                        // [nE] rank -> length bits
+    uint32_t* wsum = lens + ES;                                                      // [NW]
     const size_t lE = (size_t)l * db.E, lS = (size_t)l * (db.E + 8);
     stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, kPrepTabT);
+    const uint32_t nE = ld_glb(db.necnt, (size_t)l);
     for (int e = t; e < E; e += kPrepTabT) {
         Ms[e] = ld_glb(db.eM + lE, (size_t)e);
         ep[e] = ld_glb(db.epos + lE, (size_t)e);
-        fr[e] = ld_glb(db.cpos + lS, (size_t)e);
-        cl[e] = ld_glb(db.clsr + lS, (size_t)e);
-        qt[e] = ld_glb(db.q0t + lS, (size_t)e);
+    }
+    // scan: raw block sizes by rank -> exclusive prefix (fr[nE] = triangles <= thresh)
+    const uint32_t per = (nE + kPrepTabT - 1) / kPrepTabT, q0 = t * per, q1 = min(nE, q0 + per);
+    uint32_t loc = 0;
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t v = ld_glb(db.cpos + lS, (size_t)q);
+        fr[q] = v;
+        lens[q] = ld_glb(db.lenr + lS, (size_t)q);
+        loc += v;
+    }
+    uint32_t x = loc;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (ln >= o) x += y;
+    }
+    if (ln == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t run = x - loc, tot = 0;
+    for (int w = 0; w < NW; ++w) {
+        run += w < wv ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t v = fr[q];
+        fr[q] = run;
+        run += v;
+    }
+    if (t == 0) {
+        fr[nE] = tot;
+        if (blockIdx.y == 0) stats[l].ntri = tot;
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < nE; q += kPrepTabT) {  // length classes (short except on lattice-like inputs)
+        const uint32_t len = lens[q];
+        uint32_t a = q, b = q;
+        while (a > 0 && lens[a - 1] == len) --a;
+        while (b + 1 < nE && lens[b + 1] == len) ++b;
+        cl[q] = fr[a] | (fr[b + 1] << 16);
+        qt[q] = a | ((uint32_t)(b > a) << 16);
     }
     __syncthreads();
     EdgeRec* R = db.recs + lE;
