@@ -201,6 +201,30 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     }
 
 
+UMAP_DESC = ("UMAP before ripser (debug_tda_pipeline.py:96-104): 32 layers x 36 prompts x 4096 features, "
+             "n_neighbors 6, 3 components, min_dist 0.1, cosine, 500 epochs")
+
+
+def measure_umap(pkg, torch, dev, steps: int = 10, warmup: int = 2) -> dict:
+    """SURVEY 8(f) row 3 (outside the headline metric): the reference's UMAP
+    step for a 32-layer sweep on the GPU.  No CPU baseline: umap-learn is
+    absent here and the oracle restates only its fuzzy graph."""
+    X = torch.from_numpy(pkg.synthetic.activations(32, 36, 4096)).to(dev)
+    kw = dict(n_neighbors=6, n_components=3, min_dist=0.1, metric="cosine", random_state=42)
+    for _ in range(warmup):
+        pkg.umap_batch(X, **kw)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        pkg.umap_batch(X, **kw)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": 32 * steps / el, "unit": "layers/s", "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warmup,
+            "config": {"workload": UMAP_DESC, "layers_per_gpu_step": 32, "n_points": 36, "dim": 4096},
+            "data": DATA["raw4096"], "roofline": None,
+            "cpu_baseline": None, "note": "umap-learn is not installed here (no CPU reference to time); layout parity unpinned"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,7 +232,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
-    ap.add_argument("--extra", default="grid144,torus1024,raw4096",
+    ap.add_argument("--extra", default="grid144,torus1024,raw4096,umap36",
                     help="secondary workloads measured at N=1 (comma list, '' for none)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -298,6 +322,9 @@ def main():
             out["speedup_vs_cpu"] = {"all_cores": value / cb["value"], "one_core": value / cb["value_1core"]}
         out["workloads"] = {}
         for w in [w for w in args.extra.split(",") if w and w != args.workload]:
+            if w == "umap36":
+                out["workloads"][w] = measure_umap(pkg, torch, dev)
+                continue
             _, _, _, st, wu = WORKLOADS[w]
             m = measure(pkg, torch, dev, w, st, wu)
             rec = {k: m[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "device_ms_per_step",
