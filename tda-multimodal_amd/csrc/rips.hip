@@ -152,7 +152,8 @@ ReduceAllCfg reduce_cfg(int n, int maxdim, const uint64_t* piv_words, bool lds_m
     return c;
 }
 
-int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par) {
+// no_par: 0 = k_reduce_par for H1 and H2, 1 = H1 only (an H2 launch aborted), 2 = none
+int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par) {
     const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
     p.mst_words = (binom(N, 2) + 31) / 32 + 1;
     for (int d = 1; d <= p.maxdim; ++d) {
@@ -177,16 +178,16 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, bool no_par
         // 32 (tools/ab_reduce.py: grid144 md2 L=32 24.1 -> 6.8 ms, torus256
         // md2 L=32 926 -> 50 ms).  After a parallel abort (no_par) the old rule.
         const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big"), want_par = m && !strcmp(m, "par");
-        const bool par_ok = !no_par && p.maxdim >= 1 && !getenv_is("TDA_PAR", "0");
+        const bool par_ok = no_par < 2 && p.maxdim >= 1 && !getenv_is("TDA_PAR", "0");
         p.big = !p.lds_mode && (force_big || want_big || want_par || (!want_wave && (p.N > kBigMinN || par_ok)));
         // TDA_PAR=0: H1 on the serial k_reduce_big as well (comparison / debugging)
-        p.par = p.big && p.maxdim >= 1 && !no_par && !getenv_is("TDA_PAR", "0");
+        p.par = p.big && p.maxdim >= 1 && no_par < 2 && !getenv_is("TDA_PAR", "0");
         p.packed = p.N <= 1024;
         // C(N, 4) >= 2^32 (N > 568): the 32-bit index word of the H2 pivot keys
         // overflows; TDA_H2_WIDE=1 forces the wide keys on any big-path N (tests)
         p.wide = p.big && p.maxdim >= 2 && (binom(N, 4) >= (1ull << 32) || getenv_is("TDA_H2_WIDE", "1"));
         // TDA_PAR2=0: H2 on the serial radix-heap kernel after a parallel H1
-        p.par2 = p.par && p.maxdim >= 2 && !p.wide && !getenv_is("TDA_PAR2", "0");
+        p.par2 = p.par && p.maxdim >= 2 && no_par < 1 && !getenv_is("TDA_PAR2", "0");
         p.dense = p.lds_mode && p.maxdim >= 1 && p.N <= kDenseMaxN && p.N >= 3 && !want_wave;
     }
     if (p.dense) {  // carve of rips_reduce_small.h (h1_chain / h2_phase1), mirrored here
@@ -376,7 +377,8 @@ struct Workspace {
     struct Retry {
         int64_t N;
         int maxdim, input_kind;
-        bool force_global, force_big, no_par;
+        bool force_global, force_big;
+        int no_par;
         int scale;
     };
     std::vector<Retry> retry;
@@ -531,6 +533,7 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
+    HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_edge_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEdgeSortLds));
     HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
@@ -574,6 +577,7 @@ std::string err_flags(int e) {
     if (e & ERR_VPOOL_CAP) s += " reduction-pool-capacity";
     if (e & ERR_OUT_CAP) s += " output-capacity";
     if (e & ERR_STEP_LIMIT) s += " reduction-step-limit";
+    if (e & ERR_PAR2) s += " parallel-h2-reduction-abort";
     if (e & ERR_PAR) s += " parallel-reduction-abort";
     return s;
 }
@@ -581,7 +585,7 @@ std::string err_flags(int e) {
 // ------------------------------------------------------------------ pipeline
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
-                 bool force_global = false, int scale = 0, bool force_big = false, bool no_par = false) {
+                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0) {
     const auto h_entry = std::chrono::steady_clock::now();
     Plan p;
     p.L = a.L;
@@ -1093,15 +1097,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 const uint32_t* no_clr = nullptr;
                 if (p.packed)
                     hipLaunchKernelGGL((k_reduce_par<1, true>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], no_clr,
-                                       (uint64_t)0, rb, pb);
+                                       (uint64_t)0, rb, pb, gb.dcode, gb.dsort, gb.ecap);
                 else
                     hipLaunchKernelGGL((k_reduce_par<1, false>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], no_clr,
-                                       (uint64_t)0, rb, pb);
+                                       (uint64_t)0, rb, pb, gb.dcode, gb.dsort, gb.ecap);
                 HIPC(hipGetLastError());
                 MARK("k_reduce_par");
                 // H2 next: residual H1 pivots into the dim-1 bitmap (k_reduce_par<2>) or map (k_reduce_big)
                 hipLaunchKernelGGL(k_par_emit<1>, dim3(L), dim3(1024), 0, s, stats, db[1], rb, pb, pairs1, p.pcap[1],
-                                   p.maxdim < 2 ? 0 : p.par2 ? 2 : 1);
+                                   p.maxdim < 2 ? 0 : p.par2 ? 2 : 1, (const uint64_t*)nullptr, (uint64_t)0);
                 HIPC(hipGetLastError());
                 MARK("k_par_emit");
                 start_dim = 2;
@@ -1109,15 +1113,19 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                     HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                     hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[2], pb, 2);
                     HIPC(hipGetLastError());
-                    if (n <= kPar2PackedMaxN)
+                    if (p.wide)  // N > 568: edge-code keys (k_edge_codes ran above)
+                        hipLaunchKernelGGL((k_reduce_par<2, false, true>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats,
+                                           db[2], (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
+                    else if (n <= kPar2PackedMaxN)
                         hipLaunchKernelGGL((k_reduce_par<2, true>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[2],
-                                           (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb);
+                                           (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
                     else
                         hipLaunchKernelGGL((k_reduce_par<2, false>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[2],
-                                           (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb);
+                                           (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
                     HIPC(hipGetLastError());
                     MARK("k_reduce_par<2>");
-                    hipLaunchKernelGGL(k_par_emit<2>, dim3(L), dim3(1024), 0, s, stats, db[2], rb, pb, pairs2, p.pcap[2], 0);
+                    hipLaunchKernelGGL(k_par_emit<2>, dim3(L), dim3(1024), 0, s, stats, db[2], rb, pb, pairs2, p.pcap[2], 0,
+                                       p.wide ? gb.dsort : (const uint64_t*)nullptr, p.ecap);
                     HIPC(hipGetLastError());
                     MARK("k_par_emit<2>");
                     start_dim = 3;
@@ -1201,8 +1209,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     if (errs && getenv("TDA_DEBUG"))
         fprintf(stderr, "[tda] N=%d L=%d errs=%s force_global=%d scale=%d\n", n, L, err_flags(errs).c_str(), (int)force_global, scale);
-    if (errs & ERR_PAR) {
-        // k_reduce_par gave up (a capacity or spin limit): reduce H1 on the serial radix-heap kernel
+    if (errs & (ERR_PAR | ERR_PAR2)) {
+        // k_reduce_par gave up (a capacity or spin limit): reduce on the serial radix-heap kernel --
+        // everything after an H1 abort (ERR_PAR), only H2 after an H2 abort (ERR_PAR2 alone)
+        const int np_next = (errs & ERR_PAR) ? 2 : std::max(no_par, 1);
         ParCtl c;
         HIPC(hipMemcpy(&c, B + p.o_pctl, sizeof(c), hipMemcpyDeviceToHost));
         if (getenv("TDA_DEBUG"))
@@ -1212,13 +1222,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         const bool capacity = code == 21 || code == 22 || code == 41 || code == 53;  // pools / requeue slots
         if (capacity && scale < 2) {  // the same parallel reduction with larger pools
             guard.unlock();
-            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, false);
+            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par);
         }
         if (getenv_is("TDA_PAR_STRICT", "1"))  // tests: the parallel path itself must succeed
             return fail(TDA_E_CAPACITY, "k_reduce_par aborted: item " + std::to_string(c.err >> 16) + " code " +
                                             std::to_string(code));
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, true);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, np_next);
     }
     if ((errs & ERR_LDS_SPILL) && !force_global) {
         // a working column outgrew LDS: redo the batch with global-memory tables
@@ -1313,7 +1323,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             if (m.N == p.N && m.maxdim == p.maxdim && m.input_kind == input_kind) {
                 m.force_global = m.force_global || force_global;
                 m.force_big = m.force_big || force_big;
-                m.no_par = m.no_par || no_par;
+                m.no_par = std::max(m.no_par, no_par);
                 m.scale = std::max(m.scale, scale);
                 seen = true;
             }
@@ -1452,7 +1462,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 
 // entry: start from the configuration an earlier call of this shape ended on
 int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_result** out) {
-    bool fg = false, fb = false, np = false;
+    bool fg = false, fb = false;
+    int np = 0;
     int sc = 0;
     // not when a test forces a reducer (the memo would override what it asks for)
     if (!getenv_is("TDA_RETRY_MEMO", "0") && !getenv("TDA_REDUCE") && !getenv("TDA_PAR") && !getenv("TDA_PAR_STRICT") &&

@@ -62,7 +62,9 @@ constexpr uint64_t kParEss = kEmpty64;        // colpiv: essential (zero column)
 constexpr uint64_t kParSkip = kEmpty64 - 1;   // colpiv: cleared column (H0 death)
 constexpr uint32_t kParSpin = 1u << 22;       // polls before a wait on another workgroup is declared hung
 
-enum : int32_t { ERR_PAR = 128 };  // k_reduce_par aborted: the host falls back to k_reduce_big
+// k_reduce_par aborted: the host falls back to k_reduce_big (ERR_PAR: the H1
+// launch, everything is redone serially; ERR_PAR2: only the H2 launch)
+enum : int32_t { ERR_PAR = 128, ERR_PAR2 = 256 };
 
 struct ParCtl {  // zeroed by k_par_init
     unsigned long long next;     // next fresh item
@@ -146,6 +148,7 @@ struct ParLds {
     uint32_t last;  // radix reference (diameter bits)
     uint32_t kf;    // front holds levels 0..kf
     int32_t err;
+    uint32_t wide;  // wide H2 keys: the low 32 bits (index fingerprint) are not unique -> verify hits
 };
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
@@ -290,7 +293,8 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
 #pragma unroll
             for (int u = 7; u >= 0; --u) {  // first empty / first match, branch-free selects
                 if (ev[u] == 0) empty = u;
-                if (ev[u] != 0 && (uint32_t)(ev[u] >> 32) == fp) found = u, fe = ev[u];
+                if (ev[u] != 0 && (uint32_t)(ev[u] >> 32) == fp && (!PS.wide || (PS.log[(uint32_t)ev[u] - 1] & ~kDead) == kk))
+                    found = u, fe = ev[u];
             }
             if (empty >= 0 && found > empty) found = -1;  // slots fill in order: nothing lives past the first empty
             if (found >= 0) {  // present: flip it (this entry stays dead)
@@ -305,7 +309,7 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
             const uint64_t old = atomicCAS((unsigned long long*)&PS.idx[bo + empty], 0ull, (unsigned long long)mine);
             if (old == 0) break;  // inserted
             PS.log[pos] = kk | kDead;
-            if ((uint32_t)(old >> 32) == fp) {  // the same key, inserted by another copy of this pass
+            if ((uint32_t)(old >> 32) == fp && (!PS.wide || (PS.log[(uint32_t)old - 1] & ~kDead) == kk)) {  // the same key, inserted by another copy of this pass
                 __hip_atomic_fetch_xor(&PS.log[(uint32_t)old - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 break;
             }
@@ -708,11 +712,14 @@ __device__ __forceinline__ uint32_t tet_lo(uint64_t idx, int f) {
 
 // toggle the coboundary of triangle (a > b > c), diameter sd, into the column
 // (no barrier; the caller made room).  Round 0's rows may be prefetched (r0).
-template <bool PACKED>
+// WIDE (N > 568): D holds the layer's edge CODES (bit patterns in float
+// slots), sd is the triangle's code, keys are code << 42 | (2^42 - 1 - index).
+template <bool PACKED, bool WIDE = false>
 __device__ __forceinline__ void col_cob2(ParCol& C, const ParBufs& P, const float* __restrict__ D, int n, float r, int a, int b, int c,
                                          float sd, const float (&r0)[3][kParRV], ParStash* stash = nullptr) {
     // the triangle's own edges (facet diameters of its cofacets)
-    const float eab = ld_glb(D, (size_t)a * n + b), eac = ld_glb(D, (size_t)a * n + c), ebc = ld_glb(D, (size_t)b * n + c);
+    const float eab = WIDE ? 0.0f : ld_glb(D, (size_t)a * n + b), eac = WIDE ? 0.0f : ld_glb(D, (size_t)a * n + c),
+                ebc = WIDE ? 0.0f : ld_glb(D, (size_t)b * n + c);
     const int vs[3] = {a, b, c};
     for (int v0 = 0; v0 < n; v0 += kParT * kParRV) {
         float da[kParRV], db[kParRV], dc[kParRV];
@@ -737,6 +744,13 @@ __device__ __forceinline__ void col_cob2(ParCol& C, const ParBufs& P, const floa
             const int v = v0 + (int)threadIdx.x + q * kParT;
             key[q] = 0;
             if (v >= n || v == a || v == b || v == c) continue;
+            if constexpr (WIDE) {
+                const uint32_t cc = max(max(__float_as_uint(sd), __float_as_uint(da[q])), max(__float_as_uint(db[q]), __float_as_uint(dc[q])));
+                if (cc >= kCodeInf) continue;
+                key[q] = ((uint64_t)cc << kWideIdxBits) | (kWideIdxMask - cofacet_index<2>(vs, v));
+                vm |= 1u << q;
+                continue;
+            }
             const float cd = fmaxf(fmaxf(sd, da[q]), fmaxf(db[q], dc[q]));
             if (!(cd <= r)) continue;
             // facet diameters: omitting v -> sd; a -> (b,c,v); b -> (a,c,v); c -> (a,b,v)
@@ -903,14 +917,21 @@ __device__ __forceinline__ uint64_t par_omask(uint64_t nres, uint64_t ostride) {
 // columns, tetrahedron rows (PACKED: N <= 400); a triangle is cleared when it
 // is any H1 pivot: `clr` is the dim-1 pivot bitmap, which k_par_emit<1> has
 // completed with the residual H1 pivots.
-template <int DIM, bool PACKED>
+// WIDE (DIM 2, N > 568): rows keyed by edge codes (see rips_reduce_big.h):
+// dcode / dsort / ecap from k_edge_sort / k_edge_codes.
+template <int DIM, bool PACKED, bool WIDE = false>
 __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ dist, int n, int L, LayerStats* __restrict__ stats,
                                                       DimBufs b1, const uint32_t* __restrict__ clr, uint64_t clr_words, Reduce2Bufs rb,
-                                                      ParBufs P) {
+                                                      ParBufs P, const uint32_t* __restrict__ dcode, const uint64_t* __restrict__ dsort,
+                                                      uint64_t ecap) {
+    static_assert(!WIDE || (DIM == 2 && !PACKED), "wide keys: unpacked H2 rows only");
     ParCol C;
     const int tid = threadIdx.x;
     for (uint32_t e = tid; e < 33u * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
-    if (tid == 0) PS.err = 0;
+    if (tid == 0) {
+        PS.err = 0;
+        PS.wide = WIDE ? 1u : 0u;
+    }
     __syncthreads();
     const uint64_t total = ald(&P.ctl->total);
     bool prealloc = false;
@@ -958,6 +979,8 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         LayerStats* st = stats + l;
         const float r = st->thresh;
         const float* D = dist + (size_t)l * n * n;
+        // rows the coboundaries read: distances, or (WIDE) edge codes in float slots
+        const float* Dr = WIDE ? (const float*)(dcode + (size_t)l * n * n) : D;
         const uint64_t* resid = b1.resid + (size_t)l * b1.rcap;
         const uint32_t* pivg = b1.pivbits + (size_t)l * b1.piv_words;
         const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
@@ -997,9 +1020,14 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             prealloc = true;
         }
         for (uint32_t q = tid; q < 33; q += kParT) PS.bcnt[q] = 0;
+        uint32_t sc = 0;  // WIDE: the column's edge code
+        if constexpr (WIDE) {
+            const uint32_t* Dc = (const uint32_t*)Dr;
+            sc = max(ld_glb(Dc, (size_t)sv[0] * n + sv[1]), max(ld_glb(Dc, (size_t)sv[0] * n + sv[2]), ld_glb(Dc, (size_t)sv[1] * n + sv[2])));
+        }
         if (tid == 0) {
             PS.kf = 32;
-            PS.last = __float_as_uint(sdm + 0.0f);
+            PS.last = WIDE ? (uint32_t)(((uint64_t)sc << kWideIdxBits) >> 32) : __float_as_uint(sdm + 0.0f);
         }
         front_reset();
         if (!rec0) {
@@ -1008,12 +1036,12 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             for (int q = 0; q < kParRV; ++q) {
                 const int v = tid + q * kParT;
 #pragma unroll
-                for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(D, (size_t)sv[i] * n + v) : 0.0f;
+                for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(Dr, (size_t)sv[i] * n + v) : 0.0f;
             }
             if constexpr (DIM == 1)
                 col_cob<PACKED>(C, P, D, n, r, sv[0], sv[1], sdm, z[0], z[1]);
             else
-                col_cob2<PACKED>(C, P, D, n, r, sv[0], sv[1], sv[2], sdm, z);
+                col_cob2<PACKED, WIDE>(C, P, Dr, n, r, sv[0], sv[1], sv[2], WIDE ? __uint_as_float(sc) : sdm, z);
         } else {
             if (tid == 0) PS.last = (uint32_t)(ald(P.rec + (rec0 - 1) * 4 + 2) >> 32);
             __syncthreads();
@@ -1067,7 +1095,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             int fv[DIM + 1];
             uint64_t pidx;
             const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
-            const float pd = __uint_as_float((uint32_t)(pk >> 32));
+            const float pd = WIDE ? __uint_as_float((uint32_t)ld_glb(dsort + (size_t)l * ecap, pk >> kWideIdxBits))
+                                  : __uint_as_float((uint32_t)(pk >> 32));
+            uint32_t fsc = 0;  // WIDE: the facet's edge code
             if constexpr (DIM == 1) {
                 int t[3];
                 if (PACKED) {
@@ -1082,6 +1112,11 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                     pidx = plo;
                     (void)apparent_facet<1>(D, n, pidx, fv);
                 }
+            } else if constexpr (WIDE) {
+                pidx = kWideIdxMask - (pk & kWideIdxMask);
+                (void)apparent_facet<2>(D, n, pidx, fv);
+                const uint32_t* Dc = (const uint32_t*)Dr;
+                fsc = max(ld_glb(Dc, (size_t)fv[0] * n + fv[1]), max(ld_glb(Dc, (size_t)fv[0] * n + fv[2]), ld_glb(Dc, (size_t)fv[1] * n + fv[2])));
             } else {
                 if (PACKED) {
                     pidx = plo >> 2;
@@ -1102,7 +1137,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             for (int q = 0; q < kParRV; ++q) {
                 const int v = tid + q * kParT;
 #pragma unroll
-                for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(D, (size_t)fv[i] * n + v) : 0.0f;
+                for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(Dr, (size_t)fv[i] * n + v) : 0.0f;
             }
             // every thread reads the pivot's bitmap word (one address per wave): no barrier
             const uint32_t pw = ld_glb(pivg, pidx >> 5);
@@ -1116,7 +1151,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 if constexpr (DIM == 1)
                     col_cob<PACKED>(C, P, D, n, r, fv[0], fv[1], pd, z[0], z[1], &stash);
                 else
-                    col_cob2<PACKED>(C, P, D, n, r, fv[0], fv[1], fv[2], pd, z, &stash);
+                    col_cob2<PACKED, WIDE>(C, P, Dr, n, r, fv[0], fv[1], fv[2], WIDE ? __uint_as_float(fsc) : pd, z, &stash);
                 ++adds;
 #ifdef TDA_PROFILE
                 pf[3] += clock64() - t0;
@@ -1124,7 +1159,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 continue;
             }
             // ---------------- residual pivot: owner map
-            const uint64_t fkey = filt_key(pd, pidx);
+            const uint64_t fkey = WIDE ? pk : filt_key(pd, pidx);  // colpiv: k_par_emit decodes it
             for (uint32_t round = 0;; ++round) {
                 if (tid == 0) {
                     uint64_t slot = 0;
@@ -1253,7 +1288,8 @@ __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats
 // dim-1 pivot bitmap (k_reduce_par<2>).
 template <int DIM>
 __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stats, DimBufs b1, Reduce2Bufs rb, ParBufs P,
-                                                   Pair* __restrict__ pairs, uint64_t pcap, int fill_map) {
+                                                   Pair* __restrict__ pairs, uint64_t pcap, int fill_map,
+                                                   const uint64_t* __restrict__ dsort = nullptr, uint64_t ecap = 0) {
     __shared__ uint64_t red[3][16];
     const int l = blockIdx.x, tid = threadIdx.x;
     LayerStats* st = stats + l;
@@ -1289,8 +1325,9 @@ __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stat
                 else atomicOr(&st->err, ERR_PAIR_CAP);
                 continue;
             }
-            const uint64_t pidx = 0xFFFFFFFFull - (cp & 0xFFFFFFFFull);
-            const float pd = __uint_as_float((uint32_t)(cp >> 32));
+            // colpiv: filtration key, or (dsort given) a wide code key
+            const uint64_t pidx = dsort ? kWideIdxMask - (cp & kWideIdxMask) : 0xFFFFFFFFull - (cp & 0xFFFFFFFFull);
+            const float pd = dsort ? __uint_as_float((uint32_t)dsort[(size_t)l * ecap + (cp >> kWideIdxBits)]) : __uint_as_float((uint32_t)(cp >> 32));
             if (pd > sdm) {
                 const uint64_t pos = atomicAdd((unsigned long long*)&st->count[DIM], 1ull);
                 if (pos < pcap) store_pair(Pp, pos, sdm, pd, (int64_t)sidx, (int64_t)pidx);
@@ -1315,7 +1352,7 @@ __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stat
         uint64_t a = 0, b = 0, c = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) a += red[0][w], b += red[1][w], c += red[2][w];
         if (failed) {
-            atomicOr(&st->err, ERR_PAR);
+            atomicOr(&st->err, DIM == 1 ? ERR_PAR : ERR_PAR2);
         } else {
             atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)a);
             atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)b);

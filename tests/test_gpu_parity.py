@@ -365,12 +365,13 @@ def test_parallel_h2_reduction_vs_oracle(gpu, oracle, monkeypatch, case):
         assert_same(res[l], orc[l], 2, f"{case} layer {l}")
 
 
-@pytest.mark.parametrize("name", ["torus500", "torus600", "torus1024"])
-def test_h2_above_568_vs_committed_oracle(gpu, name):
+@pytest.mark.parametrize("name,par2", [("torus500", "1"), ("torus600", "1"), ("torus1024", "1"), ("torus600", "0")])
+def test_h2_above_568_vs_committed_oracle(gpu, monkeypatch, name, par2):
     """H0-H2 where tetrahedron indices exceed 32 bits (C(N,4) >= 2^32 above
     N = 568): the radix-heap H2 reduction on wide edge-code keys against the
     committed oracle runs (make_golden_large.py --h2-only); torus1024 is C4's
     cloud at maxdim 2 (S^1 x S^1: one dominant H2 class)."""
+    monkeypatch.setenv("TDA_PAR2", par2)  # 0: H2 on the serial radix heap (wide keys above N = 568)
     z = np.load(os.path.join(GOLDEN, "large_h2.npz"))
     X = z[f"{name}__X"]
     res = gpu.ripser_batch(X, maxdim=2)
@@ -379,12 +380,15 @@ def test_h2_above_568_vs_committed_oracle(gpu, name):
     assert pers[0] > 2.0 * pers[1]
 
 
-@pytest.mark.parametrize("wide", ["0", "1"])
-def test_h2_wide_keys_forced_vs_oracle(gpu, oracle, monkeypatch, wide):
+@pytest.mark.parametrize("wide,par2", [("0", "1"), ("1", "1"), ("0", "0"), ("1", "0")])
+def test_h2_wide_keys_forced_vs_oracle(gpu, oracle, monkeypatch, wide, par2):
     """The wide edge-code keys forced below N = 568 (TDA_H2_WIDE=1) must give
     what the 32-bit keys give: the same pairs, indices and checksums as the
-    oracle, on the big-path H2 reduction (N = 300)."""
+    oracle (N = 300), on the parallel H2 reduction and (TDA_PAR2=0) on the
+    serial radix heap; TDA_PAR_STRICT=1: no silent serial re-run."""
     monkeypatch.setenv("TDA_H2_WIDE", wide)
+    monkeypatch.setenv("TDA_PAR2", par2)
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")
     X = gpu.synthetic.torus(300, seed=0)
     res = gpu.ripser_batch(X[None], maxdim=2)[0]
     assert_same(res, oracle.rips(X, maxdim=2), 2, f"torus300 wide={wide}")
