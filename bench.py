@@ -42,17 +42,21 @@ WORKLOADS = {
     "sweep48": (32, 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2", 50, 5),
     "grid144": (32, 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2", 10, 2),
     "torus1024": (1, 1, "S1xS1 torus N=1024 (configs[3]), D=3, H0-H1", 5, 2),
+    # four sweeps per call (128 layers): the same per-layer work, a larger batch -- the
+    # latency-bound 32-layer step leaves most CUs idle (throughput capacity, not the headline)
+    "sweep48x4": (128, 2, "4 x the qwen-vl 32-layer sweep x 48 points in one call (128 layers), D=3, H0-H2", 50, 5),
     # raw hidden states (no UMAP): distance on the FP64 matrix cores + TwoNN + H0
     "raw4096": (32, 0, "32 layers x 144 tokens x 4096 raw hidden-state features: distance (FP64 MFMA) + H0 + TwoNN "
                        "intrinsic dimension (metrics.py:113-208)", 20, 3),
 }
 DATA = {
     "sweep48": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
+    "sweep48x4": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
     "grid144": "synthetic: 12x12 grid on the torus + N(0, 0.02^2) + random rotation per layer",
     "torus1024": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 0",
     "raw4096": "synthetic: activation-like f32 clouds (heavy-tailed feature scales, offsets, outlier features)",
 }
-NPOINTS = {"sweep48": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
+NPOINTS = {"sweep48": 48, "sweep48x4": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
 CALL_KW = {"raw4096": {"twonn": True}}
 
 
@@ -64,7 +68,7 @@ def algo_bytes_per_layer(n: int, d: int, maxdim: int) -> int:
 def make_workload(name: str, layers: int | None = None):
     syn = importlib.import_module("tda-multimodal_amd.synthetic")
     L = layers or WORKLOADS[name][0]
-    if name == "sweep48":
+    if name in ("sweep48", "sweep48x4"):
         return syn.sweep48(L)
     if name == "grid144":
         return syn.sweep144(L)
@@ -232,7 +236,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
-    ap.add_argument("--extra", default="grid144,torus1024,raw4096,umap36",
+    ap.add_argument("--extra", default="grid144,torus1024,raw4096,umap36,sweep48x4",
                     help="secondary workloads measured at N=1 (comma list, '' for none)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
