@@ -258,13 +258,20 @@ def main():
 
     import torch
 
+    # one GPU per rank; more ranks than GPUs only in a rehearsal (TDA_DIST_BACKEND=gloo on a 1-GPU box)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
+    backend = os.environ.get("TDA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+    coll_dev = dev if backend == "nccl" else None         # gloo: collectives on host tensors
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     pkg = importlib.import_module("tda-multimodal_amd")
     if pkg.lib().tda_device_ok(local) != 1:
         raise RuntimeError("no gfx950 device")
@@ -281,15 +288,15 @@ def main():
         def run_multi(shard: bool):
             torch.cuda.synchronize()
             for _ in range(args.warmup):
-                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=dev, shard=shard)
+                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=coll_dev, shard=shard)
             dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(args.steps):
-                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=dev, shard=shard)
+                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=coll_dev, shard=shard)
             torch.cuda.synchronize()
             dist.barrier()
-            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks
             return float(t.item())
 
@@ -309,7 +316,7 @@ def main():
             "config": {"workload": desc, "layers_per_gpu_step": L if args.scaling == "weak" else -(-L // world),
                        "n_points": NPOINTS[args.workload], "dim": 3, "maxdim": maxdim,
                        "parallelism": f"layers sharded ({args.scaling}), {world} process(es) x 1 GPU, "
-                                      f"RCCL gather of per-layer records"},
+                                      f"{'RCCL' if backend == 'nccl' else backend} gather of per-layer records"},
             "roofline": prim["roofline"] if prim else None,
             "cpu_baseline": None,
         }
