@@ -292,8 +292,11 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            # every step's records are exchanged; the exchange of step i overlaps the GPU work of step i + 1
+            pipe = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard)
             for _ in range(args.steps):
-                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=coll_dev, shard=shard)
+                pipe.step()
+            pipe.close()
             torch.cuda.synchronize()
             dist.barrier()
             t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
@@ -316,7 +319,8 @@ def main():
             "config": {"workload": desc, "layers_per_gpu_step": L if args.scaling == "weak" else -(-L // world),
                        "n_points": NPOINTS[args.workload], "dim": 3, "maxdim": maxdim,
                        "parallelism": f"layers sharded ({args.scaling}), {world} process(es) x 1 GPU, "
-                                      f"{'RCCL' if backend == 'nccl' else backend} gather of per-layer records"},
+                                      f"{'RCCL' if backend == 'nccl' else backend} gather of per-layer records "
+                                      f"(overlapped with the next step's GPU work)"},
             "roofline": prim["roofline"] if prim else None,
             "cpu_baseline": None,
         }

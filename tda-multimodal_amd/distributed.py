@@ -131,3 +131,65 @@ def sharded_sweep_step(X, maxdim: int, rank: int, world: int, dist=None, device=
     packed, cap = pack_results(res, ids, maxdim)
     out = gather_packed(packed, cap, total, dist, device)
     return out if out is not None else (None, None)
+
+
+class PipelinedSweep:
+    """Multi-GPU steps with each step's record exchange overlapped with the
+    next step's GPU work (what ``bench.py --gpus N`` times).
+
+    The calling thread runs the persistence of step i + 1 (the ctypes call
+    releases the GIL while the GPU works); one worker thread packs step i's
+    records and runs its two collectives (capacity all-reduce, record gather),
+    strictly in step order, so every rank issues the same collective sequence.
+    ``close()`` waits for the last exchange and returns its rows (rank 0).
+    Same arguments and per-step result as :func:`sharded_sweep_step`.
+    """
+
+    def __init__(self, X, maxdim: int, rank: int, world: int, dist=None, device=None, layer_base: int = 0,
+                 shard: bool = True, run=None, depth: int = 2):
+        import queue
+        import threading
+
+        from .ripser import ripser_batch
+
+        self.X, self.maxdim, self.dist, self.device = X, maxdim, dist, device
+        self.run = run or ripser_batch
+        L = int(X.shape[0])
+        if shard:
+            self.lo, self.hi = shard_range(L, rank, world)
+            self.total = L
+        else:
+            self.lo, self.hi = 0, L
+            self.total = L * world
+        self.ids = np.arange(self.lo, self.hi) + (layer_base if shard else rank * L)
+        self.q = queue.Queue(maxsize=max(1, depth))
+        self.last, self.err, self.steps = (None, None), None, 0
+        self.thread = threading.Thread(target=self._worker, daemon=True)
+        self.thread.start()
+
+    def _worker(self):
+        while True:
+            res = self.q.get()
+            if res is None:
+                return
+            try:
+                packed, cap = pack_results(res, self.ids, self.maxdim)
+                out = gather_packed(packed, cap, self.total, self.dist, self.device)
+                self.last = out if out is not None else (None, None)
+            except BaseException as e:  # re-raised by close()
+                self.err = e
+                return
+
+    def step(self):
+        if self.err is not None:
+            raise self.err
+        res = self.run(self.X[self.lo:self.hi], maxdim=self.maxdim) if self.hi > self.lo else []
+        self.q.put(res)  # blocks while the worker is `depth` exchanges behind
+        self.steps += 1
+
+    def close(self):
+        self.q.put(None)
+        self.thread.join()
+        if self.err is not None:
+            raise self.err
+        return self.last

@@ -63,6 +63,14 @@ def _worker(rank, world, port, q, case):
         g = pkg.distributed.gather_records(recs, 5)
         if rank == 0:
             out["dict"] = g
+    elif case == "pipelined":  # bench.py's timed loop: exchange of step i overlapped with step i + 1
+        clouds = pkg.synthetic.reference_clouds()
+        sweep = pkg.distributed.PipelinedSweep(clouds, 1, rank, world, run=_oracle_run)
+        for _ in range(3):
+            sweep.step()
+        rows, cap = sweep.close()
+        if rank == 0:
+            out["pipelined"] = ([pipe.unpack_record(v, cap) for v in rows], sweep.steps)
     else:  # many H1 bars on one rank only: the capacity all-reduce re-pads the other
         X = np.stack([pkg.synthetic.torus(260, seed=7), _circle(260)])
         rows, cap = pkg.distributed.sharded_sweep_step(X, 1, rank, world, run=_oracle_run)
@@ -107,3 +115,10 @@ def test_two_rank_step_carries_every_value(pkg, oracle):
     assert exp["n_h1_features"] > 64 and cap >= exp["n_h1_features"]
     assert recs[0] == exp
     assert recs[1] == pkg.layer_record(1, oracle.rips(_circle(260), maxdim=1)["dgms"])
+
+
+def test_two_rank_pipelined_steps_match_reference(summary_stats):
+    """The overlapped multi-step loop the bench times: three steps, the last
+    exchange (returned by close()) equals the reference's summary records."""
+    recs, steps = _run("pipelined")["pipelined"]
+    assert steps == 3 and recs == summary_stats
