@@ -12,9 +12,12 @@ mkdir -p gpurun_out
 for C in FETCH_SIZE WRITE_SIZE; do
     rm -rf gpurun_out/pmc_$C
     timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_$C -o run -- \
-        python3 bench.py --workload $WL --steps 5 --warmup 1 --no-cpu > gpurun_out/pmc_$C.txt 2>&1
+        python3 bench.py --workload $WL --steps 5 --warmup 1 --no-cpu --extra "" > gpurun_out/pmc_$C.txt 2>&1
     rc=$?
     echo "pmc $C rc=$rc"
     if [ $rc -ne 0 ]; then tail -20 gpurun_out/pmc_$C.txt; exit $rc; fi
 done
-python3 tools/pmc_parse.py --workload $WL gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE
+python3 tools/pmc_parse.py --workload $WL gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE > /dev/null
+rc=$?
+cp profiles/pmc_$WL.json gpurun_out/ 2>/dev/null  # gpurun merges gpurun_out/ back, not profiles/
+exit $rc
