@@ -168,6 +168,10 @@ class PipelinedSweep:
         self.thread.start()
 
     def _worker(self):
+        if self.device is not None and getattr(self.device, "type", None) == "cuda":
+            import torch
+
+            torch.cuda.set_device(self.device)  # the current device is per thread
         while True:
             res = self.q.get()
             if res is None:
