@@ -961,6 +961,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     static const int order = getenv("TDA_ORDER") ? atoi(getenv("TDA_ORDER")) : 3;  // 3: measured best (r01)
     if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
+    const bool h2_side = !p.dense && p.par && p.par2 && p.maxdim >= 2;
     auto launch_h2_columns = [&]() -> int {  // apparent<2> + their sort on the third stream
         if (int rc = tm3.begin()) return rc;
         launch_apparent(2, w.stream3);
@@ -995,6 +996,22 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 HIPC(hipGetLastError());
                 MARK("k_sort_resid<1>");
             }
+        } else if (h2_side) {
+            // parallel H1 and H2: the H2 columns' apparent pass and sort run on
+            // the third stream beside the H1 reduction (k_reduce_par<2> joins
+            // them).  k_par_emit<1> may OR residual H1 pivots into the bitmap
+            // k_apparent<2> reads as its clearing test while it runs: a triangle
+            // seen cleared is skipped there, otherwise it becomes a residual
+            // column that k_reduce_par<2> skips -- never an apparent pair (a
+            // cleared triangle is an H1 death, and apparent pairs are
+            // persistence pairs), so pairs and checksums do not depend on the race.
+            HIPC(hipEventRecord(w.evs, s));
+            HIPC(hipStreamWaitEvent(w.stream3, w.evs, 0));
+            if (int rc = launch_h2_columns()) return rc;
+            HIPC(hipEventRecord(w.evp, w.stream3));
+            launch_sort(1, 1, s);
+            HIPC(hipGetLastError());
+            MARK("k_sort_resid<1>");
         } else {
             for (int d = 2; d <= p.maxdim; ++d) {
                 launch_apparent(d, s);
@@ -1110,6 +1127,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 MARK("k_par_emit");
                 start_dim = 2;
                 if (p.par2) {  // H2 columns on the same workers (an H1 abort skips it: k_par_init keeps the flag)
+                    if (h2_side) HIPC(hipStreamWaitEvent(s, w.evp, 0));  // join: H2 columns (third stream)
                     HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                     hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[2], pb, 2);
                     HIPC(hipGetLastError());
