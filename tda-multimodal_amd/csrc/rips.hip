@@ -807,12 +807,17 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             int T = n <= 256 ? 256 : 1024;
             size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
             base = align_up(base, 16);
-            size_t avail = kLdsMax - base;
+            // n <= kH0WaveMaxN: one-wave Prim on the LDS-staged matrix (sort chunk just covers the forest)
+            const bool dlds = n <= kH0WaveMaxN && !getenv_is("TDA_H0_WAVE", "0");
+            size_t avail = kLdsMax - base - (dlds ? (size_t)4 * n * n : 0);
             uint64_t ch = 1;
-            while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
-            size_t lds = base + ch * 8;
+            if (dlds)
+                ch = next_pow2((uint64_t)n);
+            else
+                while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
+            size_t lds = base + ch * 8 + (dlds ? (size_t)4 * n * n : 0);
             hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
-                               (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
+                               (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch), dlds ? 1 : 0);
         }
         HIPC(hipGetLastError());
         if (int rc = tm4.mark("k_h0")) return rc;

@@ -441,10 +441,20 @@ __device__ void block_sort(uint64_t* keys, uint32_t* vals, uint64_t n, uint64_t*
 // elder-rule union-find [upstream compute_dim_0_pairs], consumed at
 // debug_tda_pipeline.py:112, :126.
 // LDS: best[N] u64, intree[N] u8 ... par[N] int  (N <= 8192)
+//
+// n <= kH0WaveMaxN (64 < n, the dense path has k_h0_wave below): the layer's
+// matrix is staged in LDS after the sort chunk and Prim runs on wave 0 alone
+// -- lane l owns vertices l, l + 64, l + 128; the frontier keys live in
+// registers and a step is an LDS row read + a DPP wave minimum, no block
+// barriers; the threshold and edge count read the LDS copy too (r02:
+// 32 x N=144 layers 0.47 -> 0.30 ms; the sequential thread-0 elder-rule
+// pass that follows is not parallelised yet).
+constexpr int kH0WaveMaxN = 190;  // 4 n^2 B of LDS staging
+constexpr int kH0WaveQ = (kH0WaveMaxN + 63) / 64;
 __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int n, float user_thresh,
                                              LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
                                              uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0,
-                                             uint64_t* __restrict__ scratch /* [L][2n] */, int sort_log2) {
+                                             uint64_t* __restrict__ scratch /* [L][2n] */, int sort_log2, int dlds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, T = blockDim.x, t = threadIdx.x;
     const float* Dl = dist + (size_t)l * n * n;
@@ -458,6 +468,11 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     uint64_t* red = (uint64_t*)(par + ((n + 1) & ~1));    // 32 wave partials + 8
     uint64_t* sk = red + 40;                              // sort chunk
     const int nw = T >> 6, w = t >> 6, ln = t & 63;
+    float* Ds = (float*)(sk + (1ull << sort_log2));       // dlds: the layer's matrix
+    if (dlds) {
+        stage_to_lds(Ds, Dl, 4ull * n * n, t, T);
+        __syncthreads();
+    }
 
     // -- threshold
     float thr = user_thresh;
@@ -465,7 +480,7 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         float local = INFINITY;
         for (int i = w; i < n; i += nw) {
             float r = -INFINITY;
-            for (int j = ln; j < n; j += 64) r = fmaxf(r, Dl[(size_t)i * n + j]);
+            for (int j = ln; j < n; j += 64) r = fmaxf(r, dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]);
             for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
             local = fminf(local, r);
         }
@@ -485,7 +500,7 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     {
         unsigned long long c = 0;
         for (int i = w; i < n; i += nw)
-            for (int j = i + 1 + ln; j < n; j += 64) c += Dl[(size_t)i * n + j] <= thr;
+            for (int j = i + 1 + ln; j < n; j += 64) c += (dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]) <= thr;
         atomicAdd(&s_cnt, c);
     }
     // -- Prim
@@ -503,7 +518,56 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     __syncthreads();
     uint64_t* mst = scratch + (size_t)l * 2 * n;  // MST edge keys
     int nmst = 0;
-    for (int it = 1; it < n; ++it) {
+    if (dlds) {  // one-wave Prim on the LDS matrix
+        if (w == 0) {
+            uint64_t bst[kH0WaveQ];
+            bool in[kH0WaveQ];
+#pragma unroll
+            for (int q = 0; q < kH0WaveQ; ++q) {
+                bst[q] = kEmpty64;
+                in[q] = ln + 64 * q >= n || (ln == 0 && q == 0);  // vertex 0 starts the tree
+            }
+            int cur = 0;
+            for (int it = 1; it < n; ++it) {
+                uint64_t mk = kEmpty64;
+#pragma unroll
+                for (int q = 0; q < kH0WaveQ; ++q) {
+                    const int v = ln + 64 * q;
+                    if (in[q]) continue;
+                    const float d = ld_lds(Ds, (size_t)cur * n + v);
+                    if (d <= thr) {
+                        const int a = cur > v ? cur : v, b = cur > v ? v : cur;
+                        const uint64_t k = filt_key(d, binom((uint64_t)a, 2) + b);
+                        bst[q] = k < bst[q] ? k : bst[q];
+                    }
+                    mk = bst[q] < mk ? bst[q] : mk;
+                }
+                const uint64_t gmin = wave_min_u64(mk);
+                if (gmin == kEmpty64) {  // new component: the smallest vertex not in the forest
+                    uint32_t sv = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int q = kH0WaveQ - 1; q >= 0; --q)
+                        if (!in[q]) sv = (uint32_t)(ln + 64 * q);
+                    cur = (int)wave_min_u32(sv);
+                } else {  // the owner of the minimum key joins (keys are unique)
+                    int nv = 0x7FFFFFFF;
+#pragma unroll
+                    for (int q = 0; q < kH0WaveQ; ++q)
+                        if (!in[q] && bst[q] == gmin) nv = ln + 64 * q;
+                    cur = (int)wave_min_u32((uint32_t)nv);
+                    if (ln == 0) mst[nmst] = gmin;
+                    ++nmst;
+                }
+#pragma unroll
+                for (int q = 0; q < kH0WaveQ; ++q)
+                    if (ln + 64 * q == cur) in[q] = true;
+            }
+        }
+        if (w == 0 && ln == 0) red[34] = (uint64_t)nmst;
+        __syncthreads();
+        nmst = (int)red[34];
+    }
+    for (int it = 1; it < (dlds ? 0 : n); ++it) {
         const int cur = s_cur;
         uint64_t mk = kEmpty64;
         for (int v = t; v < n; v += T) {
