@@ -624,6 +624,73 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         uint64_t eidx = 0xFFFFFFFFull - (mst[e] & 0xFFFFFFFFull);
         atomicOr(&mst_bits[(size_t)l * mst_words + (eidx >> 5)], 1u << (eidx & 31));
     }
+    if (dlds) {  // elder rule on wave 0: lane l holds the component labels (= max vertex) of vertices l, l + 64, l + 128
+        if (w == 0) {
+            int label[kH0WaveQ];
+#pragma unroll
+            for (int q = 0; q < kH0WaveQ; ++q) label[q] = ln + 64 * q;
+            auto lab_of = [&](int v) -> int {  // v wave-uniform
+                int x = label[0];
+#pragma unroll
+                for (int q = 1; q < kH0WaveQ; ++q)
+                    if ((v >> 6) == q) x = label[q];
+                return __builtin_amdgcn_readlane(x, v & 63);
+            };
+            Pair* P = pairs0 + (size_t)l * pcap0;
+            uint64_t cs = 0;
+            uint64_t cnt = 0;
+            for (int e0 = 0; e0 < nmst; e0 += 64) {
+                const int e = e0 + ln;
+                const bool valid = e < nmst;
+                const uint64_t k = valid ? mst[e] : 0;
+                const uint64_t eidx = 0xFFFFFFFFull - (k & 0xFFFFFFFFull);
+                const float d = __uint_as_float((uint32_t)(k >> 32));
+                int a = 0, b = 0;
+                if (valid) {
+                    a = max_vertex(eidx, 2, n - 1);
+                    b = (int)(eidx - binom((uint64_t)a, 2));
+                }
+                int my_young = 0;
+                const int ne = min(64, nmst - e0);
+                for (int j = 0; j < ne; ++j) {  // merges in Kruskal order
+                    const int aj = __builtin_amdgcn_readlane(a, j), bj = __builtin_amdgcn_readlane(b, j);
+                    const int ra = lab_of(aj), rb = lab_of(bj);
+                    const int young = ra < rb ? ra : rb, old = ra < rb ? rb : ra;
+#pragma unroll
+                    for (int q = 0; q < kH0WaveQ; ++q)
+                        if (label[q] == young) label[q] = old;
+                    if (ln == j) my_young = young;
+                }
+                if (valid) cs += pair_hash((uint64_t)my_young, eidx);
+                const bool fin = valid && d > 0.0f;  // finite bars in Kruskal order
+                const uint64_t m = __ballot(fin);
+                const uint64_t pos = cnt + lanes_below(m);
+                if (fin && pos < pcap0) P[pos] = Pair{0.0f, d, (int64_t)my_young, (int64_t)eidx};
+                cnt += (uint64_t)__popcll(m);
+            }
+#pragma unroll
+            for (int q = 0; q < kH0WaveQ; ++q) {  // one [0, inf) bar per component, vertex order
+                const int v = ln + 64 * q;
+                const bool root = v < n && label[q] == v;
+                const uint64_t m = __ballot(root);
+                const uint64_t pos = cnt + lanes_below(m);
+                if (root && pos < pcap0) P[pos] = Pair{0.0f, INFINITY, (int64_t)v, -1};
+                cnt += (uint64_t)__popcll(m);
+            }
+            cs = wave_sum_u64(cs);
+            if (ln == 0) {
+                if (cnt > pcap0) {
+                    st->err |= ERR_PAIR_CAP;
+                    cnt = pcap0;
+                }
+                st->count[0] = (int64_t)cnt;
+                st->checksum[0] = cs;
+                st->all_pairs[0] = nmst;
+                st->n_columns[0] = n;
+            }
+        }
+        return;
+    }
     for (int v = t; v < n; v += T) par[v] = v;
     __syncthreads();
     if (t == 0) {
