@@ -928,10 +928,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         sa.resid[d] = db[d].resid;
         sa.rcap[d] = db[d].rcap;
     }
-    auto launch_sort = [&](int d0, int nd, hipStream_t st) {
-        // LDS chunk: the largest residual list of these dims, at most 16384 keys
+    auto launch_sort = [&](int d0, int nd, hipStream_t st, uint64_t max_chunk = 16384) {
+        // LDS chunk: the largest residual list of these dims, at most max_chunk keys
         uint64_t cap = 64;
-        for (int d = d0; d < d0 + nd; ++d) cap = std::max<uint64_t>(cap, std::min<uint64_t>(next_pow2(p.rcap[d]), 16384));
+        for (int d = d0; d < d0 + nd; ++d) cap = std::max<uint64_t>(cap, std::min<uint64_t>(next_pow2(p.rcap[d]), max_chunk));
         hipLaunchKernelGGL(k_sort_resid, dim3(L, nd), dim3(1024), cap * 8, st, stats, sa, (uint64_t*)(B + p.o_tmp), p.max_rcap,
                            rb.rmap_keys, rb.rmap_stride, ilog2(cap), d0);
     };
@@ -972,7 +972,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         launch_apparent(2, w.stream3);
         HIPC(hipGetLastError());
         if (int rc = tm3.mark("k_apparent<2>")) return rc;
-        launch_sort(2, 1, w.stream3);
+        // beside k_reduce_par<1> (one 72-KB workgroup per CU) the sort's LDS chunk must fit next to
+        // it: 4096 keys (32 KB); a 128-KB chunk waited for the H1 reduction (grid144: 0.85 ms)
+        launch_sort(2, 1, w.stream3, h2_side ? 4096 : 16384);
         HIPC(hipGetLastError());
         if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
         return 0;
