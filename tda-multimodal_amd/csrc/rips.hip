@@ -84,6 +84,8 @@ struct Plan {
     bool wide = false;    // H2 on k_reduce_big with edge-code keys (tetrahedron indices > 32 bits)
     uint64_t ecap = 0;    // per-layer stride of the sorted edge lengths
     size_t o_dsort = 0, o_dtmp = 0, o_dcode = 0;
+    int dsplit = 1;       // K slices of k_distance_mfma (1: no split)
+    size_t o_gpart = 0, o_npart = 0;
     bool serial_tables = false;  // HBM working tables of k_reduce_all (global mode) / k_reduce_big
     uint64_t ostride = 0, rec_cap = 0, rpool_cap = 0, bpool_cap = 0, rq_cap = 0;
     size_t o_pctl = 0, o_pitem = 0, o_pokey = 0, o_poval = 0, o_colpiv = 0, o_prec = 0, o_prpool = 0, o_pbpool = 0, o_prq = 0;
@@ -241,6 +243,21 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     };
     const size_t esz = p.dtype == TDA_F64 ? 8 : 4;
     p.o_x = take(L * N * (p.is_dist ? N : (uint64_t)std::max<int64_t>(p.D, 1)) * esz);
+    {   // split-K for the MFMA distance when its tiles leave CUs idle: aim at ~3 workgroups per CU,
+        // at least 4 K chunks per slice (TDA_DIST_SPLIT=n forces n)
+        const bool mfma = !p.is_dist && (getenv_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !getenv_is("TDA_DIST", "scalar")));
+        if (mfma) {
+            const uint64_t nt = (N + kDmT - 1) / kDmT, tiles = nt * (nt + 1) / 2 * L, chunks = ((uint64_t)p.D + kDmKC - 1) / kDmKC;
+            uint64_t sp = std::min<uint64_t>(8, std::max<uint64_t>(1, (768 + tiles - 1) / tiles));
+            sp = std::min<uint64_t>(sp, std::max<uint64_t>(1, chunks / 4));
+            if (const char* e = getenv("TDA_DIST_SPLIT")) sp = std::max(1, atoi(e));
+            p.dsplit = (int)sp;
+            if (p.dsplit > 1) {
+                p.o_gpart = take(L * sp * N * N * 8);
+                p.o_npart = take(L * sp * N * 8);
+            }
+        }
+    }
     p.o_dist = take(L * N * N * 4);
     p.memset_lo = o;
     p.o_stats = take(L * sizeof(LayerStats));
@@ -753,12 +770,24 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         dim3 grid((n + 15) / 16, (n + 15) / 16, L);
         const bool mfma = dist_mfma;
         const unsigned nt = (unsigned)((n + kDmT - 1) / kDmT);
-        if (mfma && p.dtype == TDA_F64)
-            hipLaunchKernelGGL(k_distance_mfma<double>, dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const double*)x, n, (int)p.D,
-                               dist, rowmax);
+        double* gpart = (double*)(B + p.o_gpart);
+        double* npart = (double*)(B + p.o_npart);
+        const dim3 gsplit(nt * (nt + 1) / 2, L, (unsigned)p.dsplit);
+        const dim3 gcomb((unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256), L);
+        if (mfma && p.dsplit > 1 && p.dtype == TDA_F64) {
+            hipLaunchKernelGGL((k_distance_mfma<double, 0, true>), gsplit, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax,
+                               gpart, npart);
+            hipLaunchKernelGGL((k_distance_combine<double, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
+        } else if (mfma && p.dsplit > 1) {
+            hipLaunchKernelGGL((k_distance_mfma<float, 0, true>), gsplit, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax,
+                               gpart, npart);
+            hipLaunchKernelGGL((k_distance_combine<float, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
+        } else if (mfma && p.dtype == TDA_F64)
+            hipLaunchKernelGGL((k_distance_mfma<double>), dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const double*)x, n, (int)p.D,
+                               dist, rowmax, (double*)nullptr, (double*)nullptr);
         else if (mfma)
-            hipLaunchKernelGGL(k_distance_mfma<float>, dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const float*)x, n, (int)p.D,
-                               dist, rowmax);
+            hipLaunchKernelGGL((k_distance_mfma<float>), dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const float*)x, n, (int)p.D,
+                               dist, rowmax, (double*)nullptr, (double*)nullptr);
         else if (p.dtype == TDA_F64)
             hipLaunchKernelGGL(k_distance<double>, grid, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax);
         else

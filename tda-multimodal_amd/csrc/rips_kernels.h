@@ -161,9 +161,15 @@ typedef double dm_d4 __attribute__((ext_vector_type(4)));
 // METRIC 1: cosine distance instead (UMAP input, umap.distances.cosine:
 // 1 - <x,y> / sqrt(|x|^2 |y|^2), 0 for two zero rows, 1 for one), from the
 // same Gram tiles; clamped at 0.
-template <typename T, int METRIC = 0>
+// SPLIT (gridDim.z = S > 1 K slices, chosen on the host when the tiles alone
+// leave CUs idle -- raw4096: 6 tiles x 32 layers on 256 CUs): slice z sums
+// its K range and stores the tile's partial Gram and (diagonal tiles) the
+// partial norms in f64; k_distance_combine adds the slices in a fixed order
+// and runs the epilogue.
+template <typename T, int METRIC = 0, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, int n, int D, float* __restrict__ dist,
-                                                       uint32_t* __restrict__ rowmax) {
+                                                       uint32_t* __restrict__ rowmax, double* __restrict__ gpart = nullptr,
+                                                       double* __restrict__ npart = nullptr) {
     __shared__ double xs[2][kDmT][kDmS];  // [i/j tile][row][k]
     __shared__ double nrm[2][kDmT];
     __shared__ uint32_t rmx[2][kDmT];
@@ -185,8 +191,14 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
     if (tid < 2 * kDmT) rmx[tid >> 6][tid & 63] = 0;
     // register double buffer: chunk k0 + kDmKC is in flight while chunk k0 feeds the MFMAs
     T pre[4][4];
+    int kbeg = 0, kend = D;  // this slice's K range (whole chunks)
+    if (SPLIT) {
+        const int C = (D + kDmKC - 1) / kDmKC, S = (int)gridDim.z, z = (int)blockIdx.z;
+        kbeg = (int)((int64_t)C * z / S) * kDmKC;
+        kend = min(D, (int)((int64_t)C * (z + 1) / S) * kDmKC);
+    }
     auto load = [&](int k0) {
-        const int kc = min(kDmKC, D - k0);
+        const int kc = min(kDmKC, kend - k0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {  // 2 tiles x 64 rows x kDmKC / 4 groups of 4 consecutive k
             const int e = tid + 256 * u, t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
@@ -196,8 +208,8 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
             for (int q = 0; q < 4; ++q) pre[u][q] = (g < n && c0 + q < kc) ? src[q] : (T)0;
         }
     };
-    load(0);
-    for (int k0 = 0; k0 < D; k0 += kDmKC) {
+    load(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += kDmKC) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int e = tid + 256 * u, t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
@@ -205,7 +217,7 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
             for (int q = 0; q < 4; ++q) xs[t][r][c0 + q] = (double)pre[u][q];
         }
         __syncthreads();
-        if (k0 + kDmKC < D) load(k0 + kDmKC);
+        if (k0 + kDmKC < kend) load(k0 + kDmKC);
         if (tid < 2 * kDmT)  // zero padding adds exact zeros
 #pragma unroll 8
             for (int c = 0; c < kDmKC; ++c) {
@@ -229,6 +241,21 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
     }
     if (tid < 2 * kDmT) nrm[tid >> 6][tid & 63] = nacc;
     __syncthreads();
+    if constexpr (SPLIT) {
+        const size_t zo = ((size_t)l * gridDim.z + blockIdx.z);
+        double* G = gpart + zo * n * n;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = bi * kDmT + wr * 32 + a * 16 + (lane >> 4) + 4 * r, j = bj * kDmT + wc * 32 + b * 16 + (lane & 15);
+                    if (i < n && j < n && i < j) G[(size_t)i * n + j] = acc[a][b][r];
+                }
+        if (bi == bj && tid < kDmT && bi * kDmT + tid < n) npart[zo * n + bi * kDmT + tid] = nrm[0][tid];
+        return;
+    }
     float* Dl = dist + (size_t)l * n * n;
     // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
@@ -269,6 +296,46 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
     if (tid < 2 * kDmT) {
         const int t = tid >> 6, r = tid & 63, g = (t ? bj : bi) * kDmT + r;
         if (g < n && rmx[t][r]) atomicMax(&rm[g], rmx[t][r]);
+    }
+}
+
+// the K slices of k_distance_mfma<..., SPLIT>: fixed-order sums, then the same epilogue
+template <typename T, int METRIC = 0>
+__global__ __launch_bounds__(256) void k_distance_combine(const double* __restrict__ gpart, const double* __restrict__ npart, int S, int n,
+                                                          float* __restrict__ dist, uint32_t* __restrict__ rowmax) {
+    const int l = blockIdx.y;
+    const size_t nn = (size_t)n * n;
+    float* Dl = dist + (size_t)l * nn;
+    uint32_t* rm = rowmax + (size_t)l * n;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nn; q += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(q / n), j = (int)(q - (size_t)i * n);
+        if (i == j) Dl[q] = 0.0f;
+        if (i >= j) continue;
+        double g = 0.0, ni = 0.0, nj = 0.0;
+        for (int z = 0; z < S; ++z) {
+            const size_t zo = (size_t)l * S + z;
+            g += gpart[zo * nn + q];
+            ni += npart[zo * n + i];
+            nj += npart[zo * n + j];
+        }
+        float f;
+        if constexpr (METRIC == 1) {
+            const double d = (ni == 0.0 && nj == 0.0) ? 0.0 : (ni == 0.0 || nj == 0.0) ? 1.0 : 1.0 - g / sqrt(ni * nj);
+            f = fmaxf((float)d, 0.0f);
+        } else if constexpr (sizeof(T) == 4) {
+            f = (float)((-2.0 * g + ni) + nj);
+            f = (f != f) ? f : fmaxf(f, 0.0f);
+            f = sqrt_rn_f32(f);
+        } else {
+            double d = (-2.0 * g + ni) + nj;
+            d = (d != d) ? d : fmax(d, 0.0);
+            f = (float)__dsqrt_rn(d);
+        }
+        f = f + 0.0f;
+        Dl[q] = f;
+        Dl[(size_t)j * n + i] = f;
+        atomicMax(&rm[i], __float_as_uint(f));
+        atomicMax(&rm[j], __float_as_uint(f));
     }
 }
 

@@ -109,14 +109,14 @@ extern "C" int tda_umap_batch(const tda_umap_args* a) {
     const dim3 gm(nt * (nt + 1) / 2, (unsigned)L);
     if (a->metric == TDA_UMAP_COSINE) {
         if (a->dtype == TDA_F64)
-            hipLaunchKernelGGL((k_distance_mfma<double, 1>), gm, dim3(256), 0, s, (const double*)x, (int)N, (int)D, dist, rmax);
+            hipLaunchKernelGGL((k_distance_mfma<double, 1>), gm, dim3(256), 0, s, (const double*)x, (int)N, (int)D, dist, rmax, (double*)nullptr, (double*)nullptr);
         else
-            hipLaunchKernelGGL((k_distance_mfma<float, 1>), gm, dim3(256), 0, s, (const float*)x, (int)N, (int)D, dist, rmax);
+            hipLaunchKernelGGL((k_distance_mfma<float, 1>), gm, dim3(256), 0, s, (const float*)x, (int)N, (int)D, dist, rmax, (double*)nullptr, (double*)nullptr);
     } else if (D >= kDistMfmaMinD) {
         if (a->dtype == TDA_F64)
-            hipLaunchKernelGGL((k_distance_mfma<double, 0>), gm, dim3(256), 0, s, (const double*)x, (int)N, (int)D, dist, rmax);
+            hipLaunchKernelGGL((k_distance_mfma<double, 0>), gm, dim3(256), 0, s, (const double*)x, (int)N, (int)D, dist, rmax, (double*)nullptr, (double*)nullptr);
         else
-            hipLaunchKernelGGL((k_distance_mfma<float, 0>), gm, dim3(256), 0, s, (const float*)x, (int)N, (int)D, dist, rmax);
+            hipLaunchKernelGGL((k_distance_mfma<float, 0>), gm, dim3(256), 0, s, (const float*)x, (int)N, (int)D, dist, rmax, (double*)nullptr, (double*)nullptr);
     } else {
         const dim3 g((unsigned)((N + 15) / 16), (unsigned)((N + 15) / 16), (unsigned)L);
         if (a->dtype == TDA_F64)
