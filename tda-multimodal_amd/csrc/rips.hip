@@ -534,7 +534,8 @@ int grow_hout(Workspace& w, size_t need) {
 bool g_attr_done[64] = {false};
 int set_lds_attrs(int dev) {
     if (dev < 64 && g_attr_done[dev]) return 0;
-    HIPC(hipFuncSetAttribute((const void*)k_h0, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_h0<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_h0<kH0WaveQ, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_sort_resid, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds));
 #define TDA_ATTR_RED(LW, P1, P2) \
@@ -837,7 +838,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
             base = align_up(base, 16);
             // n <= kH0WaveMaxN: one-wave Prim on the LDS-staged matrix (sort chunk just covers the forest)
-            const bool dlds = n <= kH0WaveMaxN && !getenv_is("TDA_H0_WAVE", "0");
+            const bool wave_ok = !getenv_is("TDA_H0_WAVE", "0");
+            const bool dlds = n <= kH0WaveMaxN && wave_ok;
             size_t avail = kLdsMax - base - (dlds ? (size_t)4 * n * n : 0);
             uint64_t ch = 1;
             if (dlds)
@@ -845,8 +847,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             else
                 while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
             size_t lds = base + ch * 8 + (dlds ? (size_t)4 * n * n : 0);
-            hipLaunchKernelGGL(k_h0, dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst), p.mst_words,
-                               (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch), dlds ? 1 : 0);
+            if (dlds)
+                hipLaunchKernelGGL((k_h0<kH0WaveQ, true>), dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst),
+                                   p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
+            else
+                hipLaunchKernelGGL((k_h0<0, false>), dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst),
+                                   p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
         }
         HIPC(hipGetLastError());
         if (int rc = tm4.mark("k_h0")) return rc;

@@ -516,12 +516,21 @@ __device__ void block_sort(uint64_t* keys, uint32_t* vals, uint64_t n, uint64_t*
 // barriers; the threshold and edge count read the LDS copy too (r02:
 // 32 x N=144 layers 0.47 -> 0.30 ms; the sequential thread-0 elder-rule
 // pass that follows is not parallelised yet).
+// Template: WQ = vertices per lane of the one-wave path (0: the block path
+// above), LROWS = rows staged in LDS.  The one-wave path with rows read from
+// global memory (WQ = 16, N = 1024) measured slower than the block path
+// (torus1024: 3.95 vs 3.57 ms, latency-bound row loads), so above N = 190 the
+// block path stays.
 constexpr int kH0WaveMaxN = 190;  // 4 n^2 B of LDS staging
 constexpr int kH0WaveQ = (kH0WaveMaxN + 63) / 64;
+template <int WQ, bool LROWS>
 __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int n, float user_thresh,
                                              LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
                                              uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0,
-                                             uint64_t* __restrict__ scratch /* [L][2n] */, int sort_log2, int dlds) {
+                                             uint64_t* __restrict__ scratch /* [L][2n] */, int sort_log2) {
+    constexpr bool dlds = LROWS;   // the layer's matrix is staged in LDS
+    constexpr bool wave = WQ > 0;  // one-wave Prim + elder rule
+    constexpr int QA = WQ > 0 ? WQ : 1;  // register-array extent (unused when !wave)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, T = blockDim.x, t = threadIdx.x;
     const float* Dl = dist + (size_t)l * n * n;
@@ -585,12 +594,12 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     __syncthreads();
     uint64_t* mst = scratch + (size_t)l * 2 * n;  // MST edge keys
     int nmst = 0;
-    if (dlds) {  // one-wave Prim on the LDS matrix
+    if constexpr (wave) {  // one-wave Prim (rows from LDS, or global memory)
         if (w == 0) {
-            uint64_t bst[kH0WaveQ];
-            bool in[kH0WaveQ];
+            uint64_t bst[QA];
+            bool in[QA];
 #pragma unroll
-            for (int q = 0; q < kH0WaveQ; ++q) {
+            for (int q = 0; q < WQ; ++q) {
                 bst[q] = kEmpty64;
                 in[q] = ln + 64 * q >= n || (ln == 0 && q == 0);  // vertex 0 starts the tree
             }
@@ -598,10 +607,10 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
             for (int it = 1; it < n; ++it) {
                 uint64_t mk = kEmpty64;
 #pragma unroll
-                for (int q = 0; q < kH0WaveQ; ++q) {
+                for (int q = 0; q < WQ; ++q) {
                     const int v = ln + 64 * q;
                     if (in[q]) continue;
-                    const float d = ld_lds(Ds, (size_t)cur * n + v);
+                    const float d = LROWS ? ld_lds(Ds, (size_t)cur * n + v) : ld_glb(Dl, (size_t)cur * n + v);
                     if (d <= thr) {
                         const int a = cur > v ? cur : v, b = cur > v ? v : cur;
                         const uint64_t k = filt_key(d, binom((uint64_t)a, 2) + b);
@@ -613,20 +622,20 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
                 if (gmin == kEmpty64) {  // new component: the smallest vertex not in the forest
                     uint32_t sv = 0xFFFFFFFFu;
 #pragma unroll
-                    for (int q = kH0WaveQ - 1; q >= 0; --q)
+                    for (int q = WQ - 1; q >= 0; --q)
                         if (!in[q]) sv = (uint32_t)(ln + 64 * q);
                     cur = (int)wave_min_u32(sv);
                 } else {  // the owner of the minimum key joins (keys are unique)
                     int nv = 0x7FFFFFFF;
 #pragma unroll
-                    for (int q = 0; q < kH0WaveQ; ++q)
+                    for (int q = 0; q < WQ; ++q)
                         if (!in[q] && bst[q] == gmin) nv = ln + 64 * q;
                     cur = (int)wave_min_u32((uint32_t)nv);
                     if (ln == 0) mst[nmst] = gmin;
                     ++nmst;
                 }
 #pragma unroll
-                for (int q = 0; q < kH0WaveQ; ++q)
+                for (int q = 0; q < WQ; ++q)
                     if (ln + 64 * q == cur) in[q] = true;
             }
         }
@@ -634,7 +643,7 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         __syncthreads();
         nmst = (int)red[34];
     }
-    for (int it = 1; it < (dlds ? 0 : n); ++it) {
+    for (int it = 1; it < (wave ? 0 : n); ++it) {
         const int cur = s_cur;
         uint64_t mk = kEmpty64;
         for (int v = t; v < n; v += T) {
@@ -691,15 +700,15 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         uint64_t eidx = 0xFFFFFFFFull - (mst[e] & 0xFFFFFFFFull);
         atomicOr(&mst_bits[(size_t)l * mst_words + (eidx >> 5)], 1u << (eidx & 31));
     }
-    if (dlds) {  // elder rule on wave 0: lane l holds the component labels (= max vertex) of vertices l, l + 64, l + 128
+    if constexpr (wave) {  // elder rule on wave 0: lane l holds the component labels (= max vertex) of vertices l, l + 64, ...
         if (w == 0) {
-            int label[kH0WaveQ];
+            int label[QA];
 #pragma unroll
-            for (int q = 0; q < kH0WaveQ; ++q) label[q] = ln + 64 * q;
+            for (int q = 0; q < WQ; ++q) label[q] = ln + 64 * q;
             auto lab_of = [&](int v) -> int {  // v wave-uniform
                 int x = label[0];
 #pragma unroll
-                for (int q = 1; q < kH0WaveQ; ++q)
+                for (int q = 1; q < WQ; ++q)
                     if ((v >> 6) == q) x = label[q];
                 return __builtin_amdgcn_readlane(x, v & 63);
             };
@@ -724,7 +733,7 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
                     const int ra = lab_of(aj), rb = lab_of(bj);
                     const int young = ra < rb ? ra : rb, old = ra < rb ? rb : ra;
 #pragma unroll
-                    for (int q = 0; q < kH0WaveQ; ++q)
+                    for (int q = 0; q < WQ; ++q)
                         if (label[q] == young) label[q] = old;
                     if (ln == j) my_young = young;
                 }
@@ -736,7 +745,7 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
                 cnt += (uint64_t)__popcll(m);
             }
 #pragma unroll
-            for (int q = 0; q < kH0WaveQ; ++q) {  // one [0, inf) bar per component, vertex order
+            for (int q = 0; q < WQ; ++q) {  // one [0, inf) bar per component, vertex order
                 const int v = ln + 64 * q;
                 const bool root = v < n && label[q] == v;
                 const uint64_t m = __ballot(root);
