@@ -47,9 +47,50 @@ typedef struct tda_umap_args {
     int32_t device;
     float *out;             /* host (L, N, n_components) f32: the embedding          */
     float *graph_out;       /* optional host (L, N, N) f32: the pruned fuzzy graph   */
+    void *stream;           /* hipStream_t (or NULL): device inputs are read after the
+                               work queued on it so far (e.g. torch's current stream) */
 } tda_umap_args;
 
 int tda_umap_batch(const tda_umap_args *args);
+
+/*
+ * UMAP.transform of a fitted model, for L batches of new points at once:
+ * replaces `reducer.transform(cloud_high_dim)` in the reference's second
+ * driver, which fits one reducer on layer 31 and transforms every layer with
+ * it (analyze_tda_over_layers.py:38-44, :67-72).  umap-learn's transform in
+ * the small-data regime: exact distances to the training points, the
+ * n_neighbors nearest (ties: smaller index), smooth_knn_dist with
+ * local_connectivity - 1 = 0, bipartite memberships (neighbours at or beyond
+ * the metric's disconnection distance dropped), the weighted-mean
+ * initialisation (init_graph_transform), pruning below max / n_epochs, and
+ * n_epochs of SGD in which only the new points move (move_other = False),
+ * attracted to and repelled from the fixed training embedding, at
+ * learning_rate (umap passes its initial alpha / 4).  Same epoch-synchronous
+ * deterministic SGD as tda_umap_batch.  Returns 0 or a negative TDA_E* code.
+ */
+typedef struct tda_umap_transform_args {
+    const void *x_train;      /* (N, D) row-major points the model was fitted on   */
+    const float *emb_train;   /* host (N, n_components) f32: the fitted embedding  */
+    const void *y;            /* (L, M, D) row-major new points                    */
+    int32_t dtype;            /* TDA_F32 | TDA_F64 (x_train and y)                 */
+    int32_t x_on_device;      /* 1: x_train and y are device pointers on `device`  */
+    int64_t L, M, N, D;
+    int32_t metric;           /* TDA_UMAP_EUCLIDEAN | TDA_UMAP_COSINE              */
+    int32_t n_neighbors;      /* the fitted model's, 2 .. min(64, N)                */
+    int32_t n_components;     /* 1 .. 8                                            */
+    int32_t n_epochs;         /* umap: 100 (M <= 10000) or the fit's n_epochs // 3  */
+    int32_t negative_sample_rate;
+    float a, b;               /* the fitted curve parameters                       */
+    float learning_rate;      /* initial alpha (umap: fit learning_rate / 4)       */
+    float repulsion_strength;
+    float disconnection;      /* neighbours at >= this distance are dropped (inf: none) */
+    uint64_t seed;
+    int32_t device;
+    float *out;               /* host (L, M, n_components) f32                     */
+    void *stream;             /* hipStream_t (or NULL), as in tda_umap_args        */
+} tda_umap_transform_args;
+
+int tda_umap_transform(const tda_umap_transform_args *args);
 
 #ifdef __cplusplus
 }

@@ -106,12 +106,41 @@ class UmapArgs(ctypes.Structure):  # include/tda_umap.h
         ("device", ctypes.c_int32),
         ("out", ctypes.c_void_p),
         ("graph_out", ctypes.c_void_p),
+        ("stream", ctypes.c_void_p),
+    ]
+
+
+class UmapTransformArgs(ctypes.Structure):  # include/tda_umap.h
+    _fields_ = [
+        ("x_train", ctypes.c_void_p),
+        ("emb_train", ctypes.c_void_p),
+        ("y", ctypes.c_void_p),
+        ("dtype", ctypes.c_int32),
+        ("x_on_device", ctypes.c_int32),
+        ("L", ctypes.c_int64),
+        ("M", ctypes.c_int64),
+        ("N", ctypes.c_int64),
+        ("D", ctypes.c_int64),
+        ("metric", ctypes.c_int32),
+        ("n_neighbors", ctypes.c_int32),
+        ("n_components", ctypes.c_int32),
+        ("n_epochs", ctypes.c_int32),
+        ("negative_sample_rate", ctypes.c_int32),
+        ("a", ctypes.c_float),
+        ("b", ctypes.c_float),
+        ("learning_rate", ctypes.c_float),
+        ("repulsion_strength", ctypes.c_float),
+        ("disconnection", ctypes.c_float),
+        ("seed", ctypes.c_uint64),
+        ("device", ctypes.c_int32),
+        ("out", ctypes.c_void_p),
+        ("stream", ctypes.c_void_p),
     ]
 
 
 # every symbol declared in include/tda_rips.h and include/tda_umap.h
 EXPORTS = ("tda_rips_batch", "tda_rips_dm", "tda_rips_free", "tda_last_error", "tda_version", "tda_device_ok",
-           "tda_umap_batch")
+           "tda_umap_batch", "tda_umap_transform")
 
 _lib = None
 
@@ -168,6 +197,8 @@ def lib():
     L.tda_device_ok.restype = ctypes.c_int
     L.tda_umap_batch.argtypes = [ctypes.POINTER(UmapArgs)]
     L.tda_umap_batch.restype = ctypes.c_int
+    L.tda_umap_transform.argtypes = [ctypes.POINTER(UmapTransformArgs)]
+    L.tda_umap_transform.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -52,6 +52,19 @@ inline int ilog2(uint64_t x) {
     return r;
 }
 
+// Test / A-B knobs (TDA_REDUCE, TDA_PAR, TDA_CHAIN, TDA_DIST, TDA_ORDER, ...)
+// force a kernel variant or a launch shape.  The library honours them only
+// when TDA_TEST_OVERRIDES=1 is set as well, so a stray variable in a user's
+// environment cannot change the reducer (tests/conftest.py sets the gate).
+const char* test_env(const char* name) {
+    const char* g = getenv("TDA_TEST_OVERRIDES");
+    return (g && g[0] == '1' && !g[1]) ? getenv(name) : nullptr;
+}
+bool test_env_is(const char* name, const char* val) {
+    const char* m = test_env(name);
+    return m && !strcmp(m, val);
+}
+
 constexpr uint64_t kRCapMax = 1ull << 22;    // residual columns per layer and dim
 constexpr uint64_t kPCapMax = 1ull << 16;    // emitted pairs per layer and dim (H>=1)
 constexpr int kLdsMax = 160 * 1024;
@@ -65,7 +78,7 @@ constexpr unsigned kParGrid = 512;           // k_reduce_par workgroups at most 
 // grid144 10.5 -> 8.5 ms, torus1024 61 -> 58.5 ms at 256 vs 512)
 constexpr unsigned kParGridDefault = 256;
 unsigned par_grid_size() {
-    const char* g = getenv("TDA_PAR_GRID");
+    const char* g = test_env("TDA_PAR_GRID");
     const unsigned v = g ? (unsigned)atoi(g) : kParGridDefault;
     return v < 1 ? 1 : (v > kParGrid ? kParGrid : v);
 }
@@ -115,10 +128,11 @@ bool getenv_is(const char* name, const char* val) {
     return m && !strcmp(m, val);
 }
 
+
 // pivots per column before a reduction kernel gives up (ERR_STEP_LIMIT): an
 // exit guarantee, far above any real column (torus1024: < 2^15)
 uint64_t step_limit() {
-    const char* sl = getenv("TDA_STEP_LIMIT");
+    const char* sl = test_env("TDA_STEP_LIMIT");
     return sl ? strtoull(sl, nullptr, 10) : (1ull << 26);
 }
 
@@ -173,23 +187,23 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     p.rcfg = reduce_cfg((int)N, p.maxdim, p.piv_words, p.lds_mode);
     p.wcap_g = (N <= 256 ? 1ull << 17 : (N <= 640 ? 1ull << 21 : 1ull << 23)) << (2 * scale);
     {
-        const char* m = getenv("TDA_REDUCE");
+        const char* m = test_env("TDA_REDUCE");
         // measured (r01): one wave per layer beats the serial radix heap up to
         // N = 256 (grid144 md2 20.6 vs 26.8 ms); measured (r02): the parallel
         // reducer k_reduce_par beats both at every N > 64, H1 and H2, L = 1 and
         // 32 (tools/ab_reduce.py: grid144 md2 L=32 24.1 -> 6.8 ms, torus256
         // md2 L=32 926 -> 50 ms).  After a parallel abort (no_par) the old rule.
         const bool want_wave = m && !strcmp(m, "wave"), want_big = m && !strcmp(m, "big"), want_par = m && !strcmp(m, "par");
-        const bool par_ok = no_par < 2 && p.maxdim >= 1 && !getenv_is("TDA_PAR", "0");
+        const bool par_ok = no_par < 2 && p.maxdim >= 1 && !test_env_is("TDA_PAR", "0");
         p.big = !p.lds_mode && (force_big || want_big || want_par || (!want_wave && (p.N > kBigMinN || par_ok)));
         // TDA_PAR=0: H1 on the serial k_reduce_big as well (comparison / debugging)
-        p.par = p.big && p.maxdim >= 1 && no_par < 2 && !getenv_is("TDA_PAR", "0");
+        p.par = p.big && p.maxdim >= 1 && no_par < 2 && !test_env_is("TDA_PAR", "0");
         p.packed = p.N <= 1024;
         // C(N, 4) >= 2^32 (N > 568): the 32-bit index word of the H2 pivot keys
         // overflows; TDA_H2_WIDE=1 forces the wide keys on any big-path N (tests)
-        p.wide = p.big && p.maxdim >= 2 && (binom(N, 4) >= (1ull << 32) || getenv_is("TDA_H2_WIDE", "1"));
+        p.wide = p.big && p.maxdim >= 2 && (binom(N, 4) >= (1ull << 32) || test_env_is("TDA_H2_WIDE", "1"));
         // TDA_PAR2=0: H2 on the serial radix-heap kernel after a parallel H1
-        p.par2 = p.par && p.maxdim >= 2 && no_par < 1 && !getenv_is("TDA_PAR2", "0");
+        p.par2 = p.par && p.maxdim >= 2 && no_par < 1 && !test_env_is("TDA_PAR2", "0");
         p.dense = p.lds_mode && p.maxdim >= 1 && p.N <= kDenseMaxN && p.N >= 3 && !want_wave;
     }
     if (p.dense) {  // carve of rips_reduce_small.h (h1_chain / h2_phase1), mirrored here
@@ -212,7 +226,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         const uint64_t table_lds = 16 + al(2ull * p.cob_stride) + al(2ull * p.inv_stride) + al(4 * WP) + al(4 * p.piv_words[1]) +
                                    al(8ull * kChainMaxCols) + al(2ull * kChainMaxCols);
         // TDA_CHAIN=general|fast forces a slower variant (tests)
-        const bool want_gen = getenv_is("TDA_CHAIN", "general"), want_fast = getenv_is("TDA_CHAIN", "fast");
+        const bool want_gen = test_env_is("TDA_CHAIN", "general"), want_fast = test_env_is("TDA_CHAIN", "fast");
         p.cmode = kChainGeneral;
         if (!want_gen && p.dK <= kChainFastMaxK) {
             if (!want_fast && table_lds <= (uint64_t)kLdsMax)
@@ -244,13 +258,17 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     const size_t esz = p.dtype == TDA_F64 ? 8 : 4;
     p.o_x = take(L * N * (p.is_dist ? N : (uint64_t)std::max<int64_t>(p.D, 1)) * esz);
     {   // split-K for the MFMA distance when its tiles leave CUs idle: aim at ~3 workgroups per CU,
-        // at least 4 K chunks per slice (TDA_DIST_SPLIT=n forces n)
-        const bool mfma = !p.is_dist && (getenv_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !getenv_is("TDA_DIST", "scalar")));
+        // at least 4 K chunks per slice (TDA_DIST_SPLIT=n forces n).  The slice count fixes the f64
+        // summation order, so it depends on (N, D) only -- sized for the reference's 32-layer sweep
+        // (debug_tda_pipeline.py:92), never on this call's L: a layer's distances (and so its
+        // diagram) are the same in a single call, a batch and every multi-GPU shard.
+        const bool mfma = !p.is_dist && (test_env_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !test_env_is("TDA_DIST", "scalar")));
         if (mfma) {
-            const uint64_t nt = (N + kDmT - 1) / kDmT, tiles = nt * (nt + 1) / 2 * L, chunks = ((uint64_t)p.D + kDmKC - 1) / kDmKC;
+            constexpr uint64_t kSplitRefL = 32;
+            const uint64_t nt = (N + kDmT - 1) / kDmT, tiles = nt * (nt + 1) / 2 * kSplitRefL, chunks = ((uint64_t)p.D + kDmKC - 1) / kDmKC;
             uint64_t sp = std::min<uint64_t>(8, std::max<uint64_t>(1, (768 + tiles - 1) / tiles));
             sp = std::min<uint64_t>(sp, std::max<uint64_t>(1, chunks / 4));
-            if (const char* e = getenv("TDA_DIST_SPLIT")) sp = std::max(1, atoi(e));
+            if (const char* e = test_env("TDA_DIST_SPLIT")) sp = std::max(1, atoi(e));
             p.dsplit = (int)sp;
             if (p.dsplit > 1) {
                 p.o_gpart = take(L * sp * N * N * 8);
@@ -715,7 +733,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     StageTimer tm4{w.stage_ev4, w.stream4, tm.on, {}};
     if (serial_stages) tm2.fwd = tm3.fwd = tm4.fwd = &tm;
     // D >= 32 (raw activations): Gram tiles on the FP64 matrix cores; TDA_DIST=scalar|mfma forces one (tests)
-    const bool dist_mfma = input_kind == 0 && (getenv_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !getenv_is("TDA_DIST", "scalar")));
+    const bool dist_mfma = input_kind == 0 && (test_env_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !test_env_is("TDA_DIST", "scalar")));
     GraphKey gk;
     std::memset(&gk, 0, sizeof(gk));
     gk.L = p.L;
@@ -743,7 +761,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     GraphEntry* ge = nullptr;
     // stage-timed calls run eagerly: timing events inside a capture need
     // external event nodes, which torch's bundled HIP runtime rejects
-    const bool use_graph = !getenv_is("TDA_GRAPH", "0") && !tm.on;
+    const bool use_graph = !test_env_is("TDA_GRAPH", "0") && !tm.on;
     if (use_graph)
         for (auto& g : w.graphs)
             if (g.key == gk) ge = &g;
@@ -838,7 +856,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
             base = align_up(base, 16);
             // n <= kH0WaveMaxN: one-wave Prim on the LDS-staged matrix (sort chunk just covers the forest)
-            const bool wave_ok = !getenv_is("TDA_H0_WAVE", "0");
+            const bool wave_ok = !test_env_is("TDA_H0_WAVE", "0");
             const bool dlds = n <= kH0WaveMaxN && wave_ok;
             size_t avail = kLdsMax - base - (dlds ? (size_t)4 * n * n : 0);
             uint64_t ch = 1;
@@ -924,10 +942,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         // whose grid holds every CU while the critical small kernels wait; off
         // the dense path the apparent kernels run alone: 4096 (r02, grid144:
         // apparent<2> 1.08 -> 0.87 ms; staging the 83-KB matrix in LDS: 2.25 ms)
-        static const char* app_env = getenv("TDA_APP_GRID");
+        const char* app_env = test_env("TDA_APP_GRID");
         const uint64_t app_total = app_env ? strtoull(app_env, nullptr, 10) : (p.dense ? 1024 : 4096);
         unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, app_total / L)));
-        static const int app_lds_max = getenv("TDA_APP_LDS_MAXN") ? atoi(getenv("TDA_APP_LDS_MAXN")) : kAppLdsMaxN;
+        const int app_lds_max = test_env("TDA_APP_LDS_MAXN") ? atoi(test_env("TDA_APP_LDS_MAXN")) : kAppLdsMaxN;
         const bool dl = n <= app_lds_max && 16 + (size_t)n * n * 4 <= (size_t)kLdsMax;
         const size_t alds = 16 + (dl ? (size_t)n * n * 4 : 0);
         if (d == 1) {
@@ -998,7 +1016,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // TDA_ORDER=0 apparent<1> first; 1 side streams first; 2 side streams
     // first and the H2 branch after the triangle ranks; 3 side streams first,
     // sort<1> enqueued before the H2 branch
-    static const int order = getenv("TDA_ORDER") ? atoi(getenv("TDA_ORDER")) : 3;  // 3: measured best (r01)
+    const int order = test_env("TDA_ORDER") ? atoi(test_env("TDA_ORDER")) : 3;  // 3: measured best (r01)
     if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
     const bool h2_side = !p.dense && p.par && p.par2 && p.maxdim >= 2;
@@ -1284,7 +1302,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             guard.unlock();
             return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par);
         }
-        if (getenv_is("TDA_PAR_STRICT", "1"))  // tests: the parallel path itself must succeed
+        if (test_env_is("TDA_PAR_STRICT", "1"))  // tests: the parallel path itself must succeed
             return fail(TDA_E_CAPACITY, "k_reduce_par aborted: item " + std::to_string(c.err >> 16) + " code " +
                                             std::to_string(code));
         guard.unlock();
@@ -1295,7 +1313,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         guard.unlock();
         return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par);
     }
-    if ((errs & ERR_WORK_CAP) && !p.big && !getenv_is("TDA_REDUCE", "wave")) {
+    if ((errs & ERR_WORK_CAP) && !p.big && !test_env_is("TDA_REDUCE", "wave")) {
         // a working column outgrew the one-wave HBM tables: full scans of a
         // large column are the slow case, so switch to the radix-heap kernel
         guard.unlock();
@@ -1352,8 +1370,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)u[0], (unsigned long long)u[3], (unsigned long long)u[1], (unsigned long long)u[2],
                 (unsigned long long)u[4], (unsigned long long)u[5], (unsigned long long)u[6], (unsigned long long)u[7]);
         const uint64_t* v = w.hstats[0].prof[4];
-        fprintf(stderr, "[tda-prof]   record adds: room %llu, col_add %llu cycles, keys front %llu / all %llu; refill pass 3 %llu cycles\n",
-                (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2], (unsigned long long)v[3], (unsigned long long)v[5]);
+        fprintf(stderr, "[tda-prof]   record adds: room %llu, col_add %llu cycles, keys front %llu / all %llu; refill pass 3 %llu cycles; %llu saves (%llu keys) %llu cycles\n",
+                (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2], (unsigned long long)v[3], (unsigned long long)v[5],
+                (unsigned long long)v[6], (unsigned long long)v[7], (unsigned long long)v[4]);
     }
     if (p.big && !p.par)
         for (int d = 1; d <= p.maxdim; ++d) {
@@ -1526,8 +1545,8 @@ int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_
     int np = 0;
     int sc = 0;
     // not when a test forces a reducer (the memo would override what it asks for)
-    if (!getenv_is("TDA_RETRY_MEMO", "0") && !getenv("TDA_REDUCE") && !getenv("TDA_PAR") && !getenv("TDA_PAR_STRICT") &&
-        !getenv("TDA_CHAIN")) {
+    if (!test_env_is("TDA_RETRY_MEMO", "0") && !test_env("TDA_REDUCE") && !test_env("TDA_PAR") && !test_env("TDA_PAR_STRICT") &&
+        !test_env("TDA_CHAIN")) {
         Workspace& w = *get_ws(a.device);
         std::lock_guard<std::mutex> g(w.mu);
         for (const auto& m : w.retry)

@@ -783,8 +783,22 @@ __host__ __device__ __forceinline__ uint32_t par_need(int n) {  // log entries o
 
 // Publish the working column as an immutable record (sc1 stores, drained).
 // Returns the record id (block-uniform), or -1 on overflow.
-__device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_t pkey, uint64_t item) {
+// Small columns are copied (front + every HBM bucket).  A column with more
+// than kParSegMin keys is published ZERO-COPY: the record holds its live
+// front keys and a table of (bpool offset, count) segments that point at the
+// workgroup's own bucket chunks (*seg = true).  The caller then gives those
+// chunks up once the record is referenced (a successful claim) and takes
+// fresh ones for its next column.  (r03 profile, torus1024: the longest
+// column's final save copied 5.3 M raw bucket keys, ~10 ms of one workgroup's
+// bandwidth, on the critical path.)
+constexpr uint64_t kParSegMin = 1ull << 16;
+constexpr uint64_t kParSegBit = 1ull << 63;  // record header word 0: segmented payload
+__device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_t pkey, uint64_t item, bool* seg) {
+    drain_vm();       // this wave's bucket stores have reached L2
     __syncthreads();  // full barrier: every wave's bucket stores are visible to the copy below
+#ifdef TDA_PROFILE
+    const uint64_t tsv = clock64();
+#endif
     const uint32_t c = PS.fcnt;
     uint32_t lv = 0;
     for (uint32_t e = threadIdx.x; e < c; e += kParT) lv += PS.log[e] < kDead;
@@ -792,10 +806,13 @@ __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_
     uint64_t nback = 0;
     for (int q = 0; q <= 32; ++q) nback += PS.bcnt[q];
     const uint64_t total = nfront + nback;
+    const bool segd = total > kParSegMin;
+    constexpr uint32_t kSegs = 33u * kParChunks;
+    const uint64_t words = segd ? nfront + 2ull * kSegs : total;
     if (threadIdx.x == 0) {
-        const uint64_t o = aadd(&P.ctl->rpool_used, (total + 15) & ~15ull);  // 128-B aligned records
+        const uint64_t o = aadd(&P.ctl->rpool_used, (words + 15) & ~15ull);  // 128-B aligned records
         const uint64_t id = aadd(&P.ctl->rec_used, 1ull);
-        PS.bc[0] = (o + total <= P.rpool_cap && id < P.rec_cap) ? o : kEmpty64;
+        PS.bc[0] = (o + words <= P.rpool_cap && id < P.rec_cap) ? o : kEmpty64;
         PS.bc[1] = id;
     }
     __syncthreads();
@@ -816,46 +833,73 @@ __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_
         if (live) ast(out + w + o, x);
         w += tot;
     }
-    uint64_t pos = nfront;
-    for (int q = 0; q <= 32; ++q) {
-        const uint32_t cq = PS.bcnt[q];
-        for (uint32_t e = threadIdx.x; e < cq; e += kParT) ast(out + pos + e, bucket_at(P, (uint32_t)q, e));
-        pos += cq;
+    uint64_t hdr1 = total;
+    if (segd) {
+        // compacted segment table: one (offset, count) per non-empty (bucket, chunk)
+        uint32_t ns = 0;
+        for (uint32_t e0 = 0; e0 < kSegs; e0 += kParT) {
+            const uint32_t e = e0 + threadIdx.x;
+            const uint32_t q = e / kParChunks, kc = e % kParChunks;
+            uint32_t cnt = 0;
+            if (e < kSegs) {
+                const uint32_t cq = PS.bcnt[q], lo = chunk_start(kc);
+                if (lo < cq) cnt = min(cq, chunk_start(kc + 1)) - lo;
+            }
+            uint32_t tot;
+            const uint32_t o = C.rd.prefix(cnt ? 1u : 0u, &tot);
+            if (cnt) {
+                ast(out + nfront + 2 * (ns + o), (uint64_t)PS.cptr[q][kc] * 256);
+                ast(out + nfront + 2 * (ns + o) + 1, (uint64_t)cnt);
+            }
+            ns += tot;
+        }
+        hdr1 = nfront | ((uint64_t)ns << 32);
+    } else {
+        uint64_t pos = nfront;
+        for (int q = 0; q <= 32; ++q) {  // kParRegs bucket loads in flight per thread
+            const uint32_t cq = PS.bcnt[q];
+            for (uint32_t e0 = 0; e0 < cq; e0 += kParT * kParRegs) {
+                uint64_t x[kParRegs];
+                const uint32_t vm = bucket_batch(P, (uint32_t)q, e0, cq, x);
+#pragma unroll
+                for (int r = 0; r < kParRegs; ++r)
+                    if ((vm >> r) & 1u) ast(out + pos + e0 + threadIdx.x + r * kParT, x[r]);
+            }
+            pos += cq;
+        }
     }
+#ifdef TDA_PROFILE
+    C.q2[6] += 1;
+    C.q2[7] += total;
+    C.q2[4] += clock64() - tsv;
+#endif
+    drain_vm();
+    __syncthreads();
     if (threadIdx.x == 0) {
+        // the bucket chunks were written with plain stores: write this XCD's L2 back before
+        // the header (and the CAS after it) can be seen by a reader on another XCD
+        if (segd) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         uint64_t* rh = P.rec + id * 4;
-        ast(rh + 0, off);
-        ast(rh + 1, total);
+        ast(rh + 0, off | (segd ? kParSegBit : 0ull));
+        ast(rh + 1, hdr1);
         ast(rh + 2, pkey);
         ast(rh + 3, item);
     }
     drain_vm();  // every storing wave, before the barrier that precedes the publishing CAS
     __syncthreads();
+    *seg = segd;
     return (int64_t)id;
 }
 
-// add record `id` (sc1 loads) to the working column
-__device__ __forceinline__ void col_add_record(ParCol& C, const ParBufs& P, uint64_t id) {
-    if (threadIdx.x == 0) {  // header by sc1 loads, then ONE agent acquire: the payload reads are plain loads
-        PS.bc[2] = ald(P.rec + id * 4 + 0);
-        PS.bc[3] = ald(P.rec + id * 4 + 1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        drain_vm();
-    }
-    __syncthreads();
-    const uint64_t off = PS.bc[2], len = PS.bc[3];
-    __syncthreads();
-#ifdef TDA_PROFILE
-    C.q[4] += 1;
-    C.q[5] += len;
-#endif
+// add len keys src[0 .. len) (plain loads: the caller acquired) to the working column
+__device__ __forceinline__ void col_add_keys(ParCol& C, const ParBufs& P, const uint64_t* src, uint64_t len) {
     for (uint64_t e0 = 0; e0 < len; e0 += kParT * kParRegs) {
         uint64_t x[kParRegs];
         uint32_t vm = 0;
 #pragma unroll
         for (int q = 0; q < kParRegs; ++q) {
             const uint64_t e = e0 + threadIdx.x + (uint64_t)q * kParT;
-            x[q] = e < len ? ld_glb(P.rpool, off + e) : 0;
+            x[q] = e < len ? ld_glb(src, e) : 0;
             if (e < len) vm |= 1u << q;
         }
         PAR_T0(tr0);
@@ -877,6 +921,46 @@ __device__ __forceinline__ void col_add_record(ParCol& C, const ParBufs& P, uint
 #ifdef TDA_PROFILE
         C.q2[1] += clock64() - ta0;
 #endif
+    }
+}
+
+// add record `id` (sc1 loads) to the working column
+__device__ __forceinline__ void col_add_record(ParCol& C, const ParBufs& P, uint64_t id) {
+    if (threadIdx.x == 0) {  // header by sc1 loads, then ONE agent acquire: the payload reads are plain loads
+        PS.bc[2] = ald(P.rec + id * 4 + 0);
+        PS.bc[3] = ald(P.rec + id * 4 + 1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        drain_vm();
+    }
+    __syncthreads();
+    const uint64_t h0 = PS.bc[2], h1 = PS.bc[3];
+    __syncthreads();
+    const uint64_t off = h0 & ~kParSegBit;
+    if (!(h0 & kParSegBit)) {
+#ifdef TDA_PROFILE
+        C.q[4] += 1;
+        C.q[5] += h1;
+#endif
+        col_add_keys(C, P, P.rpool + off, h1);
+    } else {  // segmented: front keys, then every (offset, count) segment of bucket chunks
+        const uint64_t nfront = h1 & 0xFFFFFFFFull, ns = h1 >> 32;
+        const uint64_t* tab = P.rpool + off + nfront;
+#ifdef TDA_PROFILE
+        C.q[4] += 1;
+        C.q[5] += nfront;
+#endif
+        col_add_keys(C, P, P.rpool + off, nfront);
+        uint64_t so = ns ? ld_glb(tab, 0) : 0, sc = ns ? ld_glb(tab, 1) : 0;
+        for (uint64_t g = 0; g < ns && !PS.err; ++g) {
+            // the next descriptor is in flight while this segment is added
+            const uint64_t no = g + 1 < ns ? ld_glb(tab, 2 * (g + 1)) : 0, nc = g + 1 < ns ? ld_glb(tab, 2 * (g + 1) + 1) : 0;
+#ifdef TDA_PROFILE
+            C.q[5] += sc;
+#endif
+            col_add_keys(C, P, P.bpool + so, sc);
+            so = no;
+            sc = nc;
+        }
     }
     __syncthreads();
 }
@@ -1048,6 +1132,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             col_add_record(C, P, rec0 - 1);
         }
         int64_t my_rec = -1;
+        bool my_seg = false;  // my_rec is zero-copy: it owns this workgroup's bucket chunks
         uint64_t adds = 0;
         bool done = false;
 #ifdef TDA_PROFILE
@@ -1188,7 +1273,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 }
                 // free, or owned by a later column: publish R_j, then claim
                 if (my_rec < 0) {
-                    my_rec = col_save(C, P, pk, item);
+                    my_rec = col_save(C, P, pk, item, &my_seg);
                     if (my_rec < 0) break;
                 }
                 const uint64_t mine = (j << 32) | (uint64_t)(my_rec + 1);
@@ -1242,6 +1327,11 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         }
 #endif
         if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)adds);
+        if (done && my_rec >= 0 && my_seg) {  // the claimed record references this workgroup's chunks: fresh ones next
+            for (uint32_t e = tid; e < 33u * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
+            prealloc = false;
+            __syncthreads();
+        }
         if (PS.err) {
             if (tid == 0) {
                 acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)item << 16) | (uint64_t)PS.err);  // first error: item, code

@@ -63,6 +63,12 @@ struct UmapBufs {
     float* emb;             // [L][N][c] layout (init, then the result)
     uint64_t ecap;
     int n, k, c, n_epochs;
+    // kNN rows: queries qrow0 .. qrow0 + nq - 1 of a layer's distance matrix
+    // (row length `stride`, `lstride` floats per layer) against its first
+    // `ncand` columns.  Fit: all n rows against all n points; transform: the
+    // M new points (rows N..N+M-1 of [train; new]) against the N training points.
+    size_t lstride;
+    int stride, qrow0, nq, ncand;
 };
 
 __device__ __forceinline__ uint64_t umap_hash(uint64_t a, uint64_t b) { return mix64(a * 0x9E3779B97F4A7C15ull ^ mix64(b + 0x632BE59BD9B4E019ull)); }
@@ -84,11 +90,11 @@ __device__ __forceinline__ double umap_block_sum(double v, double* red) {
 __global__ __launch_bounds__(kUmapKnnT) void k_umap_knn(UmapBufs u) {
     __shared__ float ld[kUmapKnnT][kUmapMaxK];
     __shared__ int32_t li[kUmapKnnT][kUmapMaxK];
-    const int l = blockIdx.y, t = threadIdx.x, i = blockIdx.x * kUmapKnnT + t, n = u.n, k = u.k;
-    if (i >= n) return;
-    const float* row = u.dist + ((size_t)l * n + i) * n;
+    const int l = blockIdx.y, t = threadIdx.x, i = blockIdx.x * kUmapKnnT + t, nq = u.nq, k = u.k;
+    if (i >= nq) return;
+    const float* row = u.dist + (size_t)l * u.lstride + (size_t)(u.qrow0 + i) * u.stride;
     int cnt = 0;
-    for (int j = 0; j < n; ++j) {
+    for (int j = 0; j < u.ncand; ++j) {
         const float d = ld_glb(row, j);
         if (cnt == k && !(d < ld[t][k - 1])) continue;  // ties keep the smaller index (already in)
         int p = cnt < k ? cnt++ : k - 1;
@@ -100,8 +106,8 @@ __global__ __launch_bounds__(kUmapKnnT) void k_umap_knn(UmapBufs u) {
         ld[t][p] = d;
         li[t][p] = j;
     }
-    float* kd = u.kd + ((size_t)l * n + i) * k;
-    int32_t* ki = u.ki + ((size_t)l * n + i) * k;
+    float* kd = u.kd + ((size_t)l * nq + i) * k;
+    int32_t* ki = u.ki + ((size_t)l * nq + i) * k;
     for (int q = 0; q < k; ++q) {
         kd[q] = ld[t][q];
         ki[q] = li[t][q];
@@ -494,6 +500,190 @@ __global__ __launch_bounds__(kUmapT) void k_umap_sgd(UmapBufs u, double a, doubl
         __syncthreads();
     }
     for (int e = t; e < n * c; e += kUmapT) emb[e] = E[e];
+}
+
+// ---------------------------------------------------------------- transform
+// [train; new] -> one layer's M x c transform embedding, one workgroup per
+// layer (umap-learn UMAP.transform, small-data regime).  u.kd / u.ki hold the
+// M new points' n_neighbors nearest training points (k_umap_knn with qrow0 =
+// N); `temb` is the fitted N x c embedding; `vals` [L][M * k] the bipartite
+// memberships.  Edges are the (point, neighbour) slots in row-major kNN
+// order (umap's coo graph after eliminate_zeros); a dropped or pruned slot
+// has epochs_per_sample -1.
+__global__ __launch_bounds__(kUmapT) void k_umap_transform(UmapBufs u, const float* __restrict__ temb, int N, float* __restrict__ vals,
+                                                           double a, double b, double lr, double gamma, int neg_rate, uint64_t seed,
+                                                           float disc) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ double red[kUmapT / 64];
+    __shared__ uint32_t vmax_sh;
+    const int l = blockIdx.x, M = u.nq, k = u.k, c = u.c, t = threadIdx.x;
+    float* E = (float*)smem;                                                          // [M][c] new points
+    long long* acc = (long long*)(smem + (((size_t)4 * M * c + 15) & ~(size_t)15));  // [M][c] epoch move sums
+    float* T = (float*)(acc + (size_t)M * c);                                         // [N][c] training embedding (fixed)
+    const float* kd = u.kd + (size_t)l * M * k;
+    const int32_t* ki = u.ki + (size_t)l * M * k;
+    float* V = vals + (size_t)l * M * k;
+    const size_t o = (size_t)l * u.ecap;
+    for (int e = t; e < N * c; e += kUmapT) T[e] = temb[e];
+    for (int e = t; e < M * c; e += kUmapT) acc[e] = 0;
+    if (t == 0) vmax_sh = 0;
+    // smooth_knn_dist(dists, k, local_connectivity = max(0, 1 - 1) = 0): rho = 0;
+    // mean_distances over every transform distance (dropped neighbours included, as umap)
+    double s = 0.0;
+    for (int e = t; e < M * k; e += kUmapT) s += (double)kd[e];
+    const double mean_all = umap_block_sum(s, red) / (double)(M * k);
+    const double target = log2((double)k);
+    uint32_t vmax = 0;
+    for (int i = t; i < M; i += kUmapT) {
+        const float* d = kd + (size_t)i * k;
+        double lo = 0.0, hi = INFINITY, mid = 1.0;
+        for (int it = 0; it < 64; ++it) {
+            double psum = 0.0;
+            for (int j = 1; j < k; ++j) {  // umap skips slot 0 (the fit's self neighbour) here too
+                const double dd = (double)d[j];
+                psum += dd > 0.0 ? exp(-(dd / mid)) : 1.0;
+            }
+            if (fabs(psum - target) < 1e-5) break;
+            if (psum > target) {
+                hi = mid;
+                mid = (lo + hi) / 2.0;
+            } else {
+                lo = mid;
+                mid = isinf(hi) ? mid * 2.0 : (lo + hi) / 2.0;
+            }
+        }
+        double sigma = mid;
+        if (sigma < 1e-3 * mean_all) sigma = 1e-3 * mean_all;  // rho == 0 branch (MIN_K_DIST_SCALE)
+        // compute_membership_strengths(bipartite=True); index -1 (d >= disconnection) -> no entry
+        for (int j = 0; j < k; ++j) {
+            float val;
+            if (!(d[j] < disc))
+                val = 0.0f;
+            else if ((double)d[j] <= 0.0 || sigma == 0.0)
+                val = 1.0f;
+            else
+                val = (float)exp(-((double)d[j] / sigma));
+            V[(size_t)i * k + j] = val;
+            vmax = max(vmax, __float_as_uint(val));
+        }
+    }
+    vmax = (uint32_t)wave_max_u64(vmax);
+    if ((t & 63) == 0 && vmax) atomicMax(&vmax_sh, vmax);
+    __syncthreads();
+    // init_graph_transform on the unpruned graph (zeros eliminated): the
+    // membership-weighted mean of the neighbours' embeddings in f32 -- or a
+    // neighbour's own embedding when its membership is exactly 1 -- NaN without neighbours
+    for (int i = t; i < M; i += kUmapT) {
+        float rs = 0.0f;
+        int nnz = 0;
+        for (int j = 0; j < k; ++j) {
+            const float v = V[(size_t)i * k + j];
+            if (v != 0.0f) rs += v, ++nnz;
+        }
+        float r[kUmapMaxC];
+        for (int dd = 0; dd < c; ++dd) r[dd] = nnz ? 0.0f : __builtin_nanf("");
+        for (int j = 0; j < k && nnz; ++j) {
+            const float v = V[(size_t)i * k + j];
+            if (v == 0.0f) continue;
+            const int col = ki[(size_t)i * k + j];
+            if (v == 1.0f) {
+                for (int dd = 0; dd < c; ++dd) r[dd] = T[col * c + dd];
+                break;
+            }
+            const float wgt = __fdiv_rn(v, rs);
+            for (int dd = 0; dd < c; ++dd) r[dd] = __fadd_rn(r[dd], __fmul_rn(wgt, T[col * c + dd]));
+        }
+        for (int dd = 0; dd < c; ++dd) E[i * c + dd] = r[dd];
+    }
+    // prune below max / n_epochs, make_epochs_per_sample on the survivors
+    const float vm = __uint_as_float(vmax_sh);
+    const double thr = (double)vm / (double)u.n_epochs, negr = (double)neg_rate;
+    for (int e = t; e < M * k; e += kUmapT) {
+        const float w = V[e];
+        double eps = -1.0;
+        if (w != 0.0f && !((double)w < thr)) {
+            const float ns = __fmul_rn((float)u.n_epochs, __fdiv_rn(w, vm));
+            if (ns > 0.0f) eps = (double)u.n_epochs / (double)ns;
+        }
+        u.eps[o + e] = eps;
+        u.nxt[o + e] = eps;
+        u.nxn[o + e] = eps / negr;
+    }
+    __syncthreads();
+    auto add = [&](int p, int dd, double v) {
+        __hip_atomic_fetch_add((TDA_LDS long long*)&acc[p * c + dd], (long long)llrint(v * kUmapFix), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    // optimize_layout_euclidean(move_other=False): the new points move, the training embedding stays
+    for (int ep = 0; ep < u.n_epochs; ++ep) {
+        const double alpha = lr * (1.0 - (double)ep / (double)u.n_epochs);
+        for (int e = t; e < M * k; e += kUmapT) {
+            const double eps = u.eps[o + e];
+            if (eps < 0.0) continue;
+            const double nx = u.nxt[o + e];
+            if (nx > (double)ep) continue;
+            const double epsn = eps / negr;
+            const int j = e / k, kk = ki[e];
+            float cur[kUmapMaxC];
+            double d2 = 0.0;
+            for (int dd = 0; dd < c; ++dd) {
+                cur[dd] = E[j * c + dd];
+                const double df = (double)cur[dd] - (double)T[kk * c + dd];
+                d2 += df * df;
+            }
+            const float d2f = (float)d2;
+            double gc = 0.0;
+            if (d2f > 0.0f) {
+                gc = -2.0 * a * b * pow((double)d2f, b - 1.0);
+                gc /= a * pow((double)d2f, b) + 1.0;
+            }
+            for (int dd = 0; dd < c; ++dd) add(j, dd, umap_clip(gc * ((double)cur[dd] - (double)T[kk * c + dd])) * alpha);
+            u.nxt[o + e] = nx + eps;
+            const double nn = u.nxn[o + e];
+            const int nneg = (int)(((double)ep - nn) / epsn);
+            for (int p = 0; p < nneg; ++p) {
+                const int q = (int)(umap_hash(seed, ((uint64_t)ep << 32) ^ ((uint64_t)e << 8) ^ (uint64_t)p) % (uint64_t)N);
+                double r2 = 0.0;
+                for (int dd = 0; dd < c; ++dd) {
+                    const double df = (double)cur[dd] - (double)T[q * c + dd];
+                    r2 += df * df;
+                }
+                const float r2f = (float)r2;
+                double g2;
+                if (r2f > 0.0f) {
+                    g2 = 2.0 * gamma * b;
+                    g2 /= (0.001 + (double)r2f) * (a * pow((double)r2f, b) + 1.0);
+                } else if (j == q) {  // umap compares the head index with the sample's (different sets here, as there)
+                    continue;
+                } else {
+                    g2 = 0.0;
+                }
+                for (int dd = 0; dd < c; ++dd) {
+                    const double gd = g2 > 0.0 ? umap_clip(g2 * ((double)cur[dd] - (double)T[q * c + dd])) : 4.0;
+                    add(j, dd, gd * alpha);
+                }
+            }
+            u.nxn[o + e] = nn + (double)nneg * epsn;
+        }
+        __syncthreads();
+        for (int e = t; e < M * c; e += kUmapT) {
+            E[e] = (float)((double)E[e] + (double)acc[e] * (1.0 / kUmapFix));
+            acc[e] = 0;
+        }
+        __syncthreads();
+    }
+    float* emb = u.emb + (size_t)l * M * c;
+    for (int e = t; e < M * c; e += kUmapT) emb[e] = E[e];
+}
+
+// [x_train; y_l] per layer (the transform's distance input), 4-byte words
+__global__ __launch_bounds__(256) void k_umap_concat(const uint32_t* __restrict__ xt, const uint32_t* __restrict__ y, uint32_t* __restrict__ z,
+                                                     uint64_t train_words, uint64_t layer_words) {
+    const int l = blockIdx.y;
+    uint32_t* zl = z + (size_t)l * (train_words + layer_words);
+    const uint32_t* yl = y + (size_t)l * layer_words;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < train_words + layer_words; e += (uint64_t)gridDim.x * blockDim.x)
+        zl[e] = e < train_words ? xt[e] : yl[e - train_words];
 }
 
 }  // namespace tda

@@ -9,6 +9,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# the library honours its test-only variant knobs (TDA_REDUCE, TDA_CHAIN, ...)
+# only behind this gate (rips.hip test_env)
+os.environ["TDA_TEST_OVERRIDES"] = "1"
 
 
 def pytest_configure(config):

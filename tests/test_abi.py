@@ -130,3 +130,43 @@ def test_umap_invalid_arguments_rejected_before_device(pkg, built_lib):
     assert L.tda_umap_batch(ctypes.byref(U)) == -1
     U.n_neighbors = 4
     assert L.tda_umap_batch(ctypes.byref(U)) == -5  # valid, but no gfx950 here
+
+
+def test_umap_transform_struct_matches_header_layout(pkg, tmp_path):
+    import subprocess
+
+    from importlib import import_module
+
+    lb = import_module("tda-multimodal_amd._lib")
+    src = tmp_path / "tlayout.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "tda_umap.h"\n'
+        'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tda_umap_transform_args),'
+        ' offsetof(tda_umap_transform_args, L), offsetof(tda_umap_transform_args, disconnection),'
+        ' offsetof(tda_umap_transform_args, seed), offsetof(tda_umap_transform_args, out),'
+        ' offsetof(tda_umap_transform_args, stream), offsetof(tda_umap_args, stream)); return 0;}\n')
+    exe = tmp_path / "tlayout"
+    subprocess.run(["gcc", "-I", lb.INCLUDE, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    T = lb.UmapTransformArgs
+    assert got == [ctypes.sizeof(T), T.L.offset, T.disconnection.offset, T.seed.offset, T.out.offset, T.stream.offset,
+                   lb.UmapArgs.stream.offset]
+
+
+def test_umap_transform_invalid_arguments_rejected_before_device(pkg, built_lib):
+    L = pkg.lib()
+    T = pkg._lib.UmapTransformArgs()
+    X = np.zeros((8, 3), np.float32)
+    E = np.zeros((8, 2), np.float32)
+    Y = np.zeros((2, 5, 3), np.float32)
+    out = np.zeros((2, 5, 2), np.float32)
+    T.x_train, T.emb_train, T.y, T.out = X.ctypes.data, E.ctypes.data, Y.ctypes.data, out.ctypes.data
+    T.dtype, T.L, T.M, T.N, T.D = 0, 2, 5, 8, 3
+    T.metric, T.n_neighbors, T.n_components, T.n_epochs, T.a, T.b = 1, 4, 2, 30, 1.5, 0.9
+    T.disconnection = float("inf")
+    T.metric = 7
+    assert L.tda_umap_transform(ctypes.byref(T)) == -2
+    T.metric, T.n_neighbors = 1, 9  # > N
+    assert L.tda_umap_transform(ctypes.byref(T)) == -1
+    T.n_neighbors = 4
+    assert L.tda_umap_transform(ctypes.byref(T)) == -5  # valid, but no gfx950 here

@@ -4,7 +4,7 @@
 #   bash tools/ab_env.sh sweep48 "TDA_PREP=3 TDA_ORDER=3" "TDA_PREP=3" ""
 WL=$1; shift
 for V in "$@"; do
-    AB_TAG="[$V]" env $V timeout -k 10 120 python3 - "$WL" <<'PY'
+    AB_TAG="[$V]" env TDA_TEST_OVERRIDES=1 $V timeout -k 10 120 python3 - "$WL" <<'PY'
 import importlib, os, statistics, sys, time
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
 import bench, torch

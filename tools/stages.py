@@ -1,6 +1,6 @@
 """Per-stage device times (all stages serialised on one stream) of one bench
 workload under the current environment (dev aid):
-    TDA_REDUCE=big python tools/stages.py grid144
+    TDA_TEST_OVERRIDES=1 TDA_REDUCE=big python tools/stages.py grid144
 """
 import importlib
 import os
