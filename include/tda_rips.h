@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TDA_RIPS_ABI_VERSION 3
+#define TDA_RIPS_ABI_VERSION 4
 
 /* error codes */
 #define TDA_OK 0
@@ -130,6 +130,11 @@ typedef struct tda_rips_result {
     const void *blob;
     int64_t blob_bytes;
     int64_t n_pairs;
+    /* ABI >= 4: [L][N][N] float64 distances (sqrt in f64 before any rounding:
+     * what sklearn's pairwise_distances returns for float64 points and
+     * ripser.py hands back as dperm2all) when args.flags & TDA_FLAG_DIST64,
+     * want_dist and float64 point clouds, else NULL */
+    const double *dist64;
 } tda_rips_result;
 
 #define TDA_FLAG_STAGE_TIMES 1
@@ -137,6 +142,8 @@ typedef struct tda_rips_result {
  * is one kernel's duration (no overlap with, or queueing behind, the side
  * streams); for per-kernel measurement only */
 #define TDA_FLAG_STAGE_SERIAL 2
+/* with want_dist and float64 point clouds: also return result->dist64 */
+#define TDA_FLAG_DIST64 4
 
 /* Batched point clouds (or distance matrices) -> persistence diagrams. */
 int tda_rips_batch(const tda_rips_args *args, tda_rips_result **out);
@@ -151,6 +158,26 @@ const char *tda_last_error(void);
 int tda_version(void);
 /* 1 if a gfx950 device is visible, 0 otherwise (never aborts). */
 int tda_device_ok(int32_t device);
+
+/*
+ * Normalised effective dimensionality of B activation matrices (B, N, D):
+ * replaces the reference's TorchScript compute_effective_dimensionality
+ * (metrics.py:5-44): S = svdvals(X_b), ED_b = (sum S)^2 /
+ * max(sum S^2, 1e-10) / max(min(N, D), 1), as float32 into out[B] (host).
+ * The squared singular values are the eigenvalues of the f64 Gram matrix
+ * (X X^T on the FP64 matrix cores when N <= D, X^T X otherwise), found by
+ * parallel Jacobi on the GPU (csrc/ed_kernels.h).  min(N, D) <= 1024.
+ */
+typedef struct tda_ed_args {
+    const void *x;          /* (B, N, D) row-major, host or device               */
+    int32_t dtype;          /* TDA_F32 | TDA_F64                                 */
+    int32_t x_on_device;    /* 1: x is a device pointer on `device`              */
+    int64_t B, N, D;
+    int32_t device;
+    void *stream;           /* hipStream_t or NULL: device input is read after it */
+} tda_ed_args;
+
+int tda_effective_dim(const tda_ed_args *args, float *out);
 
 #ifdef __cplusplus
 }

@@ -103,3 +103,54 @@ def knn_preservation(X: np.ndarray, Y: np.ndarray, k: int, metric: str = "euclid
     a = np.argsort(DX, 1)[:, :k]
     b = np.argsort(DY, 1)[:, :k]
     return float(np.mean([len(set(a[i]) & set(b[i])) / k for i in range(n)]))
+
+
+def transform_init(X_train: np.ndarray, emb: np.ndarray, Y: np.ndarray, n_neighbors: int, metric: str = "euclidean",
+                   disconnection: float = np.inf) -> np.ndarray:
+    """umap-learn UMAP.transform up to the initial embedding (what the GPU
+    returns with learning_rate 0): distances to the training points, the
+    n_neighbors nearest (ties: smaller index), smooth_knn_dist with
+    local_connectivity 0 (rho = 0; slot 0 skipped in the bisection as umap
+    does), bipartite memberships without entries at >= the disconnection
+    distance, then init_graph_transform (f32 weighted mean, or the
+    neighbour's own embedding at membership 1, NaN without neighbours)."""
+    Z = np.concatenate([np.asarray(X_train), np.asarray(Y)]).astype(np.float32)
+    D = distances(Z, metric)
+    N, M, k = X_train.shape[0], Y.shape[0], n_neighbors
+    C = D[N:, :N]
+    idx = np.stack([np.lexsort((np.arange(N), C[i]))[:k] for i in range(M)])
+    kd = np.take_along_axis(C, idx, 1)
+    mean_all = float(np.mean(kd.astype(np.float64)))
+    target = np.log2(k)
+    out = np.empty((M, emb.shape[1]), np.float32)
+    for i in range(M):
+        d = kd[i].astype(np.float64)
+        lo, hi, mid = 0.0, np.inf, 1.0
+        for _ in range(64):
+            psum = float(np.sum(np.where(d[1:] > 0, np.exp(-(np.maximum(d[1:], 0) / mid)), 1.0)))
+            if abs(psum - target) < 1e-5:
+                break
+            if psum > target:
+                hi = mid
+                mid = (lo + hi) / 2.0
+            else:
+                lo = mid
+                mid = mid * 2.0 if np.isinf(hi) else (lo + hi) / 2.0
+        sigma = max(mid, 1e-3 * mean_all)
+        vals = np.array([0.0 if not kd[i, j] < disconnection else (1.0 if kd[i, j] <= 0.0 else np.exp(-(float(kd[i, j]) / sigma)))
+                         for j in range(k)], np.float32)
+        nz = vals != 0.0
+        if not nz.any():
+            out[i] = np.nan
+            continue
+        rs = np.float32(0.0)
+        for v in vals[nz]:
+            rs = np.float32(rs + v)
+        r = np.zeros(emb.shape[1], np.float32)
+        for j in np.flatnonzero(nz):
+            if vals[j] == 1.0:
+                r = emb[idx[i, j]].astype(np.float32).copy()
+                break
+            r = (r + np.float32(vals[j] / rs) * emb[idx[i, j]]).astype(np.float32)
+        out[i] = r
+    return out

@@ -8,7 +8,7 @@ include/tda_rips.h; no CPU fallback.
 import sys as _sys
 
 from . import distributed, metrics, synthetic, umap  # noqa: F401
-from .metrics import compute_intrinsic_dimensionality  # noqa: F401
+from .metrics import compute_effective_dimensionality, compute_intrinsic_dimensionality  # noqa: F401
 from ._lib import EXPORTS, LIB_PATH, build, lib  # noqa: F401
 from .pipeline import (get_max_persistence, get_persistence, layer_record, layer_record_adversarial, peak_layer,  # noqa: F401
                        run_adversarial_condition, run_sweep, write_layer_stats, write_summary_stats)
@@ -33,6 +33,7 @@ __all__ = [
     "peak_layer",
     "silhouette_score",
     "compute_intrinsic_dimensionality",
+    "compute_effective_dimensionality",
     "UMAP",
     "umap_batch",
     "umap_transform_batch",

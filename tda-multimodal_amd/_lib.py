@@ -77,11 +77,13 @@ class RipsResult(ctypes.Structure):
         ("blob", ctypes.c_void_p),
         ("blob_bytes", ctypes.c_int64),
         ("n_pairs", ctypes.c_int64),
+        ("dist64", ctypes.POINTER(ctypes.c_double)),
     ]
 
 
 TDA_FLAG_STAGE_TIMES = 1
 TDA_FLAG_STAGE_SERIAL = 2
+TDA_FLAG_DIST64 = 4
 
 
 class UmapArgs(ctypes.Structure):  # include/tda_umap.h
@@ -106,6 +108,19 @@ class UmapArgs(ctypes.Structure):  # include/tda_umap.h
         ("device", ctypes.c_int32),
         ("out", ctypes.c_void_p),
         ("graph_out", ctypes.c_void_p),
+        ("stream", ctypes.c_void_p),
+    ]
+
+
+class EdArgs(ctypes.Structure):  # include/tda_rips.h tda_ed_args
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("dtype", ctypes.c_int32),
+        ("x_on_device", ctypes.c_int32),
+        ("B", ctypes.c_int64),
+        ("N", ctypes.c_int64),
+        ("D", ctypes.c_int64),
+        ("device", ctypes.c_int32),
         ("stream", ctypes.c_void_p),
     ]
 
@@ -140,7 +155,7 @@ class UmapTransformArgs(ctypes.Structure):  # include/tda_umap.h
 
 # every symbol declared in include/tda_rips.h and include/tda_umap.h
 EXPORTS = ("tda_rips_batch", "tda_rips_dm", "tda_rips_free", "tda_last_error", "tda_version", "tda_device_ok",
-           "tda_umap_batch", "tda_umap_transform")
+           "tda_effective_dim", "tda_umap_batch", "tda_umap_transform")
 
 _lib = None
 
@@ -197,6 +212,8 @@ def lib():
     L.tda_device_ok.restype = ctypes.c_int
     L.tda_umap_batch.argtypes = [ctypes.POINTER(UmapArgs)]
     L.tda_umap_batch.restype = ctypes.c_int
+    L.tda_effective_dim.argtypes = [ctypes.POINTER(EdArgs), _f32p]
+    L.tda_effective_dim.restype = ctypes.c_int
     L.tda_umap_transform.argtypes = [ctypes.POINTER(UmapTransformArgs)]
     L.tda_umap_transform.restype = ctypes.c_int
     _lib = L

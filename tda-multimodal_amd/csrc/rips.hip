@@ -87,6 +87,7 @@ unsigned par_grid_size() {
 struct Plan {
     int64_t L = 0, N = 0, D = 0;
     int maxdim = 0, dtype = 0, is_dist = 0;
+    bool want64 = false;  // TDA_FLAG_DIST64: f64 distances of f64 points as well (dperm2all)
     uint64_t ncand[4] = {0}, piv_words[4] = {0}, rcap[4] = {0}, pcap[4] = {0};
     uint64_t mst_words = 0, max_rcap = 0, rmap_stride = 0, vpool_cap = 0, wcap_g = 0, vcap_g = 0, sstride = 0;
     bool lds_mode = false;
@@ -98,7 +99,8 @@ struct Plan {
     uint64_t ecap = 0;    // per-layer stride of the sorted edge lengths
     size_t o_dsort = 0, o_dtmp = 0, o_dcode = 0;
     int dsplit = 1;       // K slices of k_distance_mfma (1: no split)
-    size_t o_gpart = 0, o_npart = 0;
+    size_t o_gpart = 0, o_npart = 0, o_d64 = 0;
+    size_t o_bcomp = 0, o_bcheap = 0, o_bctl = 0;  // Borůvka H0 state (N > kH0WaveMaxN)
     bool serial_tables = false;  // HBM working tables of k_reduce_all (global mode) / k_reduce_big
     uint64_t ostride = 0, rec_cap = 0, rpool_cap = 0, bpool_cap = 0, rq_cap = 0;
     size_t o_pctl = 0, o_pitem = 0, o_pokey = 0, o_poval = 0, o_colpiv = 0, o_prec = 0, o_prpool = 0, o_pbpool = 0, o_prq = 0;
@@ -277,6 +279,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         }
     }
     p.o_dist = take(L * N * N * 4);
+    if (p.want64) p.o_d64 = take(L * N * N * 8);
     p.memset_lo = o;
     p.o_stats = take(L * sizeof(LayerStats));
     p.o_mst = take(L * p.mst_words * 4);
@@ -325,7 +328,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
             // + chunks 0..3 of the 33 buckets of every k_reduce_par workgroup
             // above N = 1024 start at 4x (torus N=2048 overflows 2x: measured r02, 3 attempts per call)
             const int big4 = N > 1024 ? 2 : 0;
-            p.bpool_cap = (clampp(N * N * 128, 24, 30) << (scale + big4)) + (uint64_t)kParGrid * 33 * 3840;
+            p.bpool_cap = (clampp(N * N * 128, 24, 30) << (scale + big4)) + (uint64_t)kParGrid * kParLv * 3840;
             // H2 records as well: grid144 (32 layers) stores ~4.4 M keys of reduced H2 columns
             p.rpool_cap = clampp(std::max<uint64_t>(N * N * 64, p.par2 ? L * N * N * 8 : 0), 22, 29) << (scale + big4);
             p.rq_cap = 1ull << 16;
@@ -365,6 +368,11 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     }
     for (int d = 0; d <= p.maxdim; ++d) p.o_pairs[d] = take(L * p.pcap[d] * sizeof(Pair));
     p.o_h0s = take(L * 2 * N * 8 + 64);
+    if (N > (uint64_t)kSmallN) {
+        p.o_bcomp = take(L * N * 4);
+        p.o_bcheap = take(L * N * 8);
+        p.o_bctl = take(L * sizeof(BorCtl));
+    }
     p.o_fk = take(L * 2 * p.sstride * 8);
     p.o_fv = take(L * 2 * p.sstride * 4);
     p.o_pptr = take(4 * sizeof(void*));
@@ -554,6 +562,7 @@ int set_lds_attrs(int dev) {
     if (dev < 64 && g_attr_done[dev]) return 0;
     HIPC(hipFuncSetAttribute((const void*)k_h0<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_h0<kH0WaveQ, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_bor_hook, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
     HIPC(hipFuncSetAttribute((const void*)k_sort_resid, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEmitLds));
 #define TDA_ATTR_RED(LW, P1, P2) \
@@ -601,6 +610,7 @@ struct ResultImpl {
     tda_rips_result pub;
     std::vector<uint64_t> blob;  // meta | num_edges | birth_idx, death_idx | thresh (padded) | birth, death
     std::vector<float> dist, stage_ms, tn;
+    std::vector<double> dist64;
     std::vector<double> sil;
     std::vector<const char*> stage_name;
 };
@@ -630,6 +640,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     p.maxdim = a.maxdim;
     p.dtype = a.dtype;
     p.is_dist = input_kind != 0;
+    p.want64 = input_kind == 0 && a.dtype == TDA_F64 && a.want_dist && (a.flags & TDA_FLAG_DIST64);
     make_plan(p, force_global, scale, force_big, no_par);
     const int dev = a.device;
     HIPC(hipSetDevice(dev));
@@ -791,24 +802,25 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         const unsigned nt = (unsigned)((n + kDmT - 1) / kDmT);
         double* gpart = (double*)(B + p.o_gpart);
         double* npart = (double*)(B + p.o_npart);
+        double* d64 = p.want64 ? (double*)(B + p.o_d64) : nullptr;
         const dim3 gsplit(nt * (nt + 1) / 2, L, (unsigned)p.dsplit);
         const dim3 gcomb((unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256), L);
         if (mfma && p.dsplit > 1 && p.dtype == TDA_F64) {
             hipLaunchKernelGGL((k_distance_mfma<double, 0, true>), gsplit, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax,
-                               gpart, npart);
-            hipLaunchKernelGGL((k_distance_combine<double, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
+                               gpart, npart, (double*)nullptr);
+            hipLaunchKernelGGL((k_distance_combine<double, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax, d64);
         } else if (mfma && p.dsplit > 1) {
             hipLaunchKernelGGL((k_distance_mfma<float, 0, true>), gsplit, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax,
                                gpart, npart);
             hipLaunchKernelGGL((k_distance_combine<float, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
         } else if (mfma && p.dtype == TDA_F64)
             hipLaunchKernelGGL((k_distance_mfma<double>), dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const double*)x, n, (int)p.D,
-                               dist, rowmax, (double*)nullptr, (double*)nullptr);
+                               dist, rowmax, (double*)nullptr, (double*)nullptr, d64);
         else if (mfma)
             hipLaunchKernelGGL((k_distance_mfma<float>), dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const float*)x, n, (int)p.D,
                                dist, rowmax, (double*)nullptr, (double*)nullptr);
         else if (p.dtype == TDA_F64)
-            hipLaunchKernelGGL(k_distance<double>, grid, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax);
+            hipLaunchKernelGGL(k_distance<double>, grid, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax, d64);
         else
             hipLaunchKernelGGL(k_distance<float>, grid, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax);
     } else {
@@ -853,7 +865,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                                (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
         } else {
             int T = n <= 256 ? 256 : 1024;
-            size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8;
+            // best | par | red | sort chunk | (LDS rows) | Borůvka hooks
+            size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8 + (size_t)n * 4;
             base = align_up(base, 16);
             // n <= kH0WaveMaxN: one-wave Prim on the LDS-staged matrix (sort chunk just covers the forest)
             const bool wave_ok = !test_env_is("TDA_H0_WAVE", "0");
@@ -865,12 +878,32 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             else
                 while (ch * 2 * 8 <= avail && ch * 2 <= 16384) ch *= 2;
             size_t lds = base + ch * 8 + (dlds ? (size_t)4 * n * n : 0);
-            if (dlds)
+            if (dlds) {
                 hipLaunchKernelGGL((k_h0<kH0WaveQ, true>), dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst),
-                                   p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
-            else
+                                   p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch),
+                                   (const BorCtl*)nullptr);
+            } else {  // Borůvka over the whole GPU: ceil(log2 N) rounds of (cheapest edges, hooking)
+                int32_t* bcomp = (int32_t*)(B + p.o_bcomp);
+                uint64_t* bcheap = (uint64_t*)(B + p.o_bcheap);
+                BorCtl* bctl = (BorCtl*)(B + p.o_bctl);
+                hipLaunchKernelGGL(k_bor_init, dim3(L), dim3(256), 0, s4, rowmax, n, a.thresh, stats, bcomp, bcheap, bctl);
+                const size_t hl = (size_t)((n + 3) & ~3) * 8 + (size_t)n * 8;
+                const int rounds = std::max(1, ilog2(next_pow2((uint64_t)n)));
+                for (int r = 0; r < rounds; ++r) {
+                    hipLaunchKernelGGL(k_bor_min, dim3((unsigned)((n + 3) / 4), L), dim3(256), 0, s4, dist, n, stats, bcomp, bcheap, bctl,
+                                       r == 0 ? 1 : 0);
+                    if (r == 0)
+                        if (int rc = tm4.mark("k_bor_min")) return rc;
+                    hipLaunchKernelGGL(k_bor_hook, dim3(L), dim3(1024), hl, s4, n, bcomp, bcheap, bctl, (uint64_t*)(B + p.o_h0s));
+                    if (r == 0)
+                        if (int rc = tm4.mark("k_bor_hook")) return rc;
+                }
+                HIPC(hipGetLastError());
+                if (int rc = tm4.mark("k_bor_rounds")) return rc;
                 hipLaunchKernelGGL((k_h0<0, false>), dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst),
-                                   p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch));
+                                   p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch),
+                                   (const BorCtl*)bctl);
+            }
         }
         HIPC(hipGetLastError());
         if (int rc = tm4.mark("k_h0")) return rc;
@@ -1366,9 +1399,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)q[4], (unsigned long long)((q[7] >> 16) & 0xFFFF), (unsigned long long)q[5], (unsigned long long)(q[7] & 0xFFFF),
                 (unsigned long long)((q[7] >> 32) & 0xFFFF), (unsigned long long)(q[7] >> 48));
         const uint64_t* u = w.hstats[0].prof[3];
-        fprintf(stderr, "[tda-prof]   inside adds: keys %llu, capacity %llu, front toggles %llu, bucket appends %llu cycles; %llu record adds (%llu keys); refills moved %llu keys; waiting for the slowest wave's rows %llu\n",
+        fprintf(stderr, "[tda-prof]   inside adds: keys %llu, capacity %llu, front toggles %llu, bucket appends %llu cycles; %llu record adds (%llu keys); refills moved %llu keys; wave 0 toggled %llu front / %llu back keys\n",
                 (unsigned long long)u[0], (unsigned long long)u[3], (unsigned long long)u[1], (unsigned long long)u[2],
-                (unsigned long long)u[4], (unsigned long long)u[5], (unsigned long long)u[6], (unsigned long long)u[7]);
+                (unsigned long long)u[4], (unsigned long long)u[5], (unsigned long long)u[6], (unsigned long long)(u[7] >> 32),
+                (unsigned long long)(u[7] & 0xFFFFFFFFull));
         const uint64_t* v = w.hstats[0].prof[4];
         fprintf(stderr, "[tda-prof]   record adds: room %llu, col_add %llu cycles, keys front %llu / all %llu; refill pass 3 %llu cycles; %llu saves (%llu keys) %llu cycles\n",
                 (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2], (unsigned long long)v[3], (unsigned long long)v[5],
@@ -1456,6 +1490,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         R->dist.resize((size_t)L * n * n);
         HIPC(hipMemcpy(R->dist.data(), dist, sizeof(float) * L * n * n, hipMemcpyDeviceToHost));
     }
+    if (p.want64) {
+        R->dist64.resize((size_t)L * n * n);
+        HIPC(hipMemcpy(R->dist64.data(), B + p.o_d64, sizeof(double) * L * n * n, hipMemcpyDeviceToHost));
+    }
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, w.ev0, w.ev1);
     tda_rips_result& o = R->pub;
@@ -1479,6 +1517,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     o.n_residual = m_res;
     o.n_adds = m_add;
     o.dist = a.want_dist ? R->dist.data() : nullptr;
+    o.dist64 = p.want64 ? R->dist64.data() : nullptr;
     if (nls) {
         R->sil.assign((const double*)(w.hsil + sil_out_off), (const double*)(w.hsil + sil_out_off) + (size_t)L * nls);
         o.silhouette = R->sil.data();
@@ -1639,3 +1678,5 @@ int tda_device_ok(int32_t device) {
 
 // UMAP embedding (include/tda_umap.h): same library, same error state
 #include "umap_host.h"
+// effective dimensionality (include/tda_rips.h tda_effective_dim)
+#include "ed_host.h"

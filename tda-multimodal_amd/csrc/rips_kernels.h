@@ -72,7 +72,7 @@ struct DimBufs {              // per reduction dim d (columns = d-simplices)
 // like unsigned ints).  rowmax must be zeroed before the launch.
 template <typename T>
 __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n, int D, float* __restrict__ dist,
-                                                  uint32_t* __restrict__ rowmax) {
+                                                  uint32_t* __restrict__ rowmax, double* __restrict__ dist64 = nullptr) {
     constexpr int TS = 16, KC = 32;
     __shared__ double xi[TS][KC + 1], xj[TS][KC + 1];
     __shared__ uint32_t rmax_i[TS], rmax_j[TS];
@@ -109,6 +109,7 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
     if (i < n && j < n && j >= i) {
         if (i == j) {
             Dl[(size_t)i * n + i] = 0.0f;
+            if (dist64) dist64[((size_t)l * n + i) * n + i] = 0.0;
         } else {
             double d = (-2.0 * dot + ni) + nj;
             float f;
@@ -118,7 +119,9 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
                 f = sqrt_rn_f32(f);
             } else {
                 d = (d != d) ? d : fmax(d, 0.0);
-                f = (float)__dsqrt_rn(d);
+                const double r = __dsqrt_rn(d);
+                f = (float)r;
+                if (dist64) dist64[((size_t)l * n + i) * n + j] = dist64[((size_t)l * n + j) * n + i] = r + 0.0;
             }
             f = f + 0.0f;
             Dl[(size_t)i * n + j] = f;
@@ -160,7 +163,8 @@ typedef double dm_d4 __attribute__((ext_vector_type(4)));
 
 // METRIC 1: cosine distance instead (UMAP input, umap.distances.cosine:
 // 1 - <x,y> / sqrt(|x|^2 |y|^2), 0 for two zero rows, 1 for one), from the
-// same Gram tiles; clamped at 0.
+// same Gram tiles; clamped at 0.  METRIC 2: the raw f64 Gram matrix X X^T
+// (both triangles) into gpart (ed_kernels.h: effective dimensionality).
 // SPLIT (gridDim.z = S > 1 K slices, chosen on the host when the tiles alone
 // leave CUs idle -- raw4096: 6 tiles x 32 layers on 256 CUs): slice z sums
 // its K range and stores the tile's partial Gram and (diagonal tiles) the
@@ -169,7 +173,7 @@ typedef double dm_d4 __attribute__((ext_vector_type(4)));
 template <typename T, int METRIC = 0, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, int n, int D, float* __restrict__ dist,
                                                        uint32_t* __restrict__ rowmax, double* __restrict__ gpart = nullptr,
-                                                       double* __restrict__ npart = nullptr) {
+                                                       double* __restrict__ npart = nullptr, double* __restrict__ dist64 = nullptr) {
     __shared__ double xs[2][kDmT][kDmS];  // [i/j tile][row][k]
     __shared__ double nrm[2][kDmT];
     __shared__ uint32_t rmx[2][kDmT];
@@ -256,6 +260,21 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
         if (bi == bj && tid < kDmT && bi * kDmT + tid < n) npart[zo * n + bi * kDmT + tid] = nrm[0][tid];
         return;
     }
+    if constexpr (METRIC == 2) {  // raw f64 Gram matrix into gpart [L][n][n] (effective dimensionality)
+        double* G = gpart + (size_t)l * n * n;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = bi * kDmT + wr * 32 + a * 16 + (lane >> 4) + 4 * r, j = bj * kDmT + wc * 32 + b * 16 + (lane & 15);
+                    if (i >= n || j >= n || j < i) continue;
+                    G[(size_t)i * n + j] = acc[a][b][r];
+                    G[(size_t)j * n + i] = acc[a][b][r];
+                }
+        return;
+    }
     float* Dl = dist + (size_t)l * n * n;
     // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
@@ -269,6 +288,7 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
                 if (i >= n || j >= n || j < i) continue;
                 if (i == j) {
                     Dl[(size_t)i * n + i] = 0.0f;
+                    if (dist64) dist64[((size_t)l * n + i) * n + i] = 0.0;
                     continue;
                 }
                 double d = (-2.0 * acc[a][b][r] + nrm[0][ri]) + nrm[1][cj];
@@ -283,7 +303,9 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
                     f = sqrt_rn_f32(f);
                 } else {
                     d = (d != d) ? d : fmax(d, 0.0);
-                    f = (float)__dsqrt_rn(d);
+                    const double r64 = __dsqrt_rn(d);
+                    f = (float)r64;
+                    if (dist64) dist64[((size_t)l * n + i) * n + j] = dist64[((size_t)l * n + j) * n + i] = r64 + 0.0;
                 }
                 f = f + 0.0f;
                 Dl[(size_t)i * n + j] = f;
@@ -302,14 +324,18 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
 // the K slices of k_distance_mfma<..., SPLIT>: fixed-order sums, then the same epilogue
 template <typename T, int METRIC = 0>
 __global__ __launch_bounds__(256) void k_distance_combine(const double* __restrict__ gpart, const double* __restrict__ npart, int S, int n,
-                                                          float* __restrict__ dist, uint32_t* __restrict__ rowmax) {
+                                                          float* __restrict__ dist, uint32_t* __restrict__ rowmax,
+                                                          double* __restrict__ dist64 = nullptr) {
     const int l = blockIdx.y;
     const size_t nn = (size_t)n * n;
     float* Dl = dist + (size_t)l * nn;
     uint32_t* rm = rowmax + (size_t)l * n;
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nn; q += (size_t)gridDim.x * blockDim.x) {
         const int i = (int)(q / n), j = (int)(q - (size_t)i * n);
-        if (i == j) Dl[q] = 0.0f;
+        if (i == j) {
+            Dl[q] = 0.0f;
+            if (dist64) dist64[(size_t)l * nn + q] = 0.0;
+        }
         if (i >= j) continue;
         double g = 0.0, ni = 0.0, nj = 0.0;
         for (int z = 0; z < S; ++z) {
@@ -329,7 +355,9 @@ __global__ __launch_bounds__(256) void k_distance_combine(const double* __restri
         } else {
             double d = (-2.0 * g + ni) + nj;
             d = (d != d) ? d : fmax(d, 0.0);
-            f = (float)__dsqrt_rn(d);
+            const double r64 = __dsqrt_rn(d);
+            f = (float)r64;
+            if (dist64) dist64[(size_t)l * nn + q] = dist64[(size_t)l * nn + (size_t)j * n + i] = r64 + 0.0;
         }
         f = f + 0.0f;
         Dl[q] = f;
@@ -504,7 +532,8 @@ __device__ void block_sort(uint64_t* keys, uint32_t* vals, uint64_t n, uint64_t*
 // ------------------------------------------------------------------ H0
 // Threshold (ripser.py rips_dm: enclosing radius when thresh is inf/FLT_MAX),
 // num_edges, minimum spanning forest under the total order (diam asc, idx
-// desc) by Prim (unique forest == Kruskal's), then Kruskal-order emission and
+// desc) by Prim (one wave, N <= 190) or Borůvka (block) -- the unique forest,
+// i.e. Kruskal's -- then Kruskal-order emission and
 // elder-rule union-find [upstream compute_dim_0_pairs], consumed at
 // debug_tda_pipeline.py:112, :126.
 // LDS: best[N] u64, intree[N] u8 ... par[N] int  (N <= 8192)
@@ -521,13 +550,147 @@ __device__ void block_sort(uint64_t* keys, uint32_t* vals, uint64_t n, uint64_t*
 // global memory (WQ = 16, N = 1024) measured slower than the block path
 // (torus1024: 3.95 vs 3.57 ms, latency-bound row loads), so above N = 190 the
 // block path stays.
+// ------------------------------------------------------------------ H0 above N = kH0WaveMaxN: Borůvka over the GPU
+// (r03; replaces a block-wide Prim of N - 1 dependent steps, torus1024 3.6 ms).
+// k_bor_init: threshold (enclosing radius = min row maximum) and per-layer
+// state; then ceil(log2 N) rounds of k_bor_min (one wave per vertex: its
+// cheapest edge <= thresh to another component under the total order (diam
+// asc, idx desc) -> atomicMin on its component's slot; round 0 also counts
+// num_edges) and k_bor_hook (one workgroup per layer, in LDS: every root
+// hooks to the other endpoint's root -- keys are unique, so the only cycles
+// are mutual pairs, whose smaller root stays -- the hooking edges are the
+// new forest edges, pointer jumping flattens the components).  The forest is
+// the unique minimum spanning forest of the total order, i.e. Kruskal's;
+// k_h0<0, false> then sorts it and runs the elder rule.
+struct BorCtl {
+    unsigned long long nmst;  // forest edges found
+    uint32_t done, pad;
+};
+
+__global__ __launch_bounds__(256) void k_bor_init(const uint32_t* __restrict__ rowmax, int n, float user_thresh,
+                                                  LayerStats* __restrict__ stats, int32_t* __restrict__ comp,
+                                                  uint64_t* __restrict__ cheap, BorCtl* __restrict__ ctl) {
+    __shared__ uint32_t s_min;
+    const int l = blockIdx.x;
+    const float thr = block_thresh(rowmax + (size_t)l * n, n, user_thresh, &s_min);
+    for (int v = threadIdx.x; v < n; v += blockDim.x) {
+        comp[(size_t)l * n + v] = v;
+        cheap[(size_t)l * n + v] = kEmpty64;
+    }
+    if (threadIdx.x == 0) {
+        stats[l].thresh = thr;
+        stats[l].num_edges = 0;
+        ctl[l].nmst = 0;
+        ctl[l].done = 0;
+    }
+}
+
+constexpr int kBorLoads = 8;  // row loads in flight per lane
+__global__ __launch_bounds__(256) void k_bor_min(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                 const int32_t* __restrict__ comp, uint64_t* __restrict__ cheap,
+                                                 const BorCtl* __restrict__ ctl, int first) {
+    const int l = blockIdx.y, u = blockIdx.x * 4 + (threadIdx.x >> 6), ln = threadIdx.x & 63;
+    if (u >= n || ctl[l].done) return;
+    const float thr = stats[l].thresh;
+    const float* row = dist + ((size_t)l * n + u) * n;
+    const int32_t* cl = comp + (size_t)l * n;
+    const int cu = cl[u];
+    uint64_t mk = kEmpty64;
+    unsigned long long cnt = 0;
+    for (int v0 = 0; v0 < n; v0 += 64 * kBorLoads) {
+        float d[kBorLoads];
+        int32_t c[kBorLoads];
+#pragma unroll
+        for (int q = 0; q < kBorLoads; ++q) {
+            const int v = v0 + ln + 64 * q;
+            d[q] = v < n ? row[v] : INFINITY;
+            c[q] = v < n ? cl[v] : cu;
+        }
+#pragma unroll
+        for (int q = 0; q < kBorLoads; ++q) {
+            const int v = v0 + ln + 64 * q;
+            if (!(d[q] <= thr)) continue;
+            cnt += v > u;
+            if (c[q] == cu) continue;
+            const int a = u > v ? u : v, b = u > v ? v : u;
+            const uint64_t k = filt_key(d[q], binom((uint64_t)a, 2) + b);
+            mk = k < mk ? k : mk;
+        }
+    }
+    mk = wave_min_u64(mk);
+    if (ln == 0 && mk != kEmpty64) atomicMin((unsigned long long*)&cheap[(size_t)l * n + cu], (unsigned long long)mk);
+    if (first) {
+        cnt = wave_sum_u64(cnt);
+        if (ln == 0 && cnt) atomicAdd((unsigned long long*)&stats[l].num_edges, cnt);
+    }
+}
+
+// LDS: comp n x i32 | hook n x i32 | cheap n x u64
+__global__ __launch_bounds__(1024) void k_bor_hook(int n, int32_t* __restrict__ comp, uint64_t* __restrict__ cheap,
+                                                   BorCtl* __restrict__ ctl, uint64_t* __restrict__ scratch /* [L][2n] */) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t flag[2], s_any;
+    const int l = blockIdx.x, t = threadIdx.x, T = blockDim.x;
+    if (ctl[l].done) return;
+    int32_t* cs = (int32_t*)smem;
+    int32_t* hook = cs + ((n + 3) & ~3);
+    uint64_t* ch = (uint64_t*)(hook + ((n + 3) & ~3));
+    int32_t* cg = comp + (size_t)l * n;
+    uint64_t* chg = cheap + (size_t)l * n;
+    uint64_t* mst = scratch + (size_t)l * 2 * n;
+    for (int v = t; v < n; v += T) {
+        cs[v] = cg[v];
+        ch[v] = chg[v];
+        chg[v] = kEmpty64;  // ready for the next round
+    }
+    if (t < 2) flag[t] = 0;
+    if (t == 0) s_any = 0;
+    __syncthreads();
+    for (int r = t; r < n; r += T) {
+        hook[r] = r;
+        if (cs[r] != r || ch[r] == kEmpty64) continue;
+        s_any = 1;
+        const uint64_t eidx = 0xFFFFFFFFull - (ch[r] & 0xFFFFFFFFull);
+        const int a = max_vertex(eidx, 2, n - 1), b = (int)(eidx - binom((uint64_t)a, 2));
+        const int ca = cs[a], cb = cs[b];
+        const int other = ca == r ? cb : ca;
+        if (ch[other] == ch[r] && r < other) continue;  // the smaller root of a mutual pair stays a root
+        hook[r] = other;
+        const unsigned long long pos = atomicAdd(&ctl[l].nmst, 1ull);
+        if (pos < (unsigned long long)n) mst[pos] = ch[r];  // every forest edge once: a mutual edge by its larger root
+    }
+    __syncthreads();
+    if (!s_any) {  // no component has an edge <= thresh to another: the forest is complete
+        if (t == 0) ctl[l].done = 1;
+        return;
+    }
+    for (int it = 0; it < 32; ++it) {  // pointer jumping on the hook forest (depth < n)
+        bool ch2 = false;
+        for (int r = t; r < n; r += T) {
+            const int h = hook[r], hh = hook[h];
+            if (h != hh) {
+                hook[r] = hh;
+                ch2 = true;
+            }
+        }
+        if (ch2) flag[it & 1] = 1;
+        __syncthreads();
+        const bool again = flag[it & 1] != 0;
+        __syncthreads();
+        if (t == 0) flag[it & 1] = 0;
+        if (!again) break;
+    }
+    for (int v = t; v < n; v += T) cg[v] = hook[cs[v]];
+}
+
 constexpr int kH0WaveMaxN = 190;  // 4 n^2 B of LDS staging
 constexpr int kH0WaveQ = (kH0WaveMaxN + 63) / 64;
 template <int WQ, bool LROWS>
 __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int n, float user_thresh,
                                              LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
                                              uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0,
-                                             uint64_t* __restrict__ scratch /* [L][2n] */, int sort_log2) {
+                                             uint64_t* __restrict__ scratch /* [L][2n] */, int sort_log2,
+                                             const BorCtl* __restrict__ bctl = nullptr) {
     constexpr bool dlds = LROWS;   // the layer's matrix is staged in LDS
     constexpr bool wave = WQ > 0;  // one-wave Prim + elder rule
     constexpr int QA = WQ > 0 ? WQ : 1;  // register-array extent (unused when !wave)
@@ -550,50 +713,51 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         __syncthreads();
     }
 
-    // -- threshold
-    float thr = user_thresh;
-    if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) {
-        float local = INFINITY;
-        for (int i = w; i < n; i += nw) {
-            float r = -INFINITY;
-            for (int j = ln; j < n; j += 64) r = fmaxf(r, dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]);
-            for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
-            local = fminf(local, r);
-        }
-        if (ln == 0) ((float*)red)[w] = local;
-        __syncthreads();
-        if (t == 0) {
-            float e = INFINITY;
-            for (int q = 0; q < nw; ++q) e = fminf(e, ((float*)red)[q]);
-            s_thresh = e;
-        }
-        __syncthreads();
-        thr = s_thresh;
-    }
-    // -- num_edges
-    if (t == 0) s_cnt = 0;
-    __syncthreads();
-    {
-        unsigned long long c = 0;
-        for (int i = w; i < n; i += nw)
-            for (int j = i + 1 + ln; j < n; j += 64) c += (dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]) <= thr;
-        atomicAdd(&s_cnt, c);
-    }
-    // -- Prim
-    for (int v = t; v < n; v += T) {
-        best[v] = kEmpty64;
-        par[v] = 0;  // par doubles as in-tree flag during Prim
-    }
-    __syncthreads();
-    if (t == 0) {
-        st->thresh = thr;
-        st->num_edges = (int64_t)s_cnt;
-        s_cur = 0;
-        par[0] = 1;
-    }
-    __syncthreads();
     uint64_t* mst = scratch + (size_t)l * 2 * n;  // MST edge keys
     int nmst = 0;
+    float thr = user_thresh;
+    if constexpr (wave) {
+        // -- threshold
+        if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) {
+            float local = INFINITY;
+            for (int i = w; i < n; i += nw) {
+                float r = -INFINITY;
+                for (int j = ln; j < n; j += 64) r = fmaxf(r, dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]);
+                for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
+                local = fminf(local, r);
+            }
+            if (ln == 0) ((float*)red)[w] = local;
+            __syncthreads();
+            if (t == 0) {
+                float e = INFINITY;
+                for (int q = 0; q < nw; ++q) e = fminf(e, ((float*)red)[q]);
+                s_thresh = e;
+            }
+            __syncthreads();
+            thr = s_thresh;
+        }
+        // -- num_edges
+        if (t == 0) s_cnt = 0;
+        __syncthreads();
+        {
+            unsigned long long c = 0;
+            for (int i = w; i < n; i += nw)
+                for (int j = i + 1 + ln; j < n; j += 64) c += (dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]) <= thr;
+            atomicAdd(&s_cnt, c);
+        }
+        __syncthreads();
+        if (t == 0) {
+            st->thresh = thr;
+            st->num_edges = (int64_t)s_cnt;
+        }
+    } else {
+        // the forest, threshold and num_edges come from k_bor_* (one pass per Borůvka round over the whole GPU)
+        nmst = (int)min(bctl[l].nmst, (unsigned long long)n);
+        thr = st->thresh;
+    }
+    (void)s_cur;
+    (void)best;
+    (void)thr;
     if constexpr (wave) {  // one-wave Prim (rows from LDS, or global memory)
         if (w == 0) {
             uint64_t bst[QA];
@@ -642,57 +806,6 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         if (w == 0 && ln == 0) red[34] = (uint64_t)nmst;
         __syncthreads();
         nmst = (int)red[34];
-    }
-    for (int it = 1; it < (wave ? 0 : n); ++it) {
-        const int cur = s_cur;
-        uint64_t mk = kEmpty64;
-        for (int v = t; v < n; v += T) {
-            if (par[v]) continue;
-            float d = Dl[(size_t)cur * n + v];
-            if (d <= thr) {
-                int a = cur > v ? cur : v, b = cur > v ? v : cur;
-                uint64_t k = filt_key(d, binom((uint64_t)a, 2) + b);
-                if (k < best[v]) best[v] = k;
-            }
-            // candidate: (key, v) packed; key unique per edge, ties impossible
-            uint64_t bk = best[v];
-            if (bk < mk) mk = bk;
-        }
-        // find min key (and the vertex that owns it) across the block
-        uint64_t wm = wave_min_u64(mk);
-        if (ln == 0) red[w] = wm;
-        __syncthreads();
-        if (t == 0) {
-            uint64_t m = kEmpty64;
-            for (int q = 0; q < nw; ++q) m = red[q] < m ? red[q] : m;
-            red[32] = m;
-        }
-        __syncthreads();
-        const uint64_t gmin = red[32];
-        if (gmin == kEmpty64) {
-            // new component: smallest vertex not in the forest
-            if (t == 0) red[33] = (uint64_t)n;
-            __syncthreads();
-            for (int v = t; v < n; v += T)
-                if (!par[v]) atomicMin((unsigned long long*)&red[33], (unsigned long long)v);
-            __syncthreads();
-            if (t == 0) {
-                s_cur = (int)red[33];
-                par[s_cur] = 1;
-            }
-        } else {
-            // the new vertex is the non-tree endpoint of edge gmin
-            if (t == 0) {
-                uint64_t eidx = 0xFFFFFFFFull - (gmin & 0xFFFFFFFFull);
-                int a = max_vertex(eidx, 2, n - 1), b = (int)(eidx - binom((uint64_t)a, 2));
-                int nv = par[a] ? b : a;
-                par[nv] = 1;
-                s_cur = nv;
-                mst[nmst] = gmin;
-            }
-            ++nmst;
-        }
-        __syncthreads();
     }
     // -- Kruskal order of the forest edges
     block_sort<false>(mst, nullptr, (uint64_t)nmst, mst + n, nullptr, sk, nullptr, sort_log2);

@@ -49,10 +49,16 @@ namespace tda {
 
 constexpr int kParT = 256;
 constexpr int kParW = kParT / 64;
-constexpr uint32_t kFrontLog = 4096;   // front log entries (live + cancelled)
-constexpr uint32_t kFrontIdx = 4096;   // front index slots (512 buckets x 8)
-constexpr uint32_t kFrontLive = 1792;  // live front keys that trigger a spill
-constexpr uint32_t kFrontFill = 768;   // refill / spill target
+#ifndef TDA_PAR_LOG  // build-time A/B knobs (tools/): front capacity and refill target
+#define TDA_PAR_LOG 4096
+#endif
+#ifndef TDA_PAR_FILL
+#define TDA_PAR_FILL 768
+#endif
+constexpr uint32_t kFrontLog = TDA_PAR_LOG;          // front log entries (live + cancelled)
+constexpr uint32_t kFrontIdx = TDA_PAR_LOG;          // front index slots (kFrontIdx / 8 buckets x 8)
+constexpr uint32_t kFrontLive = TDA_PAR_LOG * 7 / 16;  // live front keys that trigger a spill (1792 at 4096)
+constexpr uint32_t kFrontFill = TDA_PAR_FILL;        // refill / spill target
 constexpr int kParChunks = 22;         // chunk k of an HBM bucket holds 256 << k keys
 constexpr int kParRegs = 8;            // keys per thread per pass of refills and record adds
 constexpr int kParRefill = 2;          // a refill keeps up to kParRefill passes (4096 keys) in registers
@@ -114,9 +120,17 @@ __device__ __forceinline__ uint64_t aadd(unsigned long long* p, unsigned long lo
 }
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ uint32_t par_bucket(uint32_t dbits, uint32_t last) {
-    const uint32_t x = dbits ^ last;
-    return x ? 32u - (uint32_t)__builtin_clz(x) : 0u;
+// Radix levels over the WHOLE 64-bit key (r03): level of key k relative to
+// the reference `last` (a lower bound of every key in the column) is the
+// position of the highest differing bit, 0 .. 64.  With levels on the high
+// word only (r02), every key of one diameter (or, for the wide H2 keys, one
+// edge code) shared level 0, which the front had to hold at once: torus1024's
+// H2 columns exceeded it and fell back to the serial reducer.  Level 0 now
+// means equal keys, which cancel in the front.
+constexpr int kParLv = 65;
+__device__ __forceinline__ uint32_t par_bucket(uint64_t key, uint64_t last) {
+    const uint64_t x = key ^ last;
+    return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u;
 }
 __device__ __forceinline__ uint32_t chunk_of(uint32_t s) { return 31u - (uint32_t)__builtin_clz((s >> 8) + 1u); }
 __host__ __device__ constexpr uint32_t chunk_start(uint32_t k) { return ((1u << k) - 1u) << 8; }
@@ -137,15 +151,15 @@ __device__ __forceinline__ uint32_t tri_lo(int x, int y, int z, int f) {
 struct ParLds {
     uint64_t log[kFrontLog];
     uint64_t idx[kFrontIdx];
-    uint32_t bcnt[33];
-    uint32_t cptr[33][kParChunks];
-    uint32_t hist[33];
+    uint32_t bcnt[kParLv];
+    uint32_t cptr[kParLv][kParChunks];
+    uint32_t hist[kParLv];
     uint64_t red[2][kParW];
     uint32_t wsum[2][kParW];
     uint32_t anyf[2][kParW];
     uint64_t bc[8];
+    uint64_t last;  // radix reference: a lower bound of every key of the column
     uint32_t fcnt;  // front log length
-    uint32_t last;  // radix reference (diameter bits)
     uint32_t kf;    // front holds levels 0..kf
     int32_t err;
     uint32_t wide;  // wide H2 keys: the low 32 bits (index fingerprint) are not unique -> verify hits
@@ -334,12 +348,13 @@ __device__ __forceinline__ uint64_t front_min(ParRed& rd) {
 // order; rebuild the index.  Returns the new length (block-uniform).
 __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
     __syncthreads();
-    const uint32_t c = PS.fcnt, last = PS.last;
+    const uint32_t c = PS.fcnt;
+    const uint64_t last = PS.last;
     uint32_t w = 0;
     for (uint32_t e0 = 0; e0 < c; e0 += kParT) {
         const uint32_t e = e0 + threadIdx.x;
         const uint64_t x = e < c ? PS.log[e] : kEmpty64;
-        const bool lv = x < kDead && par_bucket((uint32_t)(x >> 32), last) <= keep;
+        const bool lv = x < kDead && par_bucket(x, last) <= keep;
         uint32_t tot;
         const uint32_t o = rd.prefix(lv ? 1u : 0u, &tot);  // barrier: the chunk has been read
         if (lv) PS.log[w + o] = x;                        // w + o <= e
@@ -422,7 +437,7 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
     lds_sync();
     if (PS.fcnt + need <= kFrontLog) return;
     PAR_T0(tc0);
-    uint32_t w = front_compact(C.rd, 33);
+    uint32_t w = front_compact(C.rd, kParLv);
 #ifdef TDA_PROFILE
     ++C.ncompact;
 #endif
@@ -431,10 +446,10 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
         ++C.nspill;
 #endif
         // histogram of the live front by level, keep the lowest levels up to kFrontFill
-        for (uint32_t q = threadIdx.x; q < 33; q += kParT) PS.hist[q] = 0;
+        for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
         __syncthreads();
-        const uint32_t last = PS.last;
-        for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket((uint32_t)(PS.log[e] >> 32), last)], 1u);
+        const uint64_t last = PS.last;
+        for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket(PS.log[e], last)], 1u);
         __syncthreads();
         int keep = -1;
         uint32_t cum = 0;
@@ -452,7 +467,7 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
         for (uint32_t e0 = 0; e0 < w; e0 += kParT) {
             const uint32_t e = e0 + threadIdx.x;
             uint64_t x[1] = {e < w ? PS.log[e] : 0};
-            uint32_t b[1] = {e < w ? par_bucket((uint32_t)(x[0] >> 32), last) : 0};
+            uint32_t b[1] = {e < w ? par_bucket(x[0], last) : 0};
             bucket_append<1>(x, b, (e < w && b[0] > (uint32_t)keep) ? 1u : 0u, P);
             __syncthreads();  // chunk pointers opened by this pass
         }
@@ -477,16 +492,20 @@ struct ParStash {
 template <int R>
 __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask,
                                         ParStash* stash = nullptr) {
-    const uint32_t last = PS.last, kf = PS.kf;
+    const uint64_t last = PS.last;
+    const uint32_t kf = PS.kf;
     uint32_t fm = 0, bm = 0, bb[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        bb[r] = par_bucket((uint32_t)(k[r] >> 32), last);
+        bb[r] = par_bucket(k[r], last);
         if ((vmask >> r) & 1u) {
             if (bb[r] <= kf) fm |= 1u << r;
             else bm |= 1u << r;
         }
     }
+#ifdef TDA_PROFILE
+    C.q[7] += (wave_sum_u64((uint64_t)__builtin_popcount(fm)) << 32) | wave_sum_u64((uint64_t)__builtin_popcount(bm));  // wave 0's front / back keys
+#endif
     PAR_T0(tf0);
     front_toggle<R>(k, fm);
     PAR_ACC(1, tf0);
@@ -530,7 +549,7 @@ __device__ __forceinline__ uint32_t bucket_batch(const ParBufs& P, uint32_t b, u
 __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     __syncthreads();
     int b = -1;
-    for (int q = (int)PS.kf + 1; q <= 32; ++q)
+    for (int q = (int)PS.kf + 1; q < kParLv; ++q)
         if (PS.bcnt[q]) {
             b = q;
             break;
@@ -543,7 +562,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     C.q[6] += c;
 #endif
     for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
-    for (uint32_t q = threadIdx.x; q < 33; q += kParT) PS.hist[q] = 0;
+    for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
     if (threadIdx.x == 0) PS.fcnt = 0;
     uint64_t x[kParRefill][kParRegs];
     uint32_t vm[kParRefill] = {};
@@ -565,21 +584,21 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
         }
     }
     mn = C.rd.min(mn);  // barrier: the resets above are done too
-    const uint32_t nl = (uint32_t)(mn >> 32);
+    const uint64_t nl = mn;
     // pass 2: histogram of the new levels (all < b)
     if (inreg) {
 #pragma unroll
         for (int h = 0; h < kParRefill; ++h)
 #pragma unroll
             for (int r = 0; r < kParRegs; ++r)
-                if ((vm[h] >> r) & 1u) atomicAdd(&PS.hist[par_bucket((uint32_t)(x[h][r] >> 32), nl)], 1u);
+                if ((vm[h] >> r) & 1u) atomicAdd(&PS.hist[par_bucket(x[h][r], nl)], 1u);
     } else {
         for (uint32_t e0 = 0; e0 < c; e0 += kPass) {
             uint64_t y[kParRegs];
             const uint32_t ym = bucket_batch(P, (uint32_t)b, e0, c, y);
 #pragma unroll
             for (int r = 0; r < kParRegs; ++r)
-                if ((ym >> r) & 1u) atomicAdd(&PS.hist[par_bucket((uint32_t)(y[r] >> 32), nl)], 1u);
+                if ((ym >> r) & 1u) atomicAdd(&PS.hist[par_bucket(y[r], nl)], 1u);
         }
     }
     __syncthreads();
@@ -611,11 +630,11 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     auto distribute = [&](const uint64_t (&y)[kParRegs], uint32_t ym) {
         // the front takes at most kFrontLive keys in all: compaction keeps room
         __syncthreads();  // chunk pointers opened by the previous pass
-        if (PS.fcnt + kParRegs * kParT > kFrontLog) front_compact(C.rd, 33);
+        if (PS.fcnt + kParRegs * kParT > kFrontLog) front_compact(C.rd, kParLv);
         uint32_t fm = 0, bm = 0, bb[kParRegs];
 #pragma unroll
         for (int r = 0; r < kParRegs; ++r) {
-            bb[r] = par_bucket((uint32_t)(y[r] >> 32), nl);
+            bb[r] = par_bucket(y[r], nl);
             if ((ym >> r) & 1u) {
                 if (bb[r] <= (uint32_t)keep) fm |= 1u << r;
                 else bm |= 1u << r;
@@ -804,10 +823,10 @@ __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_
     for (uint32_t e = threadIdx.x; e < c; e += kParT) lv += PS.log[e] < kDead;
     const uint64_t nfront = C.rd.sum(lv);
     uint64_t nback = 0;
-    for (int q = 0; q <= 32; ++q) nback += PS.bcnt[q];
+    for (int q = 0; q < kParLv; ++q) nback += PS.bcnt[q];
     const uint64_t total = nfront + nback;
     const bool segd = total > kParSegMin;
-    constexpr uint32_t kSegs = 33u * kParChunks;
+    constexpr uint32_t kSegs = (uint32_t)kParLv * kParChunks;
     const uint64_t words = segd ? nfront + 2ull * kSegs : total;
     if (threadIdx.x == 0) {
         const uint64_t o = aadd(&P.ctl->rpool_used, (words + 15) & ~15ull);  // 128-B aligned records
@@ -856,7 +875,7 @@ __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_
         hdr1 = nfront | ((uint64_t)ns << 32);
     } else {
         uint64_t pos = nfront;
-        for (int q = 0; q <= 32; ++q) {  // kParRegs bucket loads in flight per thread
+        for (int q = 0; q < kParLv; ++q) {  // kParRegs bucket loads in flight per thread
             const uint32_t cq = PS.bcnt[q];
             for (uint32_t e0 = 0; e0 < cq; e0 += kParT * kParRegs) {
                 uint64_t x[kParRegs];
@@ -910,7 +929,7 @@ __device__ __forceinline__ void col_add_keys(ParCol& C, const ParBufs& P, const 
             uint32_t nf = 0;
 #pragma unroll
             for (int q = 0; q < kParRegs; ++q)
-                nf += ((vm >> q) & 1u) && par_bucket((uint32_t)(x[q] >> 32), PS.last) <= PS.kf;
+                nf += ((vm >> q) & 1u) && par_bucket(x[q], PS.last) <= PS.kf;
             C.q2[2] += C.rd.sum(nf);
             C.q2[3] += C.rd.sum((uint32_t)__builtin_popcount(vm)) ;
         }
@@ -1011,7 +1030,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
     static_assert(!WIDE || (DIM == 2 && !PACKED), "wide keys: unpacked H2 rows only");
     ParCol C;
     const int tid = threadIdx.x;
-    for (uint32_t e = tid; e < 33u * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
+    for (uint32_t e = tid; e < (uint32_t)kParLv * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
     if (tid == 0) {
         PS.err = 0;
         PS.wide = WIDE ? 1u : 0u;
@@ -1086,7 +1105,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         // ---------------- working column: reset (chunks stay), then the coboundary or the record
         if (!prealloc) {  // chunks 0..3 of every bucket (bucket_append opens chunk c + 2 from chunk c)
             if (tid == 0) {
-                constexpr uint64_t per = 33ull * chunk_start(4);
+                constexpr uint64_t per = (uint64_t)kParLv * chunk_start(4);
                 const uint64_t o = aadd(&P.ctl->bpool_used, per);
                 PS.bc[5] = o + per <= P.bpool_cap ? o : kEmpty64;
             }
@@ -1099,19 +1118,19 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 }
                 break;
             }
-            for (uint32_t e = tid; e < 33u * 4u; e += kParT)
+            for (uint32_t e = tid; e < (uint32_t)kParLv * 4u; e += kParT)
                 PS.cptr[e / 4][e % 4] = (uint32_t)((o + (e / 4) * chunk_start(4) + chunk_start(e % 4)) >> 8);
             prealloc = true;
         }
-        for (uint32_t q = tid; q < 33; q += kParT) PS.bcnt[q] = 0;
+        for (uint32_t q = tid; q < kParLv; q += kParT) PS.bcnt[q] = 0;
         uint32_t sc = 0;  // WIDE: the column's edge code
         if constexpr (WIDE) {
             const uint32_t* Dc = (const uint32_t*)Dr;
             sc = max(ld_glb(Dc, (size_t)sv[0] * n + sv[1]), max(ld_glb(Dc, (size_t)sv[0] * n + sv[2]), ld_glb(Dc, (size_t)sv[1] * n + sv[2])));
         }
         if (tid == 0) {
-            PS.kf = 32;
-            PS.last = WIDE ? (uint32_t)(((uint64_t)sc << kWideIdxBits) >> 32) : __float_as_uint(sdm + 0.0f);
+            PS.kf = kParLv - 1;
+            PS.last = WIDE ? (uint64_t)sc << kWideIdxBits : (uint64_t)__float_as_uint(sdm + 0.0f) << 32;
         }
         front_reset();
         if (!rec0) {
@@ -1127,7 +1146,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             else
                 col_cob2<PACKED, WIDE>(C, P, Dr, n, r, sv[0], sv[1], sv[2], WIDE ? __uint_as_float(sc) : sdm, z);
         } else {
-            if (tid == 0) PS.last = (uint32_t)(ald(P.rec + (rec0 - 1) * 4 + 2) >> 32);
+            if (tid == 0) PS.last = ald(P.rec + (rec0 - 1) * 4 + 2);  // the record's pivot: its smallest key
             __syncthreads();
             col_add_record(C, P, rec0 - 1);
         }
@@ -1328,7 +1347,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #endif
         if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)adds);
         if (done && my_rec >= 0 && my_seg) {  // the claimed record references this workgroup's chunks: fresh ones next
-            for (uint32_t e = tid; e < 33u * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
+            for (uint32_t e = tid; e < (uint32_t)kParLv * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
             prealloc = false;
             __syncthreads();
         }

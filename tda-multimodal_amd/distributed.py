@@ -176,13 +176,14 @@ class PipelinedSweep:
             res = self.q.get()
             if res is None:
                 return
+            if self.err is not None:  # after a failure: keep draining, so step() / close() never block on a full queue
+                continue
             try:
                 packed, cap = pack_results(res, self.ids, self.maxdim)
                 out = gather_packed(packed, cap, self.total, self.dist, self.device)
                 self.last = out if out is not None else (None, None)
-            except BaseException as e:  # re-raised by close()
+            except BaseException as e:  # re-raised by the next step() or close()
                 self.err = e
-                return
 
     def step(self):
         if self.err is not None:

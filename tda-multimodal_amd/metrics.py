@@ -1,5 +1,9 @@
-"""Layer metrics of the reference's metrics.py computed on the GPU distance
-matrices of the hot path.
+"""Layer metrics of the reference's metrics.py on the GPU.
+
+``compute_effective_dimensionality`` mirrors metrics.py:5-44 (normalised
+participation ratio of the singular values) through the C entry
+``tda_effective_dim``: f64 Gram matrix on the FP64 matrix cores, Jacobi
+eigenvalues on the GPU (csrc/ed_kernels.h).
 
 ``compute_intrinsic_dimensionality`` mirrors the reference's TorchScript
 function of the same name (metrics.py:113-208: TwoNN with regression and
@@ -10,9 +14,55 @@ all batch items at once.  There is no CPU fallback.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
+from . import _lib
 from .ripser import _is_torch, ripser_batch
+
+
+def compute_effective_dimensionality(activations_batch):
+    """Normalised effective dimensionality (sum S)^2 / sum S^2 / min(n, d) of
+    every (n_samples, embed_dim) item of ``activations_batch`` (batch, n, d),
+    S = its singular values (metrics.py:5-44; the input is taken as float32,
+    metrics.py:25).  Returns (batch,) float32: a torch tensor on the input's
+    device for torch input, else a numpy array."""
+    is_t = _is_torch(activations_batch)
+    stream, on_dev, device = None, 0, 0
+    x = activations_batch
+    if is_t:
+        import torch
+
+        dev = x.device
+        x = x.detach().to(torch.float32).contiguous()  # metrics.py:25
+        if x.is_cuda:
+            on_dev = 1
+            device = x.device.index if x.device.index is not None else torch.cuda.current_device()
+            raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+            stream = raw(device) if raw else torch.cuda.current_stream(x.device).cuda_stream
+        else:
+            x = x.numpy()
+    if not on_dev:
+        x = np.ascontiguousarray(np.asarray(x), dtype=np.float32)
+        if x.ndim == 3 and not np.all(np.isfinite(x)):
+            raise ValueError("Input contains NaN or infinity")
+    if x.ndim != 3:
+        raise ValueError("activations_batch must be (batch_size, n_samples, embed_dim)")
+    ptr = x.data_ptr() if on_dev else x.ctypes.data
+    B, n, d = (int(v) for v in x.shape)
+    out = np.zeros(B, np.float32)
+    if B:
+        a = _lib.EdArgs()
+        a.x, a.dtype, a.x_on_device = ptr, _lib.TDA_F32, on_dev
+        a.B, a.N, a.D = B, n, d
+        a.device, a.stream = int(device), stream
+        _lib.check(_lib.lib().tda_effective_dim(ctypes.byref(a), out.ctypes.data_as(_lib._f32p)))
+    if is_t:
+        import torch
+
+        return torch.from_numpy(out).to(dev)
+    return out
 
 
 def compute_intrinsic_dimensionality(data, discard_fraction: float = 0.1, eps: float = 1e-10):

@@ -28,7 +28,7 @@ class _Batch:
     """Host copies of one batched call's outputs; LayerResults are views into it."""
 
     __slots__ = ("L", "nd", "N", "pairs", "cnt", "off", "bidx", "didx", "thr", "ne", "cs", "na", "nc", "nr", "nadd", "dist", "sil",
-                 "tn", "dg")
+                 "tn", "dg", "dist64")
 
 
 class LayerResult(tuple):
@@ -56,10 +56,12 @@ class LayerResult(tuple):
     @property
     def dgms(self) -> list:
         b, l = self
-        d = b.dg[l]
-        if d is None:
-            d = b.dg[l] = self._seg(b.pairs)
-        return d
+        if b.dg is None:  # first access: every layer's views in one pass (L x (maxdim+1) slices)
+            P, nd = b.pairs, b.nd
+            o = b.off.ravel()
+            v = [P[x:y] for x, y in zip(o.tolist(), (o + b.cnt.ravel()).tolist())]
+            b.dg = [v[q:q + nd] for q in range(0, len(v), nd)]
+        return b.dg[l]
 
     @property
     def birth_idx(self):
@@ -116,6 +118,12 @@ class LayerResult(tuple):
         b = self[0]
         return None if b.dist is None else b.dist[self[1]]
 
+    @property
+    def dist64(self):
+        """float64 distance matrix (float64 point clouds with want_dist64), else None."""
+        b = self[0]
+        return None if b.dist64 is None else b.dist64[self[1]]
+
 
 def _arr(ptr, n, dtype):
     """Copy n elements of a library-owned C array (one memcpy, no per-element work)."""
@@ -151,8 +159,9 @@ def _unpack(res_p, want_dist: bool, n_sets: int = 0) -> tuple[list, dict]:
     pairs[:, 0] = bd[:total]
     pairs[:, 1] = bd[total:]
     b.pairs = pairs
-    b.dg = [None] * L
+    b.dg = None
     b.dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N) if want_dist and bool(r.dist) else None
+    b.dist64 = _arr(r.dist64, L * N * N, np.float64).reshape(L, N, N) if want_dist and bool(r.dist64) else None
     b.tn = _arr(r.twonn, L, np.float32) if bool(r.twonn) else None
     b.sil = _arr(r.silhouette, L * n_sets, np.float64).reshape(L, n_sets) if bool(r.silhouette) else None
     out = list(map(LayerResult, zip(repeat(b, L), range(L))))
@@ -211,7 +220,8 @@ def encode_labels(label_sets, n: int) -> np.ndarray:
 
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
                  want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None,
-                 stage_serial: bool = False, twonn: bool = False, discard_fraction: float = 0.1, eps: float = 1e-10):
+                 stage_serial: bool = False, twonn: bool = False, discard_fraction: float = 0.1, eps: float = 1e-10,
+                 want_dist64: bool = False):
     """Persistence of L layers in one call.
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
@@ -227,6 +237,8 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     twonn: also estimate each layer's TwoNN intrinsic dimension on the same
     distance matrix (metrics.py:113-208, ``discard_fraction`` / ``eps`` as
     there); read it from ``LayerResult.twonn``.
+    want_dist64: float64 point clouds also return the float64 distance matrix
+    (``LayerResult.dist64``: sqrt in f64, what sklearn returns for f64 points).
     """
     _check_common(maxdim, 2, False, None, "euclidean")
     a = _lib.RipsArgs()
@@ -271,6 +283,10 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     a.device = int(device)
     a.want_dist = 1 if want_dist else 0
     a.flags = (_lib.TDA_FLAG_STAGE_TIMES | (_lib.TDA_FLAG_STAGE_SERIAL if stage_serial else 0)) if stage_times else 0
+    if want_dist64:  # f64 points: the f64 distance matrix too (ripser.py's dperm2all)
+        a.flags |= _lib.TDA_FLAG_DIST64
+        a.want_dist = 1
+        want_dist = True
     lab = None
     if labels is not None:
         lab = encode_labels(labels, N)
@@ -290,7 +306,9 @@ def ripser(X, maxdim: int = 1, thresh: float = np.inf, coeff: int = 2, distance_
 
     Returns the same dict as ripser.py: ``dgms`` (list of (n_k, 2) float64
     arrays, f32 values widened, ``inf`` for essential classes), ``cocycles``
-    (empty lists), ``num_edges``, ``dperm2all`` (N x N float32 distances),
+    (empty lists), ``num_edges``, ``dperm2all`` (the N x N distance matrix:
+    float32 for float32 points, float64 for float64 points as sklearn's
+    pairwise_distances returns it; the given matrix for distance_matrix=True),
     ``idx_perm`` (arange N) and ``r_cover`` (0.0).
     """
     _check_common(maxdim, coeff, do_cocycles, n_perm, metric)
@@ -306,13 +324,15 @@ def ripser(X, maxdim: int = 1, thresh: float = np.inf, coeff: int = 2, distance_
             raise NotImplementedError("non-zero diagonal (lower-star filtration) is not implemented")
     elif X.shape[1] > X.shape[0]:
         warnings.warn("The input point cloud has more columns than rows; did you mean to transpose?")
-    res = ripser_batch(X[None], maxdim=maxdim, thresh=thresh, distance_matrix=distance_matrix, want_dist=True)[0]
+    f64 = X.dtype == np.float64 and not distance_matrix
+    res = ripser_batch(X[None], maxdim=maxdim, thresh=thresh, distance_matrix=distance_matrix, want_dist=True,
+                       want_dist64=f64)[0]
     N = X.shape[0]
     return {
         "dgms": res.dgms,
         "cocycles": [[] for _ in range(maxdim + 1)],
         "num_edges": res.num_edges,
-        "dperm2all": res.dist,
+        "dperm2all": X if distance_matrix else (res.dist64 if f64 else res.dist),
         "idx_perm": np.arange(N),
         "r_cover": 0.0,
     }

@@ -122,3 +122,46 @@ def test_two_rank_pipelined_steps_match_reference(summary_stats):
     exchange (returned by close()) equals the reference's summary records."""
     recs, steps = _run("pipelined")["pipelined"]
     assert steps == 3 and recs == summary_stats
+
+
+def test_pipelined_sweep_worker_error_does_not_deadlock():
+    """an exchange that fails must not leave step()/close()
+    blocked on the bounded queue -- the worker keeps draining and the error
+    surfaces at the next step() or at close() (world 1, no collective)."""
+    import importlib
+    import sys
+    import threading
+
+    import pytest
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    pkg = importlib.import_module("tda-multimodal_amd")
+    calls = {"n": 0}
+
+    def bad_run(X, maxdim):  # step 1 returns records pack_results cannot read
+        calls["n"] += 1
+        return [object()] * len(X) if calls["n"] == 1 else _oracle_run(X, maxdim)
+
+    X = np.stack([_circle(12), _circle(12) * 2.0])
+    done = {}
+
+    def body():
+        pipe = pkg.distributed.PipelinedSweep(X, 1, 0, 1, run=bad_run, depth=1)
+        raised = False
+        try:
+            for _ in range(3):
+                pipe.step()
+        except Exception:
+            raised = True
+        try:
+            pipe.close()
+        except Exception:
+            raised = True
+        done["raised"] = raised
+
+    t = threading.Thread(target=body, daemon=True)
+    t.start()
+    t.join(60)
+    assert not t.is_alive(), "PipelinedSweep deadlocked after a worker error"
+    assert done.get("raised"), "the worker's error was swallowed"

@@ -346,6 +346,21 @@ def test_full_workload_vs_committed_oracle(gpu, name):
         assert_same_golden(res[l], z, name, l, md)
 
 
+@pytest.mark.parametrize("n,thresh", [(144, np.inf), (300, np.inf), (300, 0.9), (65, np.inf), (700, np.inf)])
+def test_boruvka_h0_vs_oracle(gpu, oracle, monkeypatch, n, thresh):
+    """H0 on the multi-kernel Borůvka path (every N > 190; forced at N = 144
+    with TDA_H0_WAVE=0): the unique spanning forest of the total order, so the
+    H0 pairs, their indices and checksums equal the oracle's Kruskal; a finite
+    threshold leaves a forest of several trees (several infinite bars)."""
+    monkeypatch.setenv("TDA_H0_WAVE", "0")
+    X = np.random.default_rng(n).normal(size=(3, n, 3)).astype(np.float32)
+    if n == 144:
+        X = gpu.synthetic.sweep144(3)
+    res = gpu.ripser_batch(X, maxdim=0, thresh=thresh)
+    for l in range(X.shape[0]):
+        assert_same(res[l], oracle.rips(X[l], maxdim=0, thresh=thresh), 0, f"n={n} layer {l}")
+
+
 @pytest.mark.parametrize("case", ["grid144", "torus256", "adv324"])
 def test_parallel_h2_reduction_vs_oracle(gpu, oracle, monkeypatch, case):
     """H1 and H2 both on k_reduce_par (every residual column in flight, owner
@@ -370,8 +385,12 @@ def test_h2_above_568_vs_committed_oracle(gpu, monkeypatch, name, par2):
     """H0-H2 where tetrahedron indices exceed 32 bits (C(N,4) >= 2^32 above
     N = 568): the radix-heap H2 reduction on wide edge-code keys against the
     committed oracle runs (make_golden_large.py --h2-only); torus1024 is C4's
-    cloud at maxdim 2 (S^1 x S^1: one dominant H2 class)."""
-    monkeypatch.setenv("TDA_PAR2", par2)  # 0: H2 on the serial radix heap (wide keys above N = 568)
+    cloud at maxdim 2 (S^1 x S^1: one dominant H2 class).  par2 = 1 runs
+    TDA_PAR_STRICT=1: the parallel H2 reduction itself must succeed (no
+    silent serial re-run); 0: H2 on the serial radix heap."""
+    monkeypatch.setenv("TDA_PAR2", par2)
+    if par2 == "1":
+        monkeypatch.setenv("TDA_PAR_STRICT", "1")
     z = np.load(os.path.join(GOLDEN, "large_h2.npz"))
     X = z[f"{name}__X"]
     res = gpu.ripser_batch(X, maxdim=2)
@@ -468,6 +487,66 @@ def test_twonn_vs_reference_goldens_and_oracle(gpu):
             assert abs(got[b] - w) <= TWONN_TOL * abs(w), (name, b, float(got[b]), w)
             o = twonn.twonn_from_dist(res[b].dist, disc, eps)
             assert abs(res[b].twonn - o) <= 1e-5 * abs(o), (name, b)
+
+
+def test_f64_points_vs_sklearn_f64_goldens(gpu):
+    """SURVEY a2' (float64 points), pinned to sklearn: the GPU's float64
+    distances (LayerResult.dist64, ripser()'s dperm2all) within 1e-12
+    relative of sklearn's float64 pairwise_distances (tests/golden/
+    dist_f64.npz) -- the summation order differs from BLAS -- and the float32
+    distances the reduction uses equal sklearn's rounded to f32 on >= 99 % of
+    the pairs (all where the f64 values agree to the f32 rounding boundary),
+    within 1e-5 everywhere; D = 3 (scalar kernel), 64 and 4096 (FP64 MFMA)."""
+    from golden.make_golden_f64 import f64_inputs, sha
+
+    z = np.load(os.path.join(GOLDEN, "dist_f64.npz"))
+    for name, X in f64_inputs().items():
+        assert str(z[name + "__sha"]) == sha(X), name
+        want = z[name + "__condensed"]
+        iu = np.triu_indices(X.shape[0], 1)
+        r = gpu.ripser_batch(X[None], maxdim=1, want_dist64=True)[0]
+        assert r.dist64.dtype == np.float64 and r.dist.dtype == np.float32
+        g64 = r.dist64[iu]
+        assert np.all(np.abs(g64 - want) <= 1e-12 * want), name
+        assert np.all(np.diagonal(r.dist64) == 0.0) and np.array_equal(r.dist64, r.dist64.T)
+        g32 = r.dist[iu]
+        assert np.array_equal(g32, g64.astype(np.float32)), name  # the f32 values are the f64 ones rounded
+        assert np.mean(g32 == want.astype(np.float32)) >= 0.99, name
+        assert np.all(np.abs(g32 - want) <= 1e-5 * want), name
+        d = gpu.ripser(X, maxdim=1)
+        assert d["dperm2all"].dtype == np.float64 and np.array_equal(d["dperm2all"], r.dist64)
+        assert all(np.array_equal(a, b) for a, b in zip(d["dgms"], r.dgms))
+
+
+ED_TOL = 1e-5  # relative (north_star's value tolerance): f64 Gram + Jacobi vs the reference's f32 svdvals
+
+
+def test_effective_dimensionality_vs_reference_goldens_and_oracle(gpu):
+    """Normalised effective dimensionality (metrics.py:5-44) on the GPU (f64
+    Gram on the FP64 matrix cores or the scalar Gram kernels, parallel Jacobi)
+    within ED_TOL of the reference's own outputs (tests/golden/ed.json) and of
+    the LAPACK restatement (oracle/ed.py); torch CUDA input comes back on the device."""
+    import torch
+
+    from golden.make_golden_ed import ed_inputs, sha
+
+    from oracle import ed
+
+    with open(os.path.join(GOLDEN, "ed.json")) as f:
+        g = json.load(f)
+    for name, X in ed_inputs().items():
+        assert g[name]["sha"] == sha(X), name
+        want = np.array(g[name]["ed"])
+        got = gpu.compute_effective_dimensionality(X)
+        assert got.dtype == np.float32 and got.shape == (X.shape[0],)
+        o = ed.effective_dimensionality(X)
+        for b in range(X.shape[0]):
+            tol = ED_TOL * abs(want[b]) + (1e-12 if want[b] == 0 else 0.0)
+            assert abs(got[b] - want[b]) <= tol, (name, b, float(got[b]), want[b])
+            assert abs(got[b] - o[b]) <= ED_TOL * abs(o[b]) + (1e-12 if o[b] == 0 else 0.0), (name, b)
+        gt = gpu.compute_effective_dimensionality(torch.from_numpy(X).to("cuda:0"))
+        assert gt.device.type == "cuda" and gt.dtype == torch.float32
+        assert np.array_equal(gt.cpu().numpy(), got), name
 
 
 @pytest.mark.parametrize("n,maxdim", [(180, 1), (324, 2)])

@@ -192,3 +192,36 @@ def test_twonn_restatement_matches_reference_goldens(oracle):
                 assert np.isnan(got), (name, b)
             else:
                 assert abs(got - want) <= TWONN_TOL * abs(want), (name, b, got, want)
+
+
+ED_TOL = 1e-6  # LAPACK f64 SVD of the f32 input vs the reference's f32 torch.linalg.svdvals
+
+
+def test_effective_dimensionality_restatement_matches_reference_goldens():
+    """oracle/ed.py (restatement of metrics.py:5-44) against the reference's own
+    outputs (tests/golden/ed.json, made by importing /root/reference/metrics.py)."""
+    from golden.make_golden_ed import ed_inputs, sha
+
+    from oracle import ed
+
+    with open(os.path.join(GOLDEN, "ed.json")) as f:
+        g = json.load(f)
+    for name, X in ed_inputs().items():
+        assert g[name]["sha"] == sha(X), name
+        got = ed.effective_dimensionality(X)
+        want = np.array(g[name]["ed"])
+        assert np.all(np.abs(got - want) <= ED_TOL * np.maximum(np.abs(want), 1e-30) + (want == 0) * 1e-12), name
+
+
+def test_oracle_f64_distances_match_sklearn_f64_goldens(oracle):
+    """SURVEY a2' (float64 points): the oracle's distances equal sklearn's
+    float64 pairwise_distances (tests/golden/dist_f64.npz) rounded to f32 --
+    the values ripser.py reduces -- bit for bit, at D = 3, 64 and 4096."""
+    from golden.make_golden_f64 import f64_inputs, sha
+
+    z = np.load(os.path.join(GOLDEN, "dist_f64.npz"))
+    for name, X in f64_inputs().items():
+        assert str(z[name + "__sha"]) == sha(X), name
+        iu = np.triu_indices(X.shape[0], 1)
+        got = oracle.distances(X)[iu]
+        assert np.array_equal(got, z[name + "__condensed"].astype(np.float32)), name
