@@ -30,6 +30,8 @@ import subprocess
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -42,6 +44,9 @@ WORKLOADS = {
     "sweep48": (32, 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2", 50, 5),
     "grid144": (32, 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2", 10, 2),
     "torus1024": (1, 1, "S1xS1 torus N=1024 (configs[3]), D=3, H0-H1", 5, 2),
+    # configs[3]'s cloud as a sweep: 32 tori (seeds 0..31) per call, like the reference's 32-layer loop --
+    # the GPU's layers in flight against the CPU baseline's layers in flight (one per worker process)
+    "torus1024x32": (32, 1, "32 S1xS1 tori N=1024 (configs[3]'s cloud, seeds 0-31) per call, D=3, H0-H1", 3, 1),
     # four sweeps per call (128 layers): the same per-layer work, a larger batch -- the
     # latency-bound 32-layer step leaves most CUs idle (throughput capacity, not the headline)
     "sweep48x4": (128, 2, "4 x the qwen-vl 32-layer sweep x 48 points in one call (128 layers), D=3, H0-H2", 50, 5),
@@ -61,9 +66,10 @@ DATA = {
     "sweep48x4": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
     "grid144": "synthetic: 12x12 grid on the torus + N(0, 0.02^2) + random rotation per layer",
     "torus1024": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 0",
+    "torus1024x32": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seeds 0-31",
     "raw4096": "synthetic: activation-like f32 clouds (heavy-tailed feature scales, offsets, outlier features)",
 }
-NPOINTS = {"sweep48": 48, "sweep48x4": 48, "sweep48_host": 48, "sweep48_L4": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
+NPOINTS = {"torus1024x32": 1024, "sweep48": 48, "sweep48x4": 48, "sweep48_host": 48, "sweep48_L4": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
 CALL_KW = {"raw4096": {"twonn": True}}
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
 CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
@@ -83,6 +89,8 @@ def make_workload(name: str, layers: int | None = None):
         return syn.sweep144(L)
     if name == "torus1024":
         return syn.torus(1024)[None].repeat(L, 0)
+    if name == "torus1024x32":
+        return np.stack([syn.torus(1024, seed=s) for s in range(L)])
     if name == "raw4096":
         return syn.activations(L, 144, 4096)
     raise ValueError(name)
@@ -257,7 +265,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
-    ap.add_argument("--extra", default="sweep48_host,sweep48_L4,grid144,torus1024,raw4096,umap36,sweep48x4",
+    ap.add_argument("--extra", default="sweep48_host,sweep48_L4,grid144,torus1024,torus1024x32,raw4096,umap36,sweep48x4",
                     help="secondary workloads measured at N=1 (comma list, '' for none)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")

@@ -325,12 +325,18 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
             // bucket chunks: every workgroup keeps its peak bucket sizes (torus N=1024 needs ~2^26 keys
             // in all, N=2048 ~2^28); records: raw copies of the paired columns.  HBM is 288 GB.
             auto clampp = [](uint64_t x, int lo, int hi) { return std::min<uint64_t>(std::max<uint64_t>(next_pow2(x), 1ull << lo), 1ull << hi); };
-            // + chunks 0..3 of the 33 buckets of every k_reduce_par workgroup
-            // above N = 1024 start at 4x (torus N=2048 overflows 2x: measured r02, 3 attempts per call)
+            // + chunks 0..3 of the kParLv buckets of every k_reduce_par workgroup
+            // above N = 1024 start at 4x (torus N=2048 overflows 2x: measured r02, 3 attempts per call).
+            // Per layer in the batch: every layer's long columns hold their bucket chunks at the same
+            // time, and zero-copy records keep theirs (r03: 32 torus1024 layers per call overflowed a
+            // per-call pool and fell back to the serial reducer)
             const int big4 = N > 1024 ? 2 : 0;
-            p.bpool_cap = (clampp(N * N * 128, 24, 30) << (scale + big4)) + (uint64_t)kParGrid * kParLv * 3840;
+            // (at most 2^33 keys = 64 GiB of the 288 GiB; torus1024 x 32 layers draws ~2.5 G keys)
+            p.bpool_cap = std::min<uint64_t>(clampp(N * N * 128 * L, 24, 32) << (scale + big4), 1ull << 33) +
+                          (uint64_t)kParGrid * kParLv * 3840;
             // H2 records as well: grid144 (32 layers) stores ~4.4 M keys of reduced H2 columns
-            p.rpool_cap = clampp(std::max<uint64_t>(N * N * 64, p.par2 ? L * N * N * 8 : 0), 22, 29) << (scale + big4);
+            p.rpool_cap = clampp(std::max<uint64_t>(N * N * 64 * std::min<uint64_t>(L, 8), p.par2 ? L * N * N * 8 : 0), 22, 29)
+                          << (scale + big4);
             p.rq_cap = 1ull << 16;
             p.o_pctl = take(sizeof(ParCtl));
             p.o_pitem = take((L + 1) * 8);
@@ -518,7 +524,15 @@ int ws_prepare(Workspace& w, const Plan& p) {
         if (w.dbuf) HIPC(hipFree(w.dbuf));
         w.dbuf = nullptr;
         size_t cap = std::max<size_t>(p.total, w.dcap + w.dcap / 2);
-        HIPC(hipMalloc(&w.dbuf, cap));
+        if (hipMalloc(&w.dbuf, cap) != hipSuccess) {
+            (void)hipGetLastError();
+            size_t fr = 0, tot = 0;
+            (void)hipMemGetInfo(&fr, &tot);
+            w.dbuf = nullptr;
+            w.dcap = 0;
+            return fail(TDA_E_HIP, "device workspace of " + std::to_string(cap >> 20) + " MiB does not fit (free " +
+                                       std::to_string(fr >> 20) + " of " + std::to_string(tot >> 20) + " MiB)");
+        }
         w.dcap = cap;
     }
     if (w.hstats_cap < (size_t)p.L) {
@@ -560,7 +574,8 @@ int grow_hout(Workspace& w, size_t need) {
 bool g_attr_done[64] = {false};
 int set_lds_attrs(int dev) {
     if (dev < 64 && g_attr_done[dev]) return 0;
-    HIPC(hipFuncSetAttribute((const void*)k_h0<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_h0<0, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    HIPC(hipFuncSetAttribute((const void*)k_h0<kH0BorWQ, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_h0<kH0WaveQ, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_bor_hook, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
     HIPC(hipFuncSetAttribute((const void*)k_sort_resid, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -900,9 +915,15 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 }
                 HIPC(hipGetLastError());
                 if (int rc = tm4.mark("k_bor_rounds")) return rc;
-                hipLaunchKernelGGL((k_h0<0, false>), dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst),
-                                   p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch),
-                                   (const BorCtl*)bctl);
+                // elder rule: one wave with register labels up to N = 64 * kH0BorWQ, thread 0 above
+                if (n <= 64 * kH0BorWQ)
+                    hipLaunchKernelGGL((k_h0<kH0BorWQ, false, true>), dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats,
+                                       (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s),
+                                       ilog2(ch), (const BorCtl*)bctl);
+                else
+                    hipLaunchKernelGGL((k_h0<0, false, true>), dim3(L), dim3(T), lds, s4, dist, n, a.thresh, stats, (uint32_t*)(B + p.o_mst),
+                                       p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0], (uint64_t*)(B + p.o_h0s), ilog2(ch),
+                                       (const BorCtl*)bctl);
             }
         }
         HIPC(hipGetLastError());

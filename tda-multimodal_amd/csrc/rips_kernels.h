@@ -685,14 +685,18 @@ __global__ __launch_bounds__(1024) void k_bor_hook(int n, int32_t* __restrict__ 
 
 constexpr int kH0WaveMaxN = 190;  // 4 n^2 B of LDS staging
 constexpr int kH0WaveQ = (kH0WaveMaxN + 63) / 64;
-template <int WQ, bool LROWS>
+constexpr int kH0BorWQ = 16;  // Borůvka path: one-wave elder rule with register labels up to N = 1024
+template <int WQ, bool LROWS, bool BOR = false>
 __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int n, float user_thresh,
                                              LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
                                              uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0,
                                              uint64_t* __restrict__ scratch /* [L][2n] */, int sort_log2,
                                              const BorCtl* __restrict__ bctl = nullptr) {
     constexpr bool dlds = LROWS;   // the layer's matrix is staged in LDS
-    constexpr bool wave = WQ > 0;  // one-wave Prim + elder rule
+    // BOR: the forest, threshold and num_edges come from k_bor_* (N > kH0WaveMaxN); WQ > 0
+    // then sizes the one-wave elder rule's register labels (N <= 64 WQ), else thread 0 runs it
+    constexpr bool wave = WQ > 0 && !BOR;  // one-wave Prim (+ threshold / num_edges here)
+    constexpr bool welder = WQ > 0;        // one-wave elder rule
     constexpr int QA = WQ > 0 ? WQ : 1;  // register-array extent (unused when !wave)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.x, T = blockDim.x, t = threadIdx.x;
@@ -813,7 +817,7 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         uint64_t eidx = 0xFFFFFFFFull - (mst[e] & 0xFFFFFFFFull);
         atomicOr(&mst_bits[(size_t)l * mst_words + (eidx >> 5)], 1u << (eidx & 31));
     }
-    if constexpr (wave) {  // elder rule on wave 0: lane l holds the component labels (= max vertex) of vertices l, l + 64, ...
+    if constexpr (welder) {  // elder rule on wave 0: lane l holds the component labels (= max vertex) of vertices l, l + 64, ...
         if (w == 0) {
             int label[QA];
 #pragma unroll
@@ -902,14 +906,37 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
                 ++cnt;
             }
         }
-        for (int i = 0; i < n; ++i) {
-            int u = i;
-            while (par[u] != u) u = par[u];
-            if (u == i) {
-                if ((uint64_t)cnt < pcap0) P[cnt] = Pair{0.0f, INFINITY, (int64_t)i, -1};
-                ++cnt;
+        red[38] = (uint64_t)cnt;
+        red[39] = cs;
+    }
+    __syncthreads();
+    // one [0, inf) bar per component in vertex order: the roots (a component's root is its
+    // largest vertex: the younger root always hooks under the older), block prefix per chunk
+    {
+        Pair* P = pairs0 + (size_t)l * pcap0;
+        uint64_t base = red[38];
+        for (int v0 = 0; v0 < n; v0 += T) {
+            const int v = v0 + t;
+            const bool root = v < n && par[v] == v;
+            const uint64_t m = __ballot(root);
+            if (ln == 0) red[w] = (uint64_t)__popcll(m);
+            __syncthreads();
+            uint64_t before = 0, tot = 0;
+            for (int q = 0; q < nw; ++q) {
+                before += q < w ? red[q] : 0;
+                tot += red[q];
             }
+            const uint64_t pos = base + before + lanes_below(m);
+            if (root && pos < pcap0) P[pos] = Pair{0.0f, INFINITY, (int64_t)v, -1};
+            base += tot;
+            __syncthreads();
         }
+        if (t == 0) red[38] = base;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint64_t cnt = red[38];
+        const uint64_t cs = red[39];
         if ((uint64_t)cnt > pcap0) {
             st->err |= ERR_PAIR_CAP;
             cnt = (int64_t)pcap0;
