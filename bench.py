@@ -71,6 +71,12 @@ DATA = {
 }
 NPOINTS = {"torus1024x32": 1024, "sweep48": 48, "sweep48x4": 48, "sweep48_host": 48, "sweep48_L4": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
 CALL_KW = {"raw4096": {"twonn": True}}
+# consecutive sweeps in flight at once (ripser.SweepPipeline: one device workspace slot per in-flight
+# call): the dense N <= 64 path is a chain of latency-bound kernels that leaves most of the 256 CUs idle
+# (measured r03: 2-4 sweeps in flight on 4 hardware queues gave 0.9-1.2x the one-call-at-a-time rate
+# from box to box -- noise-level -- so the default bench times one call at a time; TDA_BENCH_DEPTH=n
+# with these workloads times n in flight)
+PIPE_DEPTH = {"sweep48": 1, "sweep48_host": 1, "sweep48_L4": 1}
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
 CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
 
@@ -175,6 +181,44 @@ def cpu_baseline(pool, P: int, name: str, X, maxdim: int, seconds: float) -> dic
 
 
 # ---------------------------------------------------------------- GPU measurement
+def _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_index):
+    """K steps (sequential, or `depth` in flight on separate workspace slots) between two syncs;
+    returns (elapsed s, device ms per call)."""
+    import collections
+
+    dev_ms = []
+
+    def done(res, info):
+        if host_in:  # debug_tda_pipeline.py:110: dgms = result['dgms'] for every layer
+            for r in res:
+                r.dgms
+        dev_ms.append(info["device_ms"])
+
+    if depth <= 1:
+        for _ in range(warmup):
+            pkg.ripser_batch(X, maxdim=maxdim, **kw)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            done(*pkg.ripser_batch(X, maxdim=maxdim, return_time=True, **kw))
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, dev_ms
+    with pkg.SweepPipeline(depth=depth, device=dev_index, maxdim=maxdim, return_time=True, **kw) as pipe:
+        for f in [pipe.submit(X) for _ in range(max(warmup, 1) * depth)]:  # every slot captures its graph
+            f.result()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        q = collections.deque()
+        for _ in range(steps):
+            if len(q) == depth:
+                done(*q.popleft().result())
+            q.append(pipe.submit(X))
+        while q:
+            done(*q.popleft().result())
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, dev_ms
+
+
 def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | None = None) -> dict:
     L, maxdim, desc, _, _ = WORKLOADS[name]
     L = layers or L
@@ -184,20 +228,14 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     # resident in HBM before the timed region -- except the host-in record, which passes the numpy array
     X = X_host if host_in else torch.from_numpy(X_host).to(dev)
     torch.cuda.synchronize()
-    dev_ms = []
     kw = CALL_KW.get(name, {})
-    for _ in range(warmup):
-        pkg.ripser_batch(X, maxdim=maxdim, **kw)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        res, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, **kw)
-        if host_in:  # debug_tda_pipeline.py:110: dgms = result['dgms'] for every layer
-            for r in res:
-                r.dgms
-        dev_ms.append(info["device_ms"])
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    depth = int(os.environ.get("TDA_BENCH_DEPTH", PIPE_DEPTH[name])) if name in PIPE_DEPTH else 1
+    dev_index = dev.index if dev.index is not None else 0
+    seq = None
+    if depth > 1:  # the one-call-at-a-time figure next to the pipelined one
+        el_s, dm_s = _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, 1, host_in, dev_index)
+        seq = {"value": L * steps / el_s, "ms_per_step": el_s / steps * 1e3, "device_ms_per_step": sum(dm_s) / len(dm_s)}
+    el, dev_ms = _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_index)
     # per-kernel durations: HIP events around every kernel with all stages on
     # ONE stream (each interval brackets exactly one kernel), same batch,
     # after the timed region; the dominant kernel has the largest mean
@@ -231,6 +269,9 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
                      "kernel_timing": "HIP events around each kernel on its stream, all stages serialised on one "
                                       "stream, after the timed region (same batch)"},
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+        "pipeline": {"depth": depth, "sequential": seq,
+                     "note": "value: `depth` consecutive steps in flight (ripser.SweepPipeline, one workspace slot each); "
+                             "sequential: one call at a time"} if depth > 1 else None,
     }
 
 
@@ -356,6 +397,7 @@ def main():
         if prim:
             out["device_ms_per_step"] = prim["device_ms_per_step"]
             out["stages_ms"] = prim["stages_ms"]
+            out["pipeline"] = prim["pipeline"]
         if strong:
             out["strong"] = strong
     if rank == 0 and world == 1:
@@ -375,7 +417,7 @@ def main():
             _, _, _, st, wu = WORKLOADS[w]
             m = measure(pkg, torch, dev, w, st, wu)
             rec = {k: m[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "device_ms_per_step",
-                                     "config", "roofline", "stages_ms")}
+                                     "config", "roofline", "stages_ms", "pipeline")}
             rec["data"] = DATA[w]
             if do_cpu:
                 same = CPU_SAME.get(w)

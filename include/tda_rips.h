@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TDA_RIPS_ABI_VERSION 4
+#define TDA_RIPS_ABI_VERSION 5
 
 /* error codes */
 #define TDA_OK 0
@@ -82,7 +82,15 @@ typedef struct tda_rips_args {
     float twonn_eps;       /* eps (reference default 1e-10; compared in f32)   */
     double twonn_discard;  /* discard_fraction (reference default 0.1; f64 as
                               in int(len * (1.0 - discard_fraction)))          */
+    /* ABI >= 5: workspace slot 0 .. TDA_MAX_SLOTS-1 on `device`.  Each slot has
+     * its own streams, device buffers, host-mapped outputs and captured
+     * graphs, so calls on different slots (from different host threads) run
+     * concurrently on the GPU -- e.g. consecutive sweeps of a layer loop in
+     * flight at once; calls on one slot are serialised. */
+    int32_t slot;
 } tda_rips_args;
+
+#define TDA_MAX_SLOTS 8
 
 /* per (layer, dim) emitted persistence pairs, in the reference's emission
  * order: H0 = Kruskal order of the finite deaths then one [0, inf) per

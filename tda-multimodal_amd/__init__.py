@@ -13,13 +13,14 @@ from ._lib import EXPORTS, LIB_PATH, build, lib  # noqa: F401
 from .pipeline import (get_max_persistence, get_persistence, layer_record, layer_record_adversarial, peak_layer,  # noqa: F401
                        run_adversarial_condition, run_sweep, write_layer_stats, write_summary_stats)
 from .umap import UMAP, umap_batch, umap_transform_batch  # noqa: F401
-from .ripser import LayerResult, persistence_pairs, ripser, ripser_batch, rips_dm, silhouette_score  # noqa: F401
+from .ripser import LayerResult, SweepPipeline, persistence_pairs, ripser, ripser_batch, rips_dm, silhouette_score  # noqa: F401
 
 _sys.modules.setdefault("tda_multimodal_amd", _sys.modules[__name__])
 
 __all__ = [
     "ripser",
     "ripser_batch",
+    "SweepPipeline",
     "rips_dm",
     "persistence_pairs",
     "LayerResult",

@@ -42,6 +42,7 @@ class RipsArgs(ctypes.Structure):
         ("want_twonn", ctypes.c_int32),
         ("twonn_eps", ctypes.c_float),
         ("twonn_discard", ctypes.c_double),
+        ("slot", ctypes.c_int32),
     ]
 
 
@@ -84,6 +85,7 @@ class RipsResult(ctypes.Structure):
 TDA_FLAG_STAGE_TIMES = 1
 TDA_FLAG_STAGE_SERIAL = 2
 TDA_FLAG_DIST64 = 4
+TDA_MAX_SLOTS = 8
 
 
 class UmapArgs(ctypes.Structure):  # include/tda_umap.h

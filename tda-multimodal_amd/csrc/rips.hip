@@ -391,6 +391,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
 // ------------------------------------------------------------------ workspace
 struct Workspace {
     int device = -1;
+    int slot = 0;
     bool init = false;
     hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evf = nullptr, evj = nullptr, evs = nullptr, evp = nullptr, evh = nullptr, evsil = nullptr;
@@ -486,12 +487,13 @@ struct StageTimer {
 std::mutex g_ws_mu;
 std::vector<Workspace*> g_ws;
 
-Workspace* get_ws(int dev) {
+Workspace* get_ws(int dev, int slot) {
     std::lock_guard<std::mutex> g(g_ws_mu);
     for (auto* w : g_ws)
-        if (w->device == dev) return w;
+        if (w->device == dev && w->slot == slot) return w;
     auto* w = new Workspace();
     w->device = dev;
+    w->slot = slot;
     g_ws.push_back(w);
     return w;
 }
@@ -659,7 +661,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     make_plan(p, force_global, scale, force_big, no_par);
     const int dev = a.device;
     HIPC(hipSetDevice(dev));
-    Workspace& w = *get_ws(dev);
+    Workspace& w = *get_ws(dev, a.slot);
     std::unique_lock<std::mutex> guard(w.mu);  // released before any retry (which re-enters)
     if (int rc = ws_prepare(w, p)) return rc;
     if (int rc = set_lds_attrs(dev)) return rc;
@@ -1607,7 +1609,7 @@ int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_
     // not when a test forces a reducer (the memo would override what it asks for)
     if (!test_env_is("TDA_RETRY_MEMO", "0") && !test_env("TDA_REDUCE") && !test_env("TDA_PAR") && !test_env("TDA_PAR_STRICT") &&
         !test_env("TDA_CHAIN")) {
-        Workspace& w = *get_ws(a.device);
+        Workspace& w = *get_ws(a.device, a.slot);
         std::lock_guard<std::mutex> g(w.mu);
         for (const auto& m : w.retry)
             if (m.N == a.N && m.maxdim == a.maxdim && m.input_kind == input_kind) {
@@ -1630,6 +1632,7 @@ int validate(const tda_rips_args* a) {
     if (a->modulus != 2) return fail(TDA_E_UNSUPPORTED, "only coeff=2 (Z/2) is supported");
     if (a->maxdim < 0 || a->maxdim > 2) return fail(TDA_E_UNSUPPORTED, "maxdim must be 0, 1 or 2");
     if (a->N > 8192) return fail(TDA_E_UNSUPPORTED, "N > 8192 is not supported");
+    if (a->slot < 0 || a->slot >= TDA_MAX_SLOTS) return fail(TDA_E_INVALID, "slot must be in [0, TDA_MAX_SLOTS)");
     // H1 filtration keys pack a 32-bit row-simplex index: C(N, 3) < 2^32.  H2
     // above N = 568 uses edge-code keys (21-bit code + 42-bit index): C(N, 2) < 2^21
     if (a->maxdim == 1 && a->N > 2900) return fail(TDA_E_UNSUPPORTED, "maxdim=1 requires N <= 2900");

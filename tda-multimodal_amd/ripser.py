@@ -221,7 +221,7 @@ def encode_labels(label_sets, n: int) -> np.ndarray:
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
                  want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None,
                  stage_serial: bool = False, twonn: bool = False, discard_fraction: float = 0.1, eps: float = 1e-10,
-                 want_dist64: bool = False):
+                 want_dist64: bool = False, slot: int = 0):
     """Persistence of L layers in one call.
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
@@ -239,6 +239,9 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     there); read it from ``LayerResult.twonn``.
     want_dist64: float64 point clouds also return the float64 distance matrix
     (``LayerResult.dist64``: sqrt in f64, what sklearn returns for f64 points).
+    slot: the device workspace (0 .. 7) the call runs in; calls from different
+    host threads on different slots run concurrently on the GPU (see
+    :class:`SweepPipeline`).
     """
     _check_common(maxdim, 2, False, None, "euclidean")
     a = _lib.RipsArgs()
@@ -281,6 +284,7 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     a.thresh = float(thresh) if np.isfinite(thresh) else float("inf")
     a.modulus = 2
     a.device = int(device)
+    a.slot = int(slot)
     a.want_dist = 1 if want_dist else 0
     a.flags = (_lib.TDA_FLAG_STAGE_TIMES | (_lib.TDA_FLAG_STAGE_SERIAL if stage_serial else 0)) if stage_times else 0
     if want_dist64:  # f64 points: the f64 distance matrix too (ripser.py's dperm2all)
@@ -366,3 +370,38 @@ def silhouette_score(X, labels) -> float:
     if X.ndim != 2:
         raise ValueError("X must be a 2-D array")
     return ripser_batch(X[None], maxdim=0, labels=[labels])[0].silhouette[0]
+
+
+class SweepPipeline:
+    """Consecutive layer-loop batches in flight at once: ``depth`` host threads,
+    each on its own device workspace slot (streams, buffers, graphs), so batch
+    i + 1 runs on the GPU while batch i finishes -- the dense small-N path is a
+    chain of latency-bound kernels that leaves most CUs idle, and two
+    independent sweeps fill them.  ``submit(X)`` returns a future whose
+    ``result()`` is ``ripser_batch(X, **kw)``'s; results come back in
+    submission order when waited on in order.  The ctypes call releases the
+    GIL, so the threads overlap their GPU waits."""
+
+    def __init__(self, depth: int = 2, device: int = 0, **kw):
+        from concurrent.futures import ThreadPoolExecutor
+
+        if not 1 <= depth <= _lib.TDA_MAX_SLOTS:
+            raise ValueError(f"depth must be in [1, {_lib.TDA_MAX_SLOTS}]")
+        self.depth, self.device, self.kw = depth, device, kw
+        self._ex = [ThreadPoolExecutor(max_workers=1) for _ in range(depth)]  # one thread per slot: calls on a slot stay ordered
+        self._n = 0
+
+    def submit(self, X, **kw):
+        s = self._n % self.depth
+        self._n += 1
+        return self._ex[s].submit(ripser_batch, X, device=self.device, slot=s, **dict(self.kw, **kw))
+
+    def close(self):
+        for e in self._ex:
+            e.shutdown(wait=True)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

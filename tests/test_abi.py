@@ -36,7 +36,7 @@ def test_library_is_gfx950_code_object(built_lib):
 
 def test_version_and_no_device_here(pkg, built_lib):
     L = pkg.lib()
-    assert L.tda_version() == 4  # ABI 4: dist64 appended to the result (3: TwoNN, 2: silhouettes)
+    assert L.tda_version() == 5  # ABI 5: workspace slot in the args (4: dist64, 3: TwoNN, 2: silhouettes)
     assert L.tda_device_ok(12345) == 0
 
 
@@ -86,17 +86,17 @@ def test_ctypes_structs_match_header_layout(pkg, tmp_path):
     src = tmp_path / "layout.c"
     src.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "tda_rips.h"\n'
-        'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tda_rips_args), offsetof(tda_rips_args, labels),'
+        'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tda_rips_args), offsetof(tda_rips_args, labels),'
         ' offsetof(tda_rips_args, n_label_sets), sizeof(tda_rips_result), offsetof(tda_rips_result, silhouette),'
         ' offsetof(tda_rips_args, twonn_discard), offsetof(tda_rips_result, twonn), offsetof(tda_rips_result, n_pairs),'
-        ' offsetof(tda_rips_result, dist64));'
+        ' offsetof(tda_rips_result, dist64), offsetof(tda_rips_args, slot));'
         'return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", lb.INCLUDE, str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [ctypes.sizeof(lb.RipsArgs), lb.RipsArgs.labels.offset, lb.RipsArgs.n_label_sets.offset,
             ctypes.sizeof(lb.RipsResult), lb.RipsResult.silhouette.offset, lb.RipsArgs.twonn_discard.offset,
-            lb.RipsResult.twonn.offset, lb.RipsResult.n_pairs.offset, lb.RipsResult.dist64.offset]
+            lb.RipsResult.twonn.offset, lb.RipsResult.n_pairs.offset, lb.RipsResult.dist64.offset, lb.RipsArgs.slot.offset]
     assert got == want
 
 

@@ -593,3 +593,21 @@ def test_adversarial_condition_records(gpu, oracle, n):
                 assert abs(got[k] - want[k]) < 1e-9, (n, l, k)
             else:
                 assert got[k] == want[k], (n, l, k)
+
+
+def test_workspace_slots_run_concurrently_with_identical_results(gpu):
+    """Workspace slots (ABI 5): sweeps submitted through SweepPipeline (one
+    host thread and one device workspace per slot, calls in flight at once)
+    give bit-identical diagrams and checksums to one-at-a-time calls, for the
+    dense N = 48 path and the parallel-reducer N = 144 path."""
+    for X, md in ((gpu.synthetic.sweep48(32), 2), (gpu.synthetic.sweep144(4), 2)):
+        ref = gpu.ripser_batch(X, maxdim=md)
+        with gpu.SweepPipeline(depth=3, maxdim=md) as pipe:
+            futs = [pipe.submit(X) for _ in range(7)]
+            outs = [f.result() for f in futs]
+        for out in outs:
+            for l in range(X.shape[0]):
+                assert out[l].checksum == ref[l].checksum
+                assert all(np.array_equal(a, b) for a, b in zip(out[l].dgms, ref[l].dgms))
+    with pytest.raises(ValueError):
+        gpu.ripser_batch(X, maxdim=1, slot=8)
