@@ -826,10 +826,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             hipLaunchKernelGGL((k_distance_mfma<double, 0, true>), gsplit, dim3(256), 0, s, (const double*)x, n, (int)p.D, dist, rowmax,
                                gpart, npart, (double*)nullptr);
             hipLaunchKernelGGL((k_distance_combine<double, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax, d64);
+            hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
         } else if (mfma && p.dsplit > 1) {
             hipLaunchKernelGGL((k_distance_mfma<float, 0, true>), gsplit, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax,
                                gpart, npart);
             hipLaunchKernelGGL((k_distance_combine<float, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
+            hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
         } else if (mfma && p.dtype == TDA_F64)
             hipLaunchKernelGGL((k_distance_mfma<double>), dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const double*)x, n, (int)p.D,
                                dist, rowmax, (double*)nullptr, (double*)nullptr, d64);
@@ -882,6 +884,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                                (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
         } else {
             int T = n <= 256 ? 256 : 1024;
+            if (n <= kH0WaveMaxN && !test_env_is("TDA_H0_WAVE", "0")) T = 1024;  // LDS Borůvka: a wave per vertex
             // best | par | red | sort chunk | (LDS rows) | Borůvka hooks
             size_t base = 16 + (size_t)n * 8 + (size_t)((n + 1) & ~1) * 4 + 40 * 8 + (size_t)n * 4;
             base = align_up(base, 16);

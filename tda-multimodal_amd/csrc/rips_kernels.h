@@ -362,9 +362,8 @@ __global__ __launch_bounds__(256) void k_distance_combine(const double* __restri
         f = f + 0.0f;
         Dl[q] = f;
         Dl[(size_t)j * n + i] = f;
-        atomicMax(&rm[i], __float_as_uint(f));
-        atomicMax(&rm[j], __float_as_uint(f));
     }
+    (void)rm;  // row maxima: k_rowmax after this kernel (per-element atomics on N row words serialised: r03 89 us)
 }
 
 // row maxima of a square distance matrix (distance-matrix inputs): one wave per row
@@ -762,7 +761,79 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     (void)s_cur;
     (void)best;
     (void)thr;
-    if constexpr (wave) {  // one-wave Prim (rows from LDS, or global memory)
+    if constexpr (wave && LROWS) {
+        // Borůvka on the whole workgroup over the LDS-staged rows (r03; the
+        // one-wave Prim it replaces took N - 1 dependent steps: 32 x N=144
+        // 0.16 ms): every round each vertex's cheapest edge to another
+        // component (one wave per vertex), component minima by LDS
+        // atomicMin, roots hook to the other endpoint's root (unique keys:
+        // only mutual pairs form cycles, the smaller root stays), pointer
+        // jumping.  The unique minimum spanning forest, as k_bor_* and Prim.
+        int* comp = par;                         // n
+        int* hook = (int*)(Ds + (size_t)n * n);  // n (carved by the host after the rows)
+        uint64_t* cheap = best;                  // n
+        int orp = 0;
+        auto block_or = [&](bool p) {  // via red[36 + parity]: no static LDS in this kernel
+            uint64_t* f = red + 36 + (orp++ & 1);
+            if (p) *f = 1;
+            __syncthreads();
+            const bool r = *f != 0;
+            __syncthreads();
+            if (t == 0) *f = 0;
+            return r;
+        };
+        for (int v = t; v < n; v += T) comp[v] = v;
+        if (t == 0) red[35] = red[36] = red[37] = 0;
+        __syncthreads();
+        for (int round = 0; round < 64; ++round) {
+            for (int v = t; v < n; v += T) cheap[v] = kEmpty64;
+            __syncthreads();
+            for (int u = w; u < n; u += nw) {
+                const int cu = comp[u];
+                uint64_t mk = kEmpty64;
+                for (int v = ln; v < n; v += 64) {
+                    const float d = ld_lds(Ds, (size_t)u * n + v);
+                    if (d <= thr && comp[v] != cu) {
+                        const int a = u > v ? u : v, b = u > v ? v : u;
+                        const uint64_t k = filt_key(d, binom((uint64_t)a, 2) + b);
+                        mk = k < mk ? k : mk;
+                    }
+                }
+                mk = wave_min_u64(mk);
+                if (ln == 0 && mk != kEmpty64) atomicMin((unsigned long long*)&cheap[cu], (unsigned long long)mk);
+            }
+            __syncthreads();
+            bool any = false;
+            for (int r = t; r < n; r += T) {
+                hook[r] = r;
+                if (comp[r] != r || cheap[r] == kEmpty64) continue;
+                any = true;
+                const uint64_t eidx = 0xFFFFFFFFull - (cheap[r] & 0xFFFFFFFFull);
+                const int a = max_vertex(eidx, 2, n - 1), b = (int)(eidx - binom((uint64_t)a, 2));
+                const int ca = comp[a], cb = comp[b];
+                const int other = ca == r ? cb : ca;
+                if (cheap[other] == cheap[r] && r < other) continue;  // the smaller root of a mutual pair stays
+                hook[r] = other;
+                mst[atomicAdd((unsigned long long*)&red[35], 1ull)] = cheap[r];
+            }
+            if (!block_or(any)) break;
+            for (int it = 0; it < 32; ++it) {
+                bool ch = false;
+                for (int r = t; r < n; r += T) {
+                    const int h = hook[r], hh = hook[h];
+                    if (h != hh) {
+                        hook[r] = hh;
+                        ch = true;
+                    }
+                }
+                if (!block_or(ch)) break;
+            }
+            for (int v = t; v < n; v += T) comp[v] = hook[comp[v]];
+            __syncthreads();
+        }
+        nmst = (int)red[35];
+        __syncthreads();
+    } else if constexpr (wave) {  // one-wave Prim on rows from global memory
         if (w == 0) {
             uint64_t bst[QA];
             bool in[QA];
