@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
 // pairs only (bi <= bj, enumerated linearly: no idle lower-triangle blocks).
 // 4 waves, each a 32x32 quadrant as 2x2 MFMA tiles (4 independent f64x4
 // accumulators hide the MFMA latency).  K is staged through LDS in chunks of
-// kDmKC, upcast to f64, row-major with a row stride of kDmS = kDmKC + 2
+// kDmKC in the input type (widened to f64 at the operand read), row-major with a row stride of kDmS = kDmKC + 2
 // doubles: an MFMA operand read (lane -> row lane & 15, k = lane >> 4) maps
 // each half-wave's 32 lanes to 32 distinct 8-byte bank pairs (row r, k:
 // slot 2r + k mod 32), so the ds_read_b64 is conflict-free; each thread
@@ -174,8 +174,13 @@ template <typename T, int METRIC = 0, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, int n, int D, float* __restrict__ dist,
                                                        uint32_t* __restrict__ rowmax, double* __restrict__ gpart = nullptr,
                                                        double* __restrict__ npart = nullptr, double* __restrict__ dist64 = nullptr) {
-    __shared__ double xs[2][kDmT][kDmS];  // [i/j tile][row][k]
+    // K chunks staged in LDS in the INPUT type (r03: f32 for the raw activations, half the LDS
+    // bytes of the f64 staging it replaces -- LDS traffic, not the MFMA pipe, bounded the kernel)
+    // and widened to f64 at the operand read; row stride kDmS = kDmKC + 2 elements keeps the
+    // operand reads conflict-free for 4-byte and 8-byte elements alike
+    __shared__ T xs[2][2][kDmT][kDmS];  // [buffer][i/j tile][row][k]: chunk c + 1 is written while chunk c feeds the MFMAs
     __shared__ double nrm[2][kDmT];
+    __shared__ double nrp[2][2][kDmT];  // norm partials: [k half][tile][row]
     __shared__ uint32_t rmx[2][kDmT];
     const int l = blockIdx.y;
     const int nt = (n + kDmT - 1) / kDmT;
@@ -191,7 +196,11 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = dm_d4{0.0, 0.0, 0.0, 0.0};
-    double nacc = 0.0;  // threads < 128: squared norm of row (tid & 63) of tile (tid >> 6)
+    // squared norms: thread t sums row (t & 63) of tile ((t >> 6) & 1) over k half t >> 7 of every
+    // chunk (all four waves share the work; lane-rotated k order spreads the LDS banks; the order
+    // is fixed per row, so a layer's norms do not depend on the launch)
+    double nacc = 0.0;
+    const int nt_r = tid & 63, nt_t = (tid >> 6) & 1, nt_h = tid >> 7;
     if (tid < 2 * kDmT) rmx[tid >> 6][tid & 63] = 0;
     // register double buffer: chunk k0 + kDmKC is in flight while chunk k0 feeds the MFMAs
     T pre[4][4];
@@ -212,38 +221,45 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
             for (int q = 0; q < 4; ++q) pre[u][q] = (g < n && c0 + q < kc) ? src[q] : (T)0;
         }
     };
-    load(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += kDmKC) {
+    auto stage = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int e = tid + 256 * u, t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) xs[t][r][c0 + q] = (double)pre[u][q];
+            for (int q = 0; q < 4; ++q) xs[buf][t][r][c0 + q] = pre[u][q];
         }
-        __syncthreads();
-        if (k0 + kDmKC < kend) load(k0 + kDmKC);
-        if (tid < 2 * kDmT)  // zero padding adds exact zeros
+    };
+    load(kbeg);
+    stage(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += kDmKC, buf ^= 1) {
+        const bool more = k0 + kDmKC < kend;
+        if (more) load(k0 + kDmKC);  // global loads in flight under this chunk's MFMAs
 #pragma unroll 8
-            for (int c = 0; c < kDmKC; ++c) {
-                const double v = xs[tid >> 6][tid & 63][c];
-                nacc = fma(v, v, nacc);
-            }
+        for (int cc = 0; cc < kDmKC / 2; ++cc) {  // zero padding adds exact zeros
+            const double v = (double)xs[buf][nt_t][nt_r][nt_h * (kDmKC / 2) + ((cc + nt_r) & (kDmKC / 2 - 1))];
+            nacc = fma(v, v, nacc);
+        }
 #pragma unroll
         for (int ks = 0; ks < kDmKC; ks += 4) {
             const int k = ks + (lane >> 4);
             double av[2], bv[2];
 #pragma unroll
-            for (int a = 0; a < 2; ++a) av[a] = xs[0][wr * 32 + a * 16 + (lane & 15)][k];
+            for (int a = 0; a < 2; ++a) av[a] = (double)xs[buf][0][wr * 32 + a * 16 + (lane & 15)][k];
 #pragma unroll
-            for (int b = 0; b < 2; ++b) bv[b] = xs[1][wc * 32 + b * 16 + (lane & 15)][k];
+            for (int b = 0; b < 2; ++b) bv[b] = (double)xs[buf][1][wc * 32 + b * 16 + (lane & 15)][k];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
                 for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
+        if (more) stage(buf ^ 1);  // the other buffer: its last readers passed the previous barrier
         __syncthreads();
     }
-    if (tid < 2 * kDmT) nrm[tid >> 6][tid & 63] = nacc;
+    nrp[nt_h][nt_t][nt_r] = nacc;
+    __syncthreads();
+    if (tid < 2 * kDmT) nrm[tid >> 6][tid & 63] = nrp[0][tid >> 6][tid & 63] + nrp[1][tid >> 6][tid & 63];
     __syncthreads();
     if constexpr (SPLIT) {
         const size_t zo = ((size_t)l * gridDim.z + blockIdx.z);
