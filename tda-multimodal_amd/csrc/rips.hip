@@ -1433,6 +1433,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         fprintf(stderr, "[tda-prof]   record adds: room %llu, col_add %llu cycles, keys front %llu / all %llu; refill pass 3 %llu cycles; %llu saves (%llu keys) %llu cycles\n",
                 (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2], (unsigned long long)v[3], (unsigned long long)v[5],
                 (unsigned long long)v[6], (unsigned long long)v[7], (unsigned long long)v[4]);
+        const uint64_t* y = w.hstats[0].prof[1];
+        fprintf(stderr, "[tda-prof]   refill phases: search %llu, loads+min %llu, histogram %llu, level choice %llu, toggles %llu, appends %llu, compactions %llu cycles; %llu keys kept in front\n",
+                (unsigned long long)y[0], (unsigned long long)y[1], (unsigned long long)y[2], (unsigned long long)y[3],
+                (unsigned long long)y[4], (unsigned long long)y[5], (unsigned long long)y[6], (unsigned long long)y[7]);
     }
     if (p.big && !p.par)
         for (int d = 1; d <= p.maxdim; ++d) {

@@ -167,6 +167,32 @@ struct ParLds {
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
 
+// Level bookkeeping: one wave does what a serial loop over the 65 levels did
+// (r03 profile, torus1024: those LDS loops cost ~7.5 K cycles per refill).
+// Lowest non-empty HBM bucket at level >= from (-1 if none).  Block-uniform:
+// every wave computes it from the same LDS counters (no barrier).
+__device__ __forceinline__ int par_first_bucket(uint32_t from) {
+    const uint32_t ln = threadIdx.x & 63;
+    const uint64_t m = __ballot(ln >= from && PS.bcnt[ln] != 0);
+    if (m) return (int)__builtin_ctzll(m);
+    return (from <= 64u && PS.bcnt[64]) ? 64 : -1;
+}
+
+// Largest level q < lim (lim <= 64) whose cumulative count hist[0..q] is
+// <= fill, or -1.  Counts are non-negative, so the levels that qualify are a
+// prefix: a wave scan and one ballot.  Block-uniform.
+__device__ __forceinline__ int par_keep_level(const uint32_t* hist, int lim, uint32_t fill) {
+    const int ln = threadIdx.x & 63;
+    uint32_t x = ln < lim ? hist[ln] : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (ln >= o) x += y;
+    }
+    const uint64_t m = __ballot(ln < lim && x <= fill);
+    return m ? 63 - (int)__builtin_clzll(m) : -1;
+}
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup
 // release/acquire, which waits for ALL of the wave's outstanding global
 // memory operations (s_waitcnt vmcnt(0)) -- here the previous step's ~1000
@@ -275,7 +301,7 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
     if (!wtot) return;
     uint32_t base = 0;
     if (ln == 0) base = atomicAdd(&PS.fcnt, wtot);
-    base = __shfl(base, 0, 64);
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);  // lane 0 is active: the whole wave runs this
     uint32_t off = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -421,6 +447,7 @@ struct ParCol {
     uint64_t ncompact = 0, nspill = 0;
     uint64_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // keys, front toggle, bucket append, capacity, R adds, R entries, refill keys, load wait
     uint64_t q2[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // record: room, add, front keys, back keys; refill: passes 1-2, pass 3
+    uint64_t q3[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // refill: search, pass 1 (loads + min), pass 2 (histogram), level choice, toggles, appends, compactions, keys kept in front
 #endif
 };
 #ifdef TDA_PROFILE
@@ -451,12 +478,7 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
         const uint64_t last = PS.last;
         for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket(PS.log[e], last)], 1u);
         __syncthreads();
-        int keep = -1;
-        uint32_t cum = 0;
-        for (int q = 0; q <= (int)PS.kf; ++q) {
-            cum += PS.hist[q];
-            if (cum <= kFrontFill) keep = q;
-        }
+        int keep = par_keep_level(PS.hist, (int)min(PS.kf + 1u, 64u), kFrontFill);
         if (keep < 0) {  // the exact-diameter level alone is too large for the front
             if (PS.hist[0] + need <= kFrontLog) keep = 0;
             else if (threadIdx.x == 0) PS.err = 31;
@@ -548,12 +570,14 @@ __device__ __forceinline__ uint32_t bucket_batch(const ParBufs& P, uint32_t b, u
 // in flight per thread.
 __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     __syncthreads();
-    int b = -1;
-    for (int q = (int)PS.kf + 1; q < kParLv; ++q)
-        if (PS.bcnt[q]) {
-            b = q;
-            break;
-        }
+#ifdef TDA_PROFILE
+    uint64_t tq = clock64();
+#define PAR_Q3(i) do { __syncthreads(); const uint64_t tn = clock64(); C.q3[i] += tn - tq; tq = tn; } while (0)
+#else
+#define PAR_Q3(i)
+#endif
+    const int b = par_first_bucket(PS.kf + 1);
+    PAR_Q3(0);
     if (b < 0) return false;
     const uint32_t c = PS.bcnt[b];
     constexpr uint32_t kPass = kParT * kParRegs;
@@ -584,8 +608,12 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
         }
     }
     mn = C.rd.min(mn);  // barrier: the resets above are done too
+    PAR_Q3(1);
     const uint64_t nl = mn;
-    // pass 2: histogram of the new levels (all < b)
+    // pass 2: histogram of the new levels (all < b); the front keeps the lowest
+    // levels that hold at most kFrontFill keys.  (A binary search on the level
+    // with block counts instead of the atomics measured slower: 7.1 vs 4.3 M
+    // cycles over torus1024's refills.)
     if (inreg) {
 #pragma unroll
         for (int h = 0; h < kParRefill; ++h)
@@ -602,14 +630,11 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
         }
     }
     __syncthreads();
-    int keep = -1;
-    uint32_t cum = 0;
-    for (int q = 0; q < b; ++q) {
-        cum += PS.hist[q];
-        if (cum <= kFrontFill) keep = q;
-    }
+    int keep = par_keep_level(PS.hist, b, kFrontFill);
+    const uint32_t cnt0 = PS.hist[0];  // keys equal to nl (level 0)
+    PAR_Q3(2);
     if (keep < 0) {
-        if (PS.hist[0] <= kFrontLive) keep = 0;
+        if (cnt0 <= kFrontLive) keep = 0;
         else {
             if (threadIdx.x == 0) PS.err = 32;
             __syncthreads();
@@ -623,6 +648,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
         PS.kf = (uint32_t)keep;
     }
     __syncthreads();
+    PAR_Q3(3);
 #ifdef TDA_PROFILE
     const uint64_t t3 = clock64();
 #endif
@@ -631,6 +657,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
         // the front takes at most kFrontLive keys in all: compaction keeps room
         __syncthreads();  // chunk pointers opened by the previous pass
         if (PS.fcnt + kParRegs * kParT > kFrontLog) front_compact(C.rd, kParLv);
+        PAR_Q3(6);
         uint32_t fm = 0, bm = 0, bb[kParRegs];
 #pragma unroll
         for (int r = 0; r < kParRegs; ++r) {
@@ -641,7 +668,13 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
             }
         }
         front_toggle<kParRegs>(y, fm);
+        PAR_Q3(4);
+#ifdef TDA_PROFILE
+        C.q3[7] += C.rd.sum((uint32_t)__builtin_popcount(fm));
+        tq = clock64();
+#endif
         bucket_append<kParRegs>(y, bb, bm, P);
+        PAR_Q3(5);
     };
     if (inreg) {
 #pragma unroll
@@ -661,6 +694,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     C.q2[5] += clock64() - t3;
 #endif
     return PS.err == 0;
+#undef PAR_Q3
 }
 
 // toggle the coboundary of edge (a > b), diameter sd, into the column (no
@@ -1158,7 +1192,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nref = 0, fsum = 0;
         const uint64_t t_col = clock64();
         C.ncompact = C.nspill = 0;
-        for (int q = 0; q < 8; ++q) C.q[q] = C.q2[q] = 0;
+        for (int q = 0; q < 8; ++q) C.q[q] = C.q2[q] = C.q3[q] = 0;
 #endif
         uint64_t step = 0;
         const uint32_t need = par_need(n);
@@ -1343,6 +1377,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             for (int q = 0; q < 8; ++q) stats[0].prof[2][q] = pf[q];
             for (int q = 0; q < 8; ++q) stats[0].prof[3][q] = C.q[q];
             for (int q = 0; q < 8; ++q) stats[0].prof[4][q] = C.q2[q];
+            for (int q = 0; q < 8; ++q) stats[0].prof[1][q] = C.q3[q];
         }
 #endif
         if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)adds);

@@ -318,6 +318,32 @@ def test_torus2048_maxdim1_invariants(gpu):
     assert pers[1] > 2.0 * pers[2]
 
 
+def test_torus2048_maxdim2_invariants(gpu, monkeypatch):
+    """Top of the north-star N range at maxdim 2 (N=2048, H0-H2: ~1.4 s on the
+    GPU; the oracle would need hours here, so size-independent properties):
+    the forest, every H1 and H2 column paired or essential, the torus's two
+    dominant H1 classes and one dominant H2 class, bitwise-repeatable, and H0/H1
+    identical to the maxdim-1 call.  The parallel reducer must not fall back
+    (TDA_PAR_STRICT)."""
+    X = gpu.synthetic.torus(2048)
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")
+    a = gpu.ripser_batch(X[None], maxdim=2)[0]
+    b = gpu.ripser_batch(X[None], maxdim=2)[0]
+    c = gpu.ripser_batch(X[None], maxdim=1)[0]
+    for d in range(3):
+        assert _pairs(a, d) == _pairs(b, d) and a.checksum[d] == b.checksum[d]
+    for d in range(2):
+        assert _pairs(a, d) == _pairs(c, d) and a.checksum[d] == c.checksum[d]
+    assert int(np.isinf(a.dgms[0][:, 1]).sum()) == 1 and a.n_all_pairs[0] == 2047
+    for d in (1, 2):
+        assert a.n_columns[d] == a.n_all_pairs[d] + int(np.isinf(a.dgms[d][:, 1]).sum()), d
+        assert np.all(np.diff(a.dgms[d][:, 0]) <= 0), d  # emission order: decreasing birth
+    p1 = np.sort(a.dgms[1][:, 1] - a.dgms[1][:, 0])[::-1]
+    p2 = np.sort(a.dgms[2][:, 1] - a.dgms[2][:, 0])[::-1]
+    assert p1[1] > 2.0 * p1[2]
+    assert p2[0] > 5.0 * p2[1]
+
+
 def _large_golden():
     return np.load(os.path.join(GOLDEN, "large_cases.npz"))
 
