@@ -1067,7 +1067,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         hipLaunchKernelGGL(k_h2_phase1, dim3(L, kP1Grid), dim3(64), p.p1_lds, st, dist, n, stats, db[2], sb, (const uint16_t*)dnb.cls2,
                            p.n2p, p.bm_words, (const uint32_t*)dnb.res1, (uint32_t)p.piv_words[1], step_limit());
         HIPC(hipGetLastError());
-        if (int rc = (st == s && serial_stages ? tm : tm3).mark("k_h2_phase1")) return rc;
+        if (int rc = (st == s ? tm : tm3).mark("k_h2_phase1")) return rc;
         HIPC(hipEventRecord(w.evp, st));
         return 0;
     };
@@ -1089,6 +1089,32 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         launch_sort(2, 1, w.stream3, h2_side ? 4096 : 16384);
         HIPC(hipGetLastError());
         if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
+        return 0;
+    };
+    Pair* const pairs1 = (Pair*)(B + p.o_pairs[1]);
+    Pair* const pairs2 = p.maxdim >= 2 ? (Pair*)(B + p.o_pairs[2]) : pairs1;
+    auto launch_chain = [&](hipStream_t st) -> int {  // dense H1 (N <= 64): one k_h1_chain instantiation per (words, mode)
+        switch (p.dK * 3 + p.cmode) {
+#define TDA_CHAIN(K, F)                                                                                                          \
+    case K * 3 + F:                                                                                                              \
+        hipLaunchKernelGGL((k_h1_chain<K, F>), dim3(L), dim3(kChainT), p.chain_lds, st, dist, n, stats, db[1], rb, dnb, step_limit(), \
+                           pairs1, p.pcap[1]);                                                                                   \
+        break;
+            TDA_CHAIN(1, 0) TDA_CHAIN(2, 0) TDA_CHAIN(3, 0) TDA_CHAIN(4, 0) TDA_CHAIN(6, 0) TDA_CHAIN(9, 0) TDA_CHAIN(12, 0)
+            TDA_CHAIN(16, 0) TDA_CHAIN(21, 0)
+            TDA_CHAIN(1, 1) TDA_CHAIN(2, 1) TDA_CHAIN(3, 1) TDA_CHAIN(4, 1) TDA_CHAIN(6, 1) TDA_CHAIN(9, 1) TDA_CHAIN(12, 1)
+            TDA_CHAIN(1, 2) TDA_CHAIN(2, 2) TDA_CHAIN(3, 2) TDA_CHAIN(4, 2) TDA_CHAIN(6, 2) TDA_CHAIN(9, 2) TDA_CHAIN(12, 2)
+#undef TDA_CHAIN
+            default:
+                return fail(TDA_E_INVALID, "no k_h1_chain instantiation for this N");
+        }
+        HIPC(hipGetLastError());
+        return 0;
+    };
+    auto launch_h2_finish = [&](hipStream_t st) -> int {
+        hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), p.rcfg.bytes, st, dist, n, stats, db[1], db[2], rb, p.rcfg, sb,
+                           (const uint32_t*)dnb.res1, pairs2, p.pcap[2]);
+        HIPC(hipGetLastError());
         return 0;
     };
     if (p.maxdim >= 1) {
@@ -1149,37 +1175,19 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipStreamWaitEvent(s, w.evj, 0));  // join: triangle ranks
         MARK("wait:join");  // keeps the side streams' time out of the next kernel's stage
         const bool p1 = n <= 1024, p2 = n <= 256;
-        Pair* pairs1 = (Pair*)(B + p.o_pairs[1]);
-        Pair* pairs2 = p.maxdim >= 2 ? (Pair*)(B + p.o_pairs[2]) : pairs1;
         const ReduceAllCfg& rc = p.rcfg;
 #define TDA_LAUNCH_RED(LW, P1, P2)                                                                                        \
     hipLaunchKernelGGL((k_reduce_all<LW, P1, P2>), dim3(L), dim3(64), rc.bytes, s, dist, n, p.maxdim, stats, db[1], db[2], rb, rc, \
                        pairs1, pairs2, p.pcap[1], p.maxdim >= 2 ? p.pcap[2] : 0)
         if (p.dense) {
-            switch (p.dK * 3 + p.cmode) {
-#define TDA_CHAIN(K, F)                                                                                                          \
-    case K * 3 + F:                                                                                                              \
-        hipLaunchKernelGGL((k_h1_chain<K, F>), dim3(L), dim3(kChainT), p.chain_lds, s, dist, n, stats, db[1], rb, dnb, step_limit(), \
-                           pairs1, p.pcap[1]);                                                                                   \
-        break;
-                TDA_CHAIN(1, 0) TDA_CHAIN(2, 0) TDA_CHAIN(3, 0) TDA_CHAIN(4, 0) TDA_CHAIN(6, 0) TDA_CHAIN(9, 0) TDA_CHAIN(12, 0)
-                TDA_CHAIN(16, 0) TDA_CHAIN(21, 0)
-                TDA_CHAIN(1, 1) TDA_CHAIN(2, 1) TDA_CHAIN(3, 1) TDA_CHAIN(4, 1) TDA_CHAIN(6, 1) TDA_CHAIN(9, 1) TDA_CHAIN(12, 1)
-                TDA_CHAIN(1, 2) TDA_CHAIN(2, 2) TDA_CHAIN(3, 2) TDA_CHAIN(4, 2) TDA_CHAIN(6, 2) TDA_CHAIN(9, 2) TDA_CHAIN(12, 2)
-#undef TDA_CHAIN
-                default:
-                    return fail(TDA_E_INVALID, "no k_h1_chain instantiation for this N");
-            }
-            HIPC(hipGetLastError());
+            if (int rc = launch_chain(s)) return rc;
             MARK("k_h1_chain");
             if (p.maxdim >= 2) {
                 if (serial_stages)
                     if (int rc = launch_phase1(s)) return rc;
                 HIPC(hipStreamWaitEvent(s, w.evp, 0));  // phase-1 results
                 MARK("wait:phase1");
-                hipLaunchKernelGGL(k_reduce_h2_finish, dim3(L), dim3(64), rc.bytes, s, dist, n, stats, db[1], db[2], rb, rc, sb,
-                                   (const uint32_t*)dnb.res1, pairs2, p.pcap[2]);
-                HIPC(hipGetLastError());
+                if (int rc = launch_h2_finish(s)) return rc;
                 MARK("k_reduce_h2_finish");
             }
         } else if (p.big) {

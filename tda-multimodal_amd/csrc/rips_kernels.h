@@ -158,7 +158,10 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
 // LDS writes).
 // The squared norms accumulate (sequential k, FMA: the oracle's order) in the
 // same pass from the LDS tile, threads 0-63 for the i rows, 64-127 for j.
-constexpr int kDmT = 64, kDmKC = 32, kDmS = kDmKC + 2;
+#ifndef TDA_DM_KC  // build-time A/B knob (tools/): K chunk of k_distance_mfma
+#define TDA_DM_KC 32
+#endif
+constexpr int kDmT = 64, kDmKC = TDA_DM_KC, kDmS = kDmKC + 2;
 typedef double dm_d4 __attribute__((ext_vector_type(4)));
 
 // METRIC 1: cosine distance instead (UMAP input, umap.distances.cosine:
@@ -202,43 +205,68 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
     double nacc = 0.0;
     const int nt_r = tid & 63, nt_t = (tid >> 6) & 1, nt_h = tid >> 7;
     if (tid < 2 * kDmT) rmx[tid >> 6][tid & 63] = 0;
-    // register double buffer: chunk k0 + kDmKC is in flight while chunk k0 feeds the MFMAs
-    T pre[4][4];
+    // register prefetch two chunks deep (r03): chunks c + 1 and c + 2 are in flight while chunk
+    // c feeds the MFMAs (one chunk ahead left the kernel waiting on MALL/HBM latency, not on the
+    // MFMA pipe).  A diagonal tile (bi == bj) loads and stages its row panel once and reads the
+    // B operand from the A panel.
+    constexpr int kDmG = kDmKC / 4, kDmU = 2 * kDmT * kDmG / 256;  // 4-element groups per row, per thread
+    const bool diag = bi == bj;
     int kbeg = 0, kend = D;  // this slice's K range (whole chunks)
     if (SPLIT) {
         const int C = (D + kDmKC - 1) / kDmKC, S = (int)gridDim.z, z = (int)blockIdx.z;
         kbeg = (int)((int64_t)C * z / S) * kDmKC;
         kend = min(D, (int)((int64_t)C * (z + 1) / S) * kDmKC);
     }
-    auto load = [&](int k0) {
+    const bool vec4 = (D & 3) == 0;  // rows 16-B aligned: one 4-element load per group
+    auto load = [&](T (&pr)[kDmU][4], int k0) {
         const int kc = min(kDmKC, kend - k0);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {  // 2 tiles x 64 rows x kDmKC / 4 groups of 4 consecutive k
-            const int e = tid + 256 * u, t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
+        for (int u = 0; u < kDmU; ++u) {  // 2 tiles x 64 rows x kDmKC / 4 groups of 4 consecutive k
+            const int e = tid + 256 * u, t = e / (kDmT * kDmG), r = (e / kDmG) % kDmT, c0 = (e % kDmG) * 4;
             const int g = (t ? bj : bi) * kDmT + r;
             const T* src = Xl + (size_t)g * D + k0 + c0;
+            const bool live = g < n && !(diag && t);
+            if (live && vec4 && c0 + 4 <= kc) {
+                if constexpr (sizeof(T) == 4) {
+                    const float4 v = *(const float4*)src;
+                    pr[u][0] = v.x, pr[u][1] = v.y, pr[u][2] = v.z, pr[u][3] = v.w;
+                } else {
+                    const double2 v0 = *(const double2*)src, v1 = *(const double2*)(src + 2);
+                    pr[u][0] = v0.x, pr[u][1] = v0.y, pr[u][2] = v1.x, pr[u][3] = v1.y;
+                }
+            } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) pre[u][q] = (g < n && c0 + q < kc) ? src[q] : (T)0;
+                for (int q = 0; q < 4; ++q) pr[u][q] = (live && c0 + q < kc) ? src[q] : (T)0;
+            }
         }
     };
-    auto stage = [&](int buf) {
+    auto stage = [&](const T (&pr)[kDmU][4], int buf) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e = tid + 256 * u, t = e >> 9, r = (e >> 3) & 63, c0 = (e & 7) * 4;
+        for (int u = 0; u < kDmU; ++u) {
+            const int e = tid + 256 * u, t = e / (kDmT * kDmG), r = (e / kDmG) % kDmT, c0 = (e % kDmG) * 4;
+            if (diag && t) continue;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) xs[buf][t][r][c0 + q] = pre[u][q];
+            for (int q = 0; q < 4; ++q) xs[buf][t][r][c0 + q] = pr[u][q];
         }
     };
-    load(kbeg);
-    stage(0);
-    __syncthreads();
-    int buf = 0;
-    for (int k0 = kbeg; k0 < kend; k0 += kDmKC, buf ^= 1) {
-        const bool more = k0 + kDmKC < kend;
-        if (more) load(k0 + kDmKC);  // global loads in flight under this chunk's MFMAs
+    // 16x16 blocks of this wave's 32x32 quadrant that hold an output entry
+    // (i <= j, both < n): the padding rows of the last tile row/column and the
+    // blocks below a diagonal tile's diagonal are skipped (wave-uniform).  At
+    // N = 144 that is 45 of the 96 blocks of the six upper tiles (r03).
+    bool need[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int ri0 = bi * kDmT + wr * 32 + a * 16, cj0 = bj * kDmT + wc * 32 + b * 16;
+            need[a][b] = ri0 < n && cj0 < n && ri0 <= cj0 + 15;
+        }
+    const int tb = diag ? 0 : 1;    // panel of the B operand
+    const int tn = diag ? 0 : nt_t;  // panel of this thread's norm rows
+    auto compute = [&](int buf) {
 #pragma unroll 8
         for (int cc = 0; cc < kDmKC / 2; ++cc) {  // zero padding adds exact zeros
-            const double v = (double)xs[buf][nt_t][nt_r][nt_h * (kDmKC / 2) + ((cc + nt_r) & (kDmKC / 2 - 1))];
+            const double v = (double)xs[buf][tn][nt_r][nt_h * (kDmKC / 2) + ((cc + nt_r) & (kDmKC / 2 - 1))];
             nacc = fma(v, v, nacc);
         }
 #pragma unroll
@@ -248,13 +276,31 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
 #pragma unroll
             for (int a = 0; a < 2; ++a) av[a] = (double)xs[buf][0][wr * 32 + a * 16 + (lane & 15)][k];
 #pragma unroll
-            for (int b = 0; b < 2; ++b) bv[b] = (double)xs[buf][1][wc * 32 + b * 16 + (lane & 15)][k];
+            for (int b = 0; b < 2; ++b) bv[b] = (double)xs[buf][tb][wc * 32 + b * 16 + (lane & 15)][k];
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+                for (int b = 0; b < 2; ++b)
+                    if (need[a][b]) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
-        if (more) stage(buf ^ 1);  // the other buffer: its last readers passed the previous barrier
+    };
+    T pa[kDmU][4], pb[kDmU][4];
+    const int nch = (kend - kbeg + kDmKC - 1) / kDmKC;
+    load(pa, kbeg);
+    if (nch > 1) load(pb, kbeg + kDmKC);
+    stage(pa, 0);
+    __syncthreads();
+    // two chunks per trip: chunk c (buffer 0, pb holds c + 1), then c + 1 (buffer 1, pa holds c + 2);
+    // a buffer is restaged only after the barrier that its last readers passed
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 2 < nch) load(pa, kbeg + (c + 2) * kDmKC);
+        compute(0);
+        if (c + 1 < nch) stage(pb, 1);
+        __syncthreads();
+        if (c + 1 >= nch) break;
+        if (c + 3 < nch) load(pb, kbeg + (c + 3) * kDmKC);
+        compute(1);
+        if (c + 2 < nch) stage(pa, 0);
         __syncthreads();
     }
     nrp[nt_h][nt_t][nt_r] = nacc;
