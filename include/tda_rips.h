@@ -152,6 +152,11 @@ typedef struct tda_rips_result {
 #define TDA_FLAG_STAGE_SERIAL 2
 /* with want_dist and float64 point clouds: also return result->dist64 */
 #define TDA_FLAG_DIST64 4
+/* distances and the side metrics asked for (want_twonn, labels) only: no
+ * persistence at all (maxdim must be 0); every diagram is empty and thresh /
+ * num_edges are 0.  What metrics.compute_intrinsic_dimensionality needs
+ * (reference metrics.py:113-208 computes no persistence). */
+#define TDA_FLAG_NO_PERSISTENCE 8
 
 /* Batched point clouds (or distance matrices) -> persistence diagrams. */
 int tda_rips_batch(const tda_rips_args *args, tda_rips_result **out);

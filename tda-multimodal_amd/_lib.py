@@ -85,6 +85,7 @@ class RipsResult(ctypes.Structure):
 TDA_FLAG_STAGE_TIMES = 1
 TDA_FLAG_STAGE_SERIAL = 2
 TDA_FLAG_DIST64 = 4
+TDA_FLAG_NO_PERSISTENCE = 8
 TDA_MAX_SLOTS = 8
 
 

@@ -733,6 +733,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 
     // TwoNN estimates -> host-mapped buffer (stable address: a graph source)
     const bool want_tn = a.want_twonn != 0;
+    const bool no_ph = (a.flags & TDA_FLAG_NO_PERSISTENCE) != 0;  // distances + side metrics only
     if (want_tn && w.htn_cap < (size_t)L) {
         drop_graphs(w);
         if (w.htn) HIPC(hipHostFree(w.htn));
@@ -879,7 +880,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipStreamWaitEvent(s4, w.evf, 0));
         if (int rc = tm2.begin()) return rc;
         if (int rc = tm4.begin()) return rc;
-        if (n <= kSmallN) {
+        if (no_ph) {
+            // TDA_FLAG_NO_PERSISTENCE: no spanning forest, no H0 pairs
+        } else if (n <= kSmallN) {
             hipLaunchKernelGGL(k_h0_wave, dim3(L), dim3(64), 64 * 64 * 4 + 64 * 4 + 64 * 8, s4, dist, n, rowmax, a.thresh, stats,
                                (uint32_t*)(B + p.o_mst), p.mst_words, (Pair*)(B + p.o_pairs[0]), p.pcap[0]);
         } else {
@@ -932,7 +935,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             }
         }
         HIPC(hipGetLastError());
-        if (int rc = tm4.mark("k_h0")) return rc;
+        if (!no_ph)
+            if (int rc = tm4.mark("k_h0")) return rc;
         HIPC(hipEventRecord(w.evh, s4));
         if (nls) {  // silhouette scores on the same distance matrices (sklearn semantics), after the H0 join
             const size_t lds = (size_t)sil_K * kSilT * 8 + (size_t)n * 4;
@@ -1355,8 +1359,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     if (errs && getenv("TDA_DEBUG"))
         fprintf(stderr, "[tda] N=%d L=%d errs=%s force_global=%d scale=%d\n", n, L, err_flags(errs).c_str(), (int)force_global, scale);
     if (errs & (ERR_PAR | ERR_PAR2)) {
-        // k_reduce_par gave up (a capacity or spin limit): reduce on the serial radix-heap kernel --
-        // everything after an H1 abort (ERR_PAR), only H2 after an H2 abort (ERR_PAR2 alone)
+        // k_reduce_par gave up (a capacity or spin limit): the whole call is re-run (distances,
+        // H0, apparent pairs included) with the reduction on the serial radix-heap kernel -- both
+        // dimensions after an H1 abort (ERR_PAR); after an H2 abort alone (ERR_PAR2) H1 stays on
+        // k_reduce_par and only H2 moves to k_reduce_big.  An abort costs the first call of a
+        // shape about twice its time; the retry memo skips the failing attempt on later calls.
         const int np_next = (errs & ERR_PAR) ? 2 : std::max(no_par, 1);
         ParCtl c;
         HIPC(hipMemcpy(&c, B + p.o_pctl, sizeof(c), hipMemcpyDeviceToHost));
@@ -1653,6 +1660,7 @@ int validate(const tda_rips_args* a) {
     if (a->maxdim == 1 && a->N > 2900) return fail(TDA_E_UNSUPPORTED, "maxdim=1 requires N <= 2900");
     if (a->maxdim == 2 && a->N > 2048) return fail(TDA_E_UNSUPPORTED, "maxdim=2 requires N <= 2048");
     if (std::isnan(a->thresh)) return fail(TDA_E_INVALID, "thresh is NaN");
+    if ((a->flags & TDA_FLAG_NO_PERSISTENCE) && a->maxdim != 0) return fail(TDA_E_INVALID, "TDA_FLAG_NO_PERSISTENCE needs maxdim 0");
     if (a->want_twonn && !(a->twonn_discard >= 0.0 && a->twonn_discard < 1.0 && a->twonn_eps >= 0.0f))
         return fail(TDA_E_INVALID, "TwoNN needs 0 <= discard_fraction < 1 and eps >= 0");
     return 0;

@@ -68,8 +68,9 @@ constexpr uint64_t kParEss = kEmpty64;        // colpiv: essential (zero column)
 constexpr uint64_t kParSkip = kEmpty64 - 1;   // colpiv: cleared column (H0 death)
 constexpr uint32_t kParSpin = 1u << 22;       // polls before a wait on another workgroup is declared hung
 
-// k_reduce_par aborted: the host falls back to k_reduce_big (ERR_PAR: the H1
-// launch, everything is redone serially; ERR_PAR2: only the H2 launch)
+// k_reduce_par aborted: the host re-runs the call with k_reduce_big (ERR_PAR:
+// the H1 launch aborted, both dimensions go serial; ERR_PAR2: the H2 launch
+// aborted, H1 stays parallel and H2 goes serial)
 enum : int32_t { ERR_PAR = 128, ERR_PAR2 = 256 };
 
 struct ParCtl {  // zeroed by k_par_init

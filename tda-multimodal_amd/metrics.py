@@ -91,7 +91,8 @@ def compute_intrinsic_dimensionality(data, discard_fraction: float = 0.1, eps: f
     if n <= 5 or B == 0:  # metrics.py:136-137
         out = np.full(B, np.nan, dtype=np.float32)
     else:
-        res = ripser_batch(x, maxdim=0, twonn=True, discard_fraction=discard_fraction, eps=eps)
+        # distances + k_twonn only (TDA_FLAG_NO_PERSISTENCE): the reference computes no persistence here
+        res = ripser_batch(x, maxdim=0, twonn=True, discard_fraction=discard_fraction, eps=eps, persistence=False)
         out = np.array([r.twonn for r in res], dtype=np.float32)
     if is_t:
         import torch

@@ -221,7 +221,7 @@ def encode_labels(label_sets, n: int) -> np.ndarray:
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
                  want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None,
                  stage_serial: bool = False, twonn: bool = False, discard_fraction: float = 0.1, eps: float = 1e-10,
-                 want_dist64: bool = False, slot: int = 0):
+                 want_dist64: bool = False, slot: int = 0, persistence: bool = True):
     """Persistence of L layers in one call.
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
@@ -242,6 +242,8 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     slot: the device workspace (0 .. 7) the call runs in; calls from different
     host threads on different slots run concurrently on the GPU (see
     :class:`SweepPipeline`).
+    persistence=False (maxdim 0 only): distances and the side metrics asked for
+    (``twonn``, ``labels``) without any persistence; every diagram is empty.
     """
     _check_common(maxdim, 2, False, None, "euclidean")
     a = _lib.RipsArgs()
@@ -287,6 +289,10 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     a.slot = int(slot)
     a.want_dist = 1 if want_dist else 0
     a.flags = (_lib.TDA_FLAG_STAGE_TIMES | (_lib.TDA_FLAG_STAGE_SERIAL if stage_serial else 0)) if stage_times else 0
+    if not persistence:
+        if maxdim != 0:
+            raise ValueError("persistence=False needs maxdim=0")
+        a.flags |= _lib.TDA_FLAG_NO_PERSISTENCE
     if want_dist64:  # f64 points: the f64 distance matrix too (ripser.py's dperm2all)
         a.flags |= _lib.TDA_FLAG_DIST64
         a.want_dist = 1

@@ -23,6 +23,12 @@ def test_header_and_binding_agree(pkg):
     assert _declared_functions() == sorted(pkg.EXPORTS)
 
 
+def test_header_flags_match_binding(pkg):
+    src = open(os.path.join(ROOT, "include", "tda_rips.h")).read()
+    flags = dict(re.findall(r"#define (TDA_FLAG_[A-Z0-9_]+) (\d+)", src))
+    assert flags and all(int(v) == getattr(pkg._lib, k) for k, v in flags.items())
+
+
 def test_library_exports_every_declared_symbol(built_lib):
     lib = ctypes.CDLL(built_lib)
     for name in _declared_functions():
@@ -55,7 +61,9 @@ def test_invalid_arguments_rejected_before_device(pkg, built_lib):
     assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1
     a.N, a.thresh = 4, float("nan")
     assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1
-    a.thresh = float("inf")
+    a.thresh, a.flags = float("inf"), _lib.TDA_FLAG_NO_PERSISTENCE
+    assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1  # no persistence needs maxdim 0
+    a.flags = 0
     assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -5  # no gfx950 here
     D = np.zeros(5, np.float32)
     assert L.tda_rips_dm(D.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 5, 2, 1, float("inf"), 0,

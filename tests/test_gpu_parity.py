@@ -515,6 +515,22 @@ def test_twonn_vs_reference_goldens_and_oracle(gpu):
             assert abs(res[b].twonn - o) <= 1e-5 * abs(o), (name, b)
 
 
+def test_twonn_without_persistence(gpu):
+    """compute_intrinsic_dimensionality runs distances + k_twonn only
+    (TDA_FLAG_NO_PERSISTENCE): the same estimates, bit for bit, as the call that
+    also computes H0, and empty diagrams."""
+    X = np.random.default_rng(7).normal(size=(4, 144, 64)).astype(np.float32)
+    with_ph = gpu.ripser_batch(X, maxdim=0, twonn=True)
+    no_ph = gpu.ripser_batch(X, maxdim=0, twonn=True, persistence=False)
+    for a, b in zip(with_ph, no_ph):
+        assert np.float32(a.twonn) == np.float32(b.twonn)
+        assert len(a.dgms[0]) == 144 and len(b.dgms[0]) == 0
+    got = gpu.compute_intrinsic_dimensionality(X)
+    assert np.array_equal(got, np.array([r.twonn for r in with_ph], np.float32))
+    with pytest.raises(ValueError):
+        gpu.ripser_batch(X, maxdim=1, persistence=False)
+
+
 def test_f64_points_vs_sklearn_f64_goldens(gpu):
     """SURVEY a2' (float64 points), pinned to sklearn: the GPU's float64
     distances (LayerResult.dist64, ripser()'s dperm2all) within 1e-12
