@@ -1,5 +1,5 @@
 // rips_reduce_par.h -- large-N H1 reduction with many residual columns in
-// flight at once (k_reduce_par), one 256-thread workgroup per column.
+// flight at once (k_reduce_par), one 512-thread workgroup per column.
 //
 // [upstream ripser.cpp compute_pairs] reduces the residual columns one after
 // the other.  The persistence PAIRING does not depend on that order: any
@@ -47,7 +47,10 @@
 
 namespace tda {
 
-constexpr int kParT = 256;
+#ifndef TDA_PAR_T  // build-time A/B knob (tools/): threads per column workgroup
+#define TDA_PAR_T 512
+#endif
+constexpr int kParT = TDA_PAR_T;
 constexpr int kParW = kParT / 64;
 #ifndef TDA_PAR_LOG  // build-time A/B knobs (tools/): front capacity and refill target
 #define TDA_PAR_LOG 4096
@@ -60,9 +63,9 @@ constexpr uint32_t kFrontIdx = TDA_PAR_LOG;          // front index slots (kFron
 constexpr uint32_t kFrontLive = TDA_PAR_LOG * 7 / 16;  // live front keys that trigger a spill (1792 at 4096)
 constexpr uint32_t kFrontFill = TDA_PAR_FILL;        // refill / spill target
 constexpr int kParChunks = 22;         // chunk k of an HBM bucket holds 256 << k keys
-constexpr int kParRegs = 8;            // keys per thread per pass of refills and record adds
+constexpr int kParRegs = 2048 / kParT;  // keys per thread per pass of refills and record adds (2048 per pass)
 constexpr int kParRefill = 2;          // a refill keeps up to kParRefill passes (4096 keys) in registers
-constexpr int kParRV = 4;              // coboundary vertices per thread per round (kParT * 4 = 1024)
+constexpr int kParRV = 1024 / kParT;   // coboundary vertices per thread per round (1024 per round)
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
 constexpr uint64_t kParEss = kEmpty64;        // colpiv: essential (zero column)
 constexpr uint64_t kParSkip = kEmpty64 - 1;   // colpiv: cleared column (H0 death)
