@@ -485,6 +485,7 @@ struct StageTimer {
 };
 
 std::mutex g_ws_mu;
+std::mutex g_capture_mu;  // graph capture + instantiation
 std::vector<Workspace*> g_ws;
 
 Workspace* get_ws(int dev, int slot) {
@@ -574,7 +575,9 @@ int grow_hout(Workspace& w, size_t need) {
 }
 
 bool g_attr_done[64] = {false};
+std::mutex g_attr_mu;
 int set_lds_attrs(int dev) {
+    std::lock_guard<std::mutex> lk(g_attr_mu);  // first calls on several workspace slots at once
     if (dev < 64 && g_attr_done[dev]) return 0;
     HIPC(hipFuncSetAttribute((const void*)k_h0<0, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_h0<kH0BorWQ, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -1314,6 +1317,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipGraphLaunch(ge->exec, s));
         HIPC(hipEventRecord(w.ev1, s));
     } else if (capture) {
+        // capture + instantiate one graph at a time across the process: concurrent
+        // captures from several slot threads crashed the HIP runtime once (r03, host
+        // segfault inside a first call of two slots); replays run concurrently
+        std::lock_guard<std::mutex> cap_lock(g_capture_mu);
         HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         const int rc = enqueue();
         hipGraph_t graph = nullptr;
