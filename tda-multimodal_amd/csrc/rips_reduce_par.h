@@ -64,7 +64,10 @@ constexpr uint32_t kFrontLive = TDA_PAR_LOG * 7 / 16;  // live front keys that t
 constexpr uint32_t kFrontFill = TDA_PAR_FILL;        // refill / spill target
 constexpr int kParChunks = 22;         // chunk k of an HBM bucket holds 256 << k keys
 constexpr int kParRegs = 2048 / kParT;  // keys per thread per pass of refills and record adds (2048 per pass)
-constexpr int kParRefill = 2;          // a refill keeps up to kParRefill passes (4096 keys) in registers
+#ifndef TDA_PAR_REFILL  // build-time A/B knob (tools/): refill passes kept in registers
+#define TDA_PAR_REFILL 2
+#endif
+constexpr int kParRefill = TDA_PAR_REFILL;          // a refill keeps up to kParRefill passes (4096 keys) in registers
 constexpr int kParRV = 1024 / kParT;   // coboundary vertices per thread per round (1024 per round)
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
 constexpr uint64_t kParEss = kEmpty64;        // colpiv: essential (zero column)
