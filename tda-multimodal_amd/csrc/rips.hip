@@ -834,7 +834,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         } else if (mfma && p.dsplit > 1) {
             hipLaunchKernelGGL((k_distance_mfma<float, 0, true>), gsplit, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax,
                                gpart, npart);
+            MARK("k_distance_mfma");  // the Gram kernel alone (bench roofline): combine and row maxima are their own stages
             hipLaunchKernelGGL((k_distance_combine<float, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
+            MARK("k_distance_combine");
             hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
         } else if (mfma && p.dtype == TDA_F64)
             hipLaunchKernelGGL((k_distance_mfma<double>), dim3(nt * (nt + 1) / 2, L), dim3(256), 0, s, (const double*)x, n, (int)p.D,
@@ -867,7 +869,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
     }
     HIPC(hipGetLastError());
-    MARK(input_kind != 0 ? "k_square_dist" : dist_mfma ? "k_distance_mfma" : "k_distance");
+    MARK(input_kind != 0 ? "k_square_dist" : dist_mfma ? (p.dsplit > 1 && p.dtype == TDA_F32 ? "k_rowmax" : "k_distance_mfma") : "k_distance");
     HIPC(hipEventRecord(w.evf, s));  // fork point of the side streams
 
     DenseBufs dnb = {};
