@@ -99,6 +99,7 @@ struct Plan {
     uint64_t ecap = 0;    // per-layer stride of the sorted edge lengths
     size_t o_dsort = 0, o_dtmp = 0, o_dcode = 0;
     int dsplit = 1;       // K slices of k_distance_mfma (1: no split)
+    bool gram_layer = false;  // N <= 144, f32: k_gram_layer (whole upper triangle per workgroup) + combine
     size_t o_gpart = 0, o_npart = 0, o_d64 = 0;
     size_t o_bcomp = 0, o_bcheap = 0, o_bctl = 0;  // Borůvka H0 state (N > kH0WaveMaxN)
     bool serial_tables = false;  // HBM working tables of k_reduce_all (global mode) / k_reduce_big
@@ -265,7 +266,17 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         // (debug_tda_pipeline.py:92), never on this call's L: a layer's distances (and so its
         // diagram) are the same in a single call, a batch and every multi-GPU shard.
         const bool mfma = !p.is_dist && (test_env_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !test_env_is("TDA_DIST", "scalar")));
-        if (mfma) {
+        if (mfma && p.dtype == TDA_F32 && N <= (uint64_t)kGlMaxN && !test_env_is("TDA_DIST", "tiles")) {
+            // whole-layer Gram (k_gram_layer): K slices so that ~256 workgroups run a 32-layer
+            // sweep, at least 16 chunks each -- again from (N, D) only
+            const uint64_t chunks = ((uint64_t)p.D + kDmKC - 1) / kDmKC;
+            uint64_t sp = std::min<uint64_t>(8, std::max<uint64_t>(1, chunks / 16));
+            if (const char* e = test_env("TDA_DIST_SPLIT")) sp = std::max(1, atoi(e));
+            p.dsplit = (int)sp;
+            p.gram_layer = true;
+            p.o_gpart = take(L * sp * N * N * 8);
+            p.o_npart = take(L * sp * N * 8);
+        } else if (mfma) {
             constexpr uint64_t kSplitRefL = 32;
             const uint64_t nt = (N + kDmT - 1) / kDmT, tiles = nt * (nt + 1) / 2 * kSplitRefL, chunks = ((uint64_t)p.D + kDmKC - 1) / kDmKC;
             uint64_t sp = std::min<uint64_t>(8, std::max<uint64_t>(1, (768 + tiles - 1) / tiles));
@@ -831,9 +842,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                                gpart, npart, (double*)nullptr);
             hipLaunchKernelGGL((k_distance_combine<double, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax, d64);
             hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
-        } else if (mfma && p.dsplit > 1) {
-            hipLaunchKernelGGL((k_distance_mfma<float, 0, true>), gsplit, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax,
-                               gpart, npart);
+        } else if (mfma && (p.dsplit > 1 || p.gram_layer)) {
+            if (p.gram_layer)
+                hipLaunchKernelGGL(k_gram_layer, dim3((unsigned)p.dsplit, L), dim3(256), 0, s, (const float*)x, n, (int)p.D, gpart, npart);
+            else
+                hipLaunchKernelGGL((k_distance_mfma<float, 0, true>), gsplit, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax,
+                                   gpart, npart);
             MARK("k_distance_mfma");  // the Gram kernel alone (bench roofline): combine and row maxima are their own stages
             hipLaunchKernelGGL((k_distance_combine<float, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
             MARK("k_distance_combine");
@@ -869,7 +883,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
     }
     HIPC(hipGetLastError());
-    MARK(input_kind != 0 ? "k_square_dist" : dist_mfma ? (p.dsplit > 1 && p.dtype == TDA_F32 ? "k_rowmax" : "k_distance_mfma") : "k_distance");
+    MARK(input_kind != 0 ? "k_square_dist" : dist_mfma ? ((p.dsplit > 1 || p.gram_layer) && p.dtype == TDA_F32 ? "k_rowmax" : "k_distance_mfma") : "k_distance");
     HIPC(hipEventRecord(w.evf, s));  // fork point of the side streams
 
     DenseBufs dnb = {};

@@ -383,6 +383,113 @@ __global__ __launch_bounds__(256) void k_distance_mfma(const T* __restrict__ X, 
     }
 }
 
+// N <= 144 (r03): the whole upper triangle of a layer's Gram matrix in one
+// workgroup per (K slice, layer).  The layer's rows of a K chunk are staged in
+// LDS once and every one of the nb(nb+1)/2 16x16 blocks (45 at N = 144) is an
+// accumulator of one of the four waves (block q -> wave q % 4, <= 12 each), so
+// every row is read from HBM once per slice (k_distance_mfma's 64-row tiles
+// read each panel once per tile of its row and column: 3.1x the input at
+// N = 144) and the MFMA work is spread evenly over the waves.  Partial Gram
+// entries (i < j) and row norms per slice go to k_distance_combine, the same
+// fixed-order combine as the tiled split.  f32 input, Euclidean.
+constexpr int kGlMaxNB = 9, kGlMaxN = 16 * kGlMaxNB, kGlMB = (kGlMaxNB * (kGlMaxNB + 1) / 2 + 3) / 4;
+__global__ __launch_bounds__(256) void k_gram_layer(const float* __restrict__ X, int n, int D, double* __restrict__ gpart,
+                                                    double* __restrict__ npart) {
+    __shared__ float xs[2][kGlMaxN][kDmS];
+    const int l = blockIdx.y, z = blockIdx.x, S = gridDim.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nb = (n + 15) >> 4, np = nb * 16, nblk = nb * (nb + 1) / 2;
+    const float* Xl = X + (size_t)l * n * D;
+    const int C = (D + kDmKC - 1) / kDmKC;
+    const int kbeg = (int)((int64_t)C * z / S) * kDmKC, kend = min(D, (int)((int64_t)C * (z + 1) / S) * kDmKC);
+    // this wave's blocks: q = wv, wv + 4, ... of the row-major upper triangle
+    int bi[kGlMB], bj[kGlMB];
+    int nw = 0;
+#pragma unroll
+    for (int u = 0; u < kGlMB; ++u) {
+        int q = wv + 4 * u, r = 0;
+        bi[u] = bj[u] = 0;
+        if (q < nblk) {
+            while (q >= nb - r) q -= nb - r, ++r;
+            bi[u] = r, bj[u] = r + q;
+            nw = u + 1;
+        }
+    }
+    dm_d4 acc[kGlMB];
+#pragma unroll
+    for (int u = 0; u < kGlMB; ++u) acc[u] = dm_d4{0.0, 0.0, 0.0, 0.0};
+    double nacc = 0.0;  // row tid's squared norm over this slice, k in order
+    constexpr int kG = kDmKC / 4;                         // 4-element groups per row
+    constexpr int kU = (kGlMaxN * kG + 255) / 256;        // groups per thread per chunk
+    float pre[kU][4];
+    const bool vec4 = (D & 3) == 0;
+    auto load = [&](int k0) {
+        const int kc = min(kDmKC, kend - k0);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int e = tid + 256 * u, r = e / kG, c0 = (e % kG) * 4;
+            const float* src = Xl + (size_t)r * D + k0 + c0;
+            const bool live = r < n && e < np * kG;
+            if (live && vec4 && c0 + 4 <= kc) {
+                const float4 v = *(const float4*)src;
+                pre[u][0] = v.x, pre[u][1] = v.y, pre[u][2] = v.z, pre[u][3] = v.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pre[u][q] = (live && c0 + q < kc) ? src[q] : 0.0f;
+            }
+        }
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int e = tid + 256 * u, r = e / kG, c0 = (e % kG) * 4;
+            if (e < np * kG)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) xs[buf][r][c0 + q] = pre[u][q];
+        }
+    };
+    load(kbeg);
+    stage(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += kDmKC, buf ^= 1) {
+        const bool more = k0 + kDmKC < kend;
+        if (more) load(k0 + kDmKC);  // global loads in flight under this chunk's MFMAs
+        if (tid < n) {
+#pragma unroll 8
+            for (int c = 0; c < kDmKC; ++c) {  // zero padding adds exact zeros
+                const double v = (double)xs[buf][tid][c];
+                nacc = fma(v, v, nacc);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < kDmKC; ks += 4) {
+            const int k = ks + (lane >> 4);
+#pragma unroll
+            for (int u = 0; u < kGlMB; ++u)
+                if (u < nw) {
+                    const double av = (double)xs[buf][bi[u] * 16 + (lane & 15)][k];
+                    const double bv = (double)xs[buf][bj[u] * 16 + (lane & 15)][k];
+                    acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+                }
+        }
+        if (more) stage(buf ^ 1);  // the other buffer: its last readers passed the previous barrier
+        __syncthreads();
+    }
+    const size_t zo = (size_t)l * S + z;
+    double* G = gpart + zo * n * n;
+    // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+    for (int u = 0; u < kGlMB; ++u)
+        if (u < nw)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = bi[u] * 16 + (lane >> 4) + 4 * r, j = bj[u] * 16 + (lane & 15);
+                if (i < n && j < n && i < j) G[(size_t)i * n + j] = acc[u][r];
+            }
+    if (tid < n) npart[zo * n + tid] = nacc;
+}
+
 // the K slices of k_distance_mfma<..., SPLIT>: fixed-order sums, then the same epilogue
 template <typename T, int METRIC = 0>
 __global__ __launch_bounds__(256) void k_distance_combine(const double* __restrict__ gpart, const double* __restrict__ npart, int S, int n,

@@ -60,7 +60,7 @@ constexpr int kParW = kParT / 64;
 #endif
 constexpr uint32_t kFrontLog = TDA_PAR_LOG;          // front log entries (live + cancelled)
 #ifndef TDA_PAR_IDX  // build-time A/B knob (tools/): front index slots per log entry
-#define TDA_PAR_IDX 1
+#define TDA_PAR_IDX 2
 #endif
 constexpr uint32_t kFrontIdx = TDA_PAR_LOG * TDA_PAR_IDX;  // front index slots (kFrontIdx / 8 buckets x 8)
 constexpr uint32_t kFrontLive = TDA_PAR_LOG * 7 / 16;  // live front keys that trigger a spill (1792 at 4096)
