@@ -267,10 +267,11 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         // diagram) are the same in a single call, a batch and every multi-GPU shard.
         const bool mfma = !p.is_dist && (test_env_is("TDA_DIST", "mfma") || (p.D >= kDistMfmaMinD && !test_env_is("TDA_DIST", "scalar")));
         if (mfma && p.dtype == TDA_F32 && N <= (uint64_t)kGlMaxN && !test_env_is("TDA_DIST", "tiles")) {
-            // whole-layer Gram (k_gram_layer): K slices so that ~256 workgroups run a 32-layer
-            // sweep, at least 16 chunks each -- again from (N, D) only
+            // whole-layer Gram (k_gram_layer): K slices so that a 32-layer sweep runs two
+            // workgroups per CU (512), at least 8 chunks each -- again from (N, D) only.
+            // raw4096: 16 slices 94 us + combine 26 us; 8: 130 + 15; 32: 101 + 35 (r03)
             const uint64_t chunks = ((uint64_t)p.D + kDmKC - 1) / kDmKC;
-            uint64_t sp = std::min<uint64_t>(8, std::max<uint64_t>(1, chunks / 16));
+            uint64_t sp = std::min<uint64_t>(16, std::max<uint64_t>(1, chunks / 8));
             if (const char* e = test_env("TDA_DIST_SPLIT")) sp = std::max(1, atoi(e));
             p.dsplit = (int)sp;
             p.gram_layer = true;
