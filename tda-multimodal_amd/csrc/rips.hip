@@ -849,7 +849,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             else
                 hipLaunchKernelGGL((k_distance_mfma<float, 0, true>), gsplit, dim3(256), 0, s, (const float*)x, n, (int)p.D, dist, rowmax,
                                    gpart, npart);
-            MARK("k_distance_mfma");  // the Gram kernel alone (bench roofline): combine and row maxima are their own stages
+            MARK(p.gram_layer ? "k_gram_layer" : "k_distance_mfma");  // the Gram kernel alone (bench roofline): combine, row maxima: own stages
             hipLaunchKernelGGL((k_distance_combine<float, 0>), gcomb, dim3(256), 0, s, gpart, npart, p.dsplit, n, dist, rowmax);
             MARK("k_distance_combine");
             hipLaunchKernelGGL(k_rowmax, dim3((n + 3) / 4, L), dim3(256), 0, s, dist, n, rowmax);
@@ -966,10 +966,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             if (int rc = tm4.mark("k_silhouette")) return rc;
         }
         if (want_tn) {  // TwoNN intrinsic dimension on the same distance matrices
+            // beside H0 on the ranks stream when there are no ranks (the raw-activation sweeps:
+            // H0 and TwoNN only read the distances; r03 raw4096: they ran back to back on s4)
+            const bool tn_s2 = !p.dense;
             const int pw2 = (int)next_pow2((uint64_t)std::max(n, 64));
-            hipLaunchKernelGGL(k_twonn, dim3(L), dim3(kTnT), (size_t)pw2 * 4, s4, dist, n, a.twonn_discard, a.twonn_eps, pw2, w.htn_dev);
+            hipLaunchKernelGGL(k_twonn, dim3(L), dim3(kTnT), (size_t)pw2 * 4, tn_s2 ? s2 : s4, dist, n, a.twonn_discard, a.twonn_eps, pw2,
+                               w.htn_dev);
             HIPC(hipGetLastError());
-            if (int rc = tm4.mark("k_twonn")) return rc;
+            if (int rc = (tn_s2 ? tm2 : tm4).mark("k_twonn")) return rc;
         }
         if (nls || want_tn) HIPC(hipEventRecord(w.evsil, s4));
         if (p.dense) {  // triangle ranks for the dense H1 chain, off the critical path
@@ -1316,7 +1320,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipStreamWaitEvent(s, w.evj, 0));
     }
 
-    if (nls || want_tn) HIPC(hipStreamWaitEvent(s, w.evsil, 0));  // join: silhouette scores, TwoNN
+    if (nls || want_tn) HIPC(hipStreamWaitEvent(s, w.evsil, 0));  // join: silhouette scores, TwoNN on s4
+    if (want_tn) HIPC(hipStreamWaitEvent(s, w.evj, 0));          // join: TwoNN on s2
     // ---- emission order, straight into host-mapped memory
     hipLaunchKernelGGL(k_emit, dim3(L), dim3(1024), kEmitLds, s, stats, L, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
                        (uint32_t*)(B + p.o_fv), p.sstride, w.houtoff_dev, w.hout_dev, (uint64_t)w.hout_cap, w.hstats_dev);
