@@ -406,6 +406,8 @@ def main():
             "cpu_baseline": None,
         }
         if prim:
+            if prim.get("roofline_mfma"):
+                out["roofline_mfma"] = prim["roofline_mfma"]
             out["device_ms_per_step"] = prim["device_ms_per_step"]
             out["stages_ms"] = prim["stages_ms"]
             out["pipeline"] = prim["pipeline"]
