@@ -1102,8 +1102,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // capture order of the launches (the graph executor dispatches in it):
     // TDA_ORDER=0 apparent<1> first; 1 side streams first; 2 side streams
     // first and the H2 branch after the triangle ranks; 3 side streams first,
-    // sort<1> enqueued before the H2 branch
-    const int order = test_env("TDA_ORDER") ? atoi(test_env("TDA_ORDER")) : 3;  // 3: measured best (r01)
+    // sort<1> enqueued before the H2 branch; 5 (N <= 64 with H2) as 3, with
+    // apparent<1> at the head of the H2 branch's stream: sweep48 0.182 ->
+    // 0.175 ms device, L = 4 0.136 -> 0.131 ms (replayed graph; eager slower)
+    const int order = test_env("TDA_ORDER") ? atoi(test_env("TDA_ORDER")) : 5;  // 5: measured best (r03; 3 in r01-r02)
     if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
     const bool h2_side = !p.dense && p.par && p.par2 && p.maxdim >= 2;
@@ -1145,13 +1147,41 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipGetLastError());
         return 0;
     };
-    if (p.maxdim >= 1) {
-        launch_apparent(1, s);
+    // order 5 (N <= 64, H0-H2): apparent<1> opens the H2 branch's stream (its pivot
+    // bitmap is apparent<2>'s clearing test), so the branch runs on one queue up to
+    // phase 1; the main stream picks up apparent<1>'s residuals for sort<1> and the chain
+    const bool app1_side = split2 && order == 5 && !serial_stages;
+    if (p.maxdim >= 1 && app1_side) {
+        HIPC(hipStreamWaitEvent(w.stream3, w.evf, 0));
+        if (int rc = tm3.begin()) return rc;
+        launch_apparent(1, w.stream3);
         HIPC(hipGetLastError());
-        MARK("k_apparent<1>");
+        if (int rc = tm3.mark("k_apparent<1>")) return rc;
+        HIPC(hipEventRecord(w.evs, w.stream3));
+        launch_apparent(2, w.stream3);
+        HIPC(hipGetLastError());
+        if (int rc = tm3.mark("k_apparent<2>")) return rc;
+        launch_sort(2, 1, w.stream3, 16384);
+        HIPC(hipGetLastError());
+        if (int rc = tm3.mark("k_sort_resid<2>")) return rc;
+        HIPC(hipStreamWaitEvent(w.stream3, w.evj, 0));  // edge classes (k_prep_*)
+        if (int rc = launch_phase1(w.stream3)) return rc;
+        HIPC(hipStreamWaitEvent(s, w.evs, 0));
+        launch_sort(1, 1, s);
+        HIPC(hipGetLastError());
+        MARK("k_sort_resid<1>");
+    }
+    if (p.maxdim >= 1) {
+        if (!app1_side) {
+            launch_apparent(1, s);
+            HIPC(hipGetLastError());
+            MARK("k_apparent<1>");
+        }
         if (order == 0)
             if (int rc = launch_side()) return rc;
-        if (split2) {
+        if (app1_side) {
+            // enqueued above
+        } else if (split2) {
             HIPC(hipEventRecord(w.evs, s));
             if (order == 3) {
                 launch_sort(1, 1, s);
