@@ -1105,7 +1105,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // sort<1> enqueued before the H2 branch; 5 (N <= 64 with H2) as 3, with
     // apparent<1> at the head of the H2 branch's stream: sweep48 0.182 ->
     // 0.175 ms device, L = 4 0.136 -> 0.131 ms (replayed graph; eager slower)
-    const int order = test_env("TDA_ORDER") ? atoi(test_env("TDA_ORDER")) : 5;  // 5: measured best (r03; 3 in r01-r02)
+    // 5 up to 64 layers per call; 3 above (sweep48x4, 128 layers: 0.42 vs 0.48 ms with 5)
+    const int order = test_env("TDA_ORDER") ? atoi(test_env("TDA_ORDER")) : (L <= 64 ? 5 : 3);
     if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
     const bool h2_side = !p.dense && p.par && p.par2 && p.maxdim >= 2;
