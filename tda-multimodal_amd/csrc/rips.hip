@@ -1493,6 +1493,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)tt, (unsigned long long)sc, (unsigned long long)cb, (unsigned long long)ad, (unsigned long long)mx,
                 (unsigned long long)mxa);
     }
+    if (n > kSmallN) {
+        const uint64_t* h = w.hstats[0].prof[0];
+        fprintf(stderr, "[tda-prof] k_h0 layer 0 (cycles from entry): staged %llu, thresh+edges %llu, forest %llu, sort %llu, end %llu\n",
+                (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
+                (unsigned long long)h[4]);
+    }
     if (p.par) {
         const uint64_t* q = w.hstats[0].prof[2];
         fprintf(stderr, "[tda-prof] k_reduce_par longest column: %llu steps, %llu cycles: front_min %llu, pivot+rows %llu, apparent adds %llu, refills %llu (%llu), owner path %llu; avg front log %llu, compactions %llu, spills %llu\n",

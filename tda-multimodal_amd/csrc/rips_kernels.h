@@ -880,10 +880,17 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     uint64_t* sk = red + 40;                              // sort chunk
     const int nw = T >> 6, w = t >> 6, ln = t & 63;
     float* Ds = (float*)(sk + (1ull << sort_log2));       // dlds: the layer's matrix
+#ifdef TDA_PROFILE
+    const uint64_t h0t0 = clock64();
+#define H0M(i) if (t == 0 && l == 0) st->prof[0][i] = clock64() - h0t0;
+#else
+#define H0M(i)
+#endif
     if (dlds) {
         stage_to_lds(Ds, Dl, 4ull * n * n, t, T);
         __syncthreads();
     }
+    H0M(0)
 
     uint64_t* mst = scratch + (size_t)l * 2 * n;  // MST edge keys
     int nmst = 0;
@@ -930,6 +937,7 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
     (void)s_cur;
     (void)best;
     (void)thr;
+    H0M(1)
     if constexpr (wave && LROWS) {
         // Borůvka on the whole workgroup over the LDS-staged rows (r03; the
         // one-wave Prim it replaces took N - 1 dependent steps: 32 x N=144
@@ -1051,8 +1059,10 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         __syncthreads();
         nmst = (int)red[34];
     }
+    H0M(2)
     // -- Kruskal order of the forest edges
     block_sort<false>(mst, nullptr, (uint64_t)nmst, mst + n, nullptr, sk, nullptr, sort_log2);
+    H0M(3)
     for (int e = t; e < nmst; e += T) {
         uint64_t eidx = 0xFFFFFFFFull - (mst[e] & 0xFFFFFFFFull);
         atomicOr(&mst_bits[(size_t)l * mst_words + (eidx >> 5)], 1u << (eidx & 31));
@@ -1186,6 +1196,8 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         st->all_pairs[0] = nmst;
         st->n_columns[0] = n;
     }
+    H0M(4)
+#undef H0M
 }
 
 // Small-N H0 (N <= 64): one wave per layer, distance matrix in LDS, lane v
