@@ -323,6 +323,15 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) { TDA_WAVE_REDUCE64
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) { TDA_WAVE_REDUCE64(op_min64, ~0ull) }
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) { TDA_WAVE_REDUCE64(op_max64, 0ull) }
 #undef TDA_WAVE_REDUCE64
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, dpp32<0x111, 0xf>(0u, v));
+    v = max(v, dpp32<0x112, 0xf>(0u, v));
+    v = max(v, dpp32<0x114, 0xf>(0u, v));
+    v = max(v, dpp32<0x118, 0xf>(0u, v));
+    v = max(v, dpp32<0x142, 0xa>(0u, v));
+    v = max(v, dpp32<0x143, 0xc>(0u, v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     v = min(v, dpp32<0x111, 0xf>(~0u, v));
     v = min(v, dpp32<0x112, 0xf>(~0u, v));

@@ -900,10 +900,9 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
         if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) {
             float local = INFINITY;
             for (int i = w; i < n; i += nw) {
-                float r = -INFINITY;
+                float r = 0.0f;  // distances are >= 0 (the diagonal is 0): the bits order like the values
                 for (int j = ln; j < n; j += 64) r = fmaxf(r, dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]);
-                for (int m = 32; m >= 1; m >>= 1) r = fmaxf(r, __shfl_xor(r, m, 64));
-                local = fminf(local, r);
+                local = fminf(local, __uint_as_float(wave_max_u32(__float_as_uint(r))));  // DPP, no LDS round trips
             }
             if (ln == 0) ((float*)red)[w] = local;
             __syncthreads();
@@ -922,7 +921,8 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
             unsigned long long c = 0;
             for (int i = w; i < n; i += nw)
                 for (int j = i + 1 + ln; j < n; j += 64) c += (dlds ? ld_lds(Ds, (size_t)i * n + j) : Dl[(size_t)i * n + j]) <= thr;
-            atomicAdd(&s_cnt, c);
+            c = wave_sum_u64(c);  // one LDS atomic per wave, not per thread
+            if (ln == 0) atomicAdd(&s_cnt, c);
         }
         __syncthreads();
         if (t == 0) {

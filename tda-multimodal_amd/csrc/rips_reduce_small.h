@@ -63,7 +63,6 @@ __device__ __forceinline__ void edge_verts(uint32_t q, int& a, int& b) {
     a = x;
     b = (int)(q - c2u(x));
 }
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return (uint32_t)wave_max_u64((uint64_t)v); }
 // set bits of M above bit v
 __device__ __forceinline__ uint32_t bits_above(uint64_t M, int v) { return v >= 63 ? 0u : (uint32_t)__popcll(M >> (v + 1)); }
 // bit position of the k-th highest set bit of M (k = 0: the highest), one lane
