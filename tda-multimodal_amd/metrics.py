@@ -72,7 +72,9 @@ def compute_intrinsic_dimensionality(data, discard_fraction: float = 0.1, eps: f
 
     The distances are the hot path's (sklearn's f64-accumulated Euclidean form
     rounded to f32) where the reference uses torch.cdist in f32; estimates
-    agree within the tolerance stated in tests/test_gpu_parity.py."""
+    agree within the tolerance stated in tests/test_gpu_parity.py.  No
+    persistence is computed (TDA_FLAG_NO_PERSISTENCE).  n_samples <= 8192 (the
+    per-item ratio sort runs in LDS); the reference has no such limit."""
     is_t = _is_torch(data)
     if is_t:
         import torch
