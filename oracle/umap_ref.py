@@ -113,7 +113,8 @@ def transform_init(X_train: np.ndarray, emb: np.ndarray, Y: np.ndarray, n_neighb
     local_connectivity 0 (rho = 0; slot 0 skipped in the bisection as umap
     does), bipartite memberships without entries at >= the disconnection
     distance, then init_graph_transform (f32 weighted mean, or the
-    neighbour's own embedding at membership 1, NaN without neighbours)."""
+    neighbour's own embedding at membership 1, NaN without neighbours), over
+    each row's entries in ascending training index (graph.tocsr() order)."""
     Z = np.concatenate([np.asarray(X_train), np.asarray(Y)]).astype(np.float32)
     D = distances(Z, metric)
     N, M, k = X_train.shape[0], Y.shape[0], n_neighbors
@@ -143,11 +144,13 @@ def transform_init(X_train: np.ndarray, emb: np.ndarray, Y: np.ndarray, n_neighb
         if not nz.any():
             out[i] = np.nan
             continue
+        # graph.tocsr() row order: ascending training index
+        order = [j for j in np.argsort(idx[i], kind="stable") if nz[j]]
         rs = np.float32(0.0)
-        for v in vals[nz]:
-            rs = np.float32(rs + v)
+        for j in order:
+            rs = np.float32(rs + vals[j])
         r = np.zeros(emb.shape[1], np.float32)
-        for j in np.flatnonzero(nz):
+        for j in order:
             if vals[j] == 1.0:
                 r = emb[idx[i, j]].astype(np.float32).copy()
                 break

@@ -22,6 +22,7 @@
 #include "rips_reduce_big.h"
 #include "rips_reduce_par.h"
 #include "rips_reduce_small.h"
+#include "rips_dense.h"
 
 using namespace tda;
 
@@ -117,6 +118,9 @@ struct Plan {
     uint32_t n2p = 0;         // stride of the per-layer edge-class table (N * N rounded up)
     uint32_t bm_words = 0;    // tetrahedron membership bitmap of k_h2_phase1 (words)
     uint32_t prep_lds = 0;    // dynamic LDS of k_prep_edges
+    bool fused = false;       // N <= 48: the whole dense path in one launch (k_dense_fused, rips_dense.h)
+    uint32_t fused_lds = 0;
+    size_t o_fdone = 0, o_fout = 0, o_f1k = 0, o_f1i = 0, o_froff = 0, o_frlen = 0;
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
@@ -172,7 +176,8 @@ ReduceAllCfg reduce_cfg(int n, int maxdim, const uint64_t* piv_words, bool lds_m
 }
 
 // no_par: 0 = k_reduce_par for H1 and H2, 1 = H1 only (an H2 launch aborted), 2 = none
-int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par) {
+// no_fused: the fused dense kernel gave up on this shape (ERR_FUSED): the multi-kernel dense path
+int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par, bool no_fused) {
     const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
     p.mst_words = (binom(N, 2) + 31) / 32 + 1;
     for (int d = 1; d <= p.maxdim; ++d) {
@@ -248,6 +253,14 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
     }
+    if (p.dense && !no_fused && test_env_is("TDA_FUSED", "1") && p.N >= 4 && binom(N, 2) <= 2048) {
+        bool kok = false;
+        for (int k : kFusedKs) kok |= k == p.dK;
+        const FCarve ca = fused_carve_a((int)N, p.dK, p.tri_stride, p.inv_stride, (uint32_t)p.piv_words[1]);
+        const FCarve cb = fused_carve_b((int)N, (uint32_t)p.piv_words[1]);
+        p.fused_lds = std::max<uint32_t>(ca.endA, p.maxdim >= 2 ? cb.endB : 0u);
+        p.fused = kok && p.fused_lds <= (uint32_t)kLdsMax;
+    }
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
     p.sstride = 3 * maxp;
@@ -302,6 +315,10 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     if (p.dense) {
         p.o_res1 = take(L * p.piv_words[1] * 4);
         p.o_necnt = take(L * 4);
+    }
+    if (p.fused) {
+        p.o_fdone = take(L * 4);
+        p.o_fout = take(8);
     }
     p.memset_hi = o;
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
@@ -374,6 +391,12 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
                 p.o_rof = take(L * (uint64_t)p.tri_stride * 2);
             }
             if (p.cmode == kChainTable) p.o_cobt = take(L * (uint64_t)p.cob_stride * 2);
+            if (p.fused && p.maxdim >= 2) {
+                p.o_f1k = take(L * kF2Cap * 4);
+                p.o_f1i = take(L * kF2Cap * 4);
+                p.o_froff = take(L * kF2Cap * 4);
+                p.o_frlen = take(L * kF2Cap * 4);
+            }
             if (p.maxdim >= 2) {
                 p.o_p1k = take(L * p.rcap[2] * 8);
                 p.o_p1i = take(L * p.rcap[2] * 4);
@@ -442,6 +465,7 @@ struct Workspace {
         bool force_global, force_big;
         int no_par;
         int scale;
+        bool no_fused;
     };
     std::vector<Retry> retry;
     std::mutex mu;
@@ -497,7 +521,20 @@ struct StageTimer {
 };
 
 std::mutex g_ws_mu;
-std::mutex g_capture_mu;  // graph capture + instantiation
+// Graph capture + instantiation AND every workspace (re)allocation / free, across
+// all slots of the process.  r03 saw a host segfault inside the first calls of
+// two slots that ran concurrently; the cause was not isolated then.  The HIP
+// calls those first calls made at the same time were: hipFuncSetAttribute
+// (one-time, now under g_attr_mu), stream capture + hipGraphInstantiate on
+// the two slots' streams, and hipMalloc / hipHostMalloc of the workspaces --
+// and on growth hipFree / hipHostFree / hipGraphExecDestroy.  ThreadLocal
+// capture only restricts the CAPTURING thread, and HIP's hipFree synchronises
+// the whole device (all streams, a capturing one included) while another
+// thread captures; it is the one call whose contract does not cover running
+// beside a capture.  So no (re)allocation, free or graph destruction runs
+// while any slot captures: they take this lock too (first call / growth only;
+// replays never take it).
+std::mutex g_capture_mu;
 std::vector<Workspace*> g_ws;
 
 Workspace* get_ws(int dev, int slot) {
@@ -626,6 +663,9 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_prep_edges, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_prep_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)prep_tables_lds(kDenseMaxN)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+#define TDA_ATTR_FUSED(K) HIPC(hipFuncSetAttribute((const void*)k_dense_fused<K>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+    TDA_ATTR_FUSED(1) TDA_ATTR_FUSED(2) TDA_ATTR_FUSED(3) TDA_ATTR_FUSED(4) TDA_ATTR_FUSED(6) TDA_ATTR_FUSED(9)
+#undef TDA_ATTR_FUSED
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -663,7 +703,7 @@ std::string err_flags(int e) {
 // ------------------------------------------------------------------ pipeline
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
-                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0) {
+                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0, bool no_fused = false) {
     const auto h_entry = std::chrono::steady_clock::now();
     Plan p;
     p.L = a.L;
@@ -673,11 +713,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     p.dtype = a.dtype;
     p.is_dist = input_kind != 0;
     p.want64 = input_kind == 0 && a.dtype == TDA_F64 && a.want_dist && (a.flags & TDA_FLAG_DIST64);
-    make_plan(p, force_global, scale, force_big, no_par);
+    make_plan(p, force_global, scale, force_big, no_par, no_fused);
     const int dev = a.device;
     HIPC(hipSetDevice(dev));
     Workspace& w = *get_ws(dev, a.slot);
     std::unique_lock<std::mutex> guard(w.mu);  // released before any retry (which re-enters)
+    // allocations (first call / growth) never overlap another slot's capture
+    std::unique_lock<std::mutex> rt_lock(g_capture_mu);
     if (int rc = ws_prepare(w, p)) return rc;
     if (int rc = set_lds_attrs(dev)) return rc;
     // all work runs on the library stream, ordered after the caller's stream
@@ -758,6 +800,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         w.htn_cap = std::max(L, 64);
     }
 
+    rt_lock.unlock();  // host buffers are in place; the capture below re-takes it
+
     // TDA_FLAG_STAGE_SERIAL: every stage on the main stream, so each pair of
     // events brackets one kernel only (no time spent queued behind the side
     // streams' kernels); the side streams are restored on return
@@ -793,7 +837,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.force_big = force_big;
     gk.no_par = no_par;
     gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0) |
-                 (p.wide ? 1 << 10 : 0);
+                 (p.wide ? 1 << 10 : 0) | (p.want64 ? 1 << 11 : 0) | (p.fused ? 1 << 12 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
     gk.sil_K = sil_K;  // baked into the k_silhouette launch (argument K and its LDS size)
@@ -887,6 +931,81 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     MARK(input_kind != 0 ? "k_square_dist" : dist_mfma ? ((p.dsplit > 1 || p.gram_layer) && p.dtype == TDA_F32 ? "k_rowmax" : "k_distance_mfma") : "k_distance");
     HIPC(hipEventRecord(w.evf, s));  // fork point of the side streams
 
+    if (p.fused) {  // N <= 48: everything after the distances in one launch (rips_dense.h)
+        if (nls || want_tn) {  // silhouettes / TwoNN read the same matrices, beside it
+            hipStream_t s4 = w.stream4;
+            HIPC(hipStreamWaitEvent(s4, w.evf, 0));
+            if (int rc = tm4.begin()) return rc;
+            if (nls) {
+                const size_t lds = (size_t)sil_K * kSilT * 8 + (size_t)n * 4;
+                hipLaunchKernelGGL(k_silhouette, dim3(L, nls), dim3(kSilT), lds, s4, dist, n, (const int32_t*)w.hsil_dev, sil_K,
+                                   (double*)(w.hsil_dev + sil_out_off));
+                HIPC(hipGetLastError());
+                if (int rc = tm4.mark("k_silhouette")) return rc;
+            }
+            if (want_tn) {
+                const int pw2 = (int)next_pow2((uint64_t)std::max(n, 64));
+                hipLaunchKernelGGL(k_twonn, dim3(L), dim3(kTnT), (size_t)pw2 * 4, s4, dist, n, a.twonn_discard, a.twonn_eps, pw2, w.htn_dev);
+                HIPC(hipGetLastError());
+                if (int rc = tm4.mark("k_twonn")) return rc;
+            }
+            HIPC(hipEventRecord(w.evsil, s4));
+        }
+        FusedBufs fb = {};
+        fb.dist = dist;
+        fb.rowmax = rowmax;
+        fb.user_thresh = a.thresh;
+        fb.stats = stats;
+        for (int d = 0; d < 3; ++d) {
+            fb.pairs[d] = ps.p[std::min(d, p.maxdim)];
+            fb.pcap[d] = ps.cap[std::min(d, p.maxdim)];
+        }
+        fb.res1 = (uint32_t*)(B + p.o_res1);
+        fb.res1_words = p.piv_words[1];
+        fb.clsg = (uint32_t*)(B + p.o_cls);
+        fb.pool1 = (uint32_t*)(B + p.o_vpool);
+        fb.pool1_words = 2ull * p.vpool_cap;
+        fb.done = (uint32_t*)(B + p.o_fdone);
+        if (p.maxdim >= 2) {
+            fb.p1_key = (uint32_t*)(B + p.o_f1k);
+            fb.p1_info = (uint32_t*)(B + p.o_f1i);
+            fb.roff2 = (uint32_t*)(B + p.o_froff);
+            fb.rlen2 = (uint32_t*)(B + p.o_frlen);
+            fb.rpool2 = (uint64_t*)(B + p.o_rpool2);
+            fb.rpool2_cap = p.vpool_cap;
+        }
+        fb.out_used = (unsigned long long*)(B + p.o_fout);
+        fb.hout = w.hout_dev;
+        fb.hout_cap = w.hout_cap;
+        fb.houtoff = w.houtoff_dev;
+        fb.hstats = w.hstats_dev;
+        fb.step_limit = step_limit();
+        fb.tri_stride = p.tri_stride;
+        fb.inv_stride = p.inv_stride;
+        fb.piv_words1 = (uint32_t)p.piv_words[1];
+        // one workgroup per CU (LDS): B(l) spins on A(l), so a chunk keeps both roles resident
+        const int chunk = p.maxdim >= 2 ? 128 : 256;
+        for (int l0 = 0; l0 < L; l0 += chunk) {
+            const int Lc = std::min(chunk, L - l0), L8 = (Lc + 7) & ~7;
+            const unsigned grid = p.maxdim >= 2 ? (unsigned)(2 * L8) : (unsigned)Lc;
+            switch (p.dK) {
+#define TDA_FUSED(K)                                                                                                    \
+    case K:                                                                                                             \
+        hipLaunchKernelGGL(k_dense_fused<K>, dim3(grid), dim3(kFT), p.fused_lds, s, fb, n, p.maxdim, l0, Lc, L8); \
+        break;
+                TDA_FUSED(1) TDA_FUSED(2) TDA_FUSED(3) TDA_FUSED(4) TDA_FUSED(6) TDA_FUSED(9)
+#undef TDA_FUSED
+                default:
+                    return fail(TDA_E_INVALID, "no k_dense_fused instantiation for this N");
+            }
+            HIPC(hipGetLastError());
+        }
+        MARK("k_dense_fused");
+        if (nls || want_tn) HIPC(hipStreamWaitEvent(s, w.evsil, 0));
+        HIPC(rec_t(w.ev1));
+        return 0;
+    }
+
     DenseBufs dnb = {};
 
     // ---- H0 on its own stream: it overlaps the apparent-pair kernels, which
@@ -968,7 +1087,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         if (want_tn) {  // TwoNN intrinsic dimension on the same distance matrices
             // beside H0 on the ranks stream when there are no ranks (the raw-activation sweeps:
             // H0 and TwoNN only read the distances; r03 raw4096: they ran back to back on s4)
-            const bool tn_s2 = !p.dense;
+            // (only without H1: with H1 the main stream joins s2 before the reduction, and
+            // TwoNN there would sit on the critical path -- ADVICE r03)
+            const bool tn_s2 = !p.dense && p.maxdim == 0;
             const int pw2 = (int)next_pow2((uint64_t)std::max(n, 64));
             hipLaunchKernelGGL(k_twonn, dim3(L), dim3(kTnT), (size_t)pw2 * 4, tn_s2 ? s2 : s4, dist, n, a.twonn_discard, a.twonn_eps, pw2,
                                w.htn_dev);
@@ -1406,7 +1527,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         size_t need = 0;
         for (int l = 0; l < L; ++l)
             for (int d = 0; d <= p.maxdim; ++d) need += (size_t)std::min<uint64_t>(w.hstats[l].count[d], p.pcap[d]);
-        if (int rc = grow_hout(w, need + 16)) return rc;
+        {
+            std::lock_guard<std::mutex> g(g_capture_mu);
+            if (int rc = grow_hout(w, need + 16)) return rc;
+        }
         for (int l = 0; l < L; ++l) w.hstats[l].err = 0;
         HIPC(hipMemcpyAsync(stats, w.hstats, sizeof(LayerStats) * L, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_emit, dim3(L), dim3(1024), kEmitLds, s, stats, L, p.maxdim, ps, (uint64_t*)(B + p.o_fk),
@@ -1434,29 +1558,34 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         const bool capacity = code == 21 || code == 22 || code == 41 || code == 53;  // pools / requeue slots
         if (capacity && scale < 2) {  // the same parallel reduction with larger pools
             guard.unlock();
-            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par);
+            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par, no_fused);
         }
         if (test_env_is("TDA_PAR_STRICT", "1"))  // tests: the parallel path itself must succeed
             return fail(TDA_E_CAPACITY, "k_reduce_par aborted: item " + std::to_string(c.err >> 16) + " code " +
                                             std::to_string(code));
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, np_next);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, np_next, no_fused);
+    }
+    if (p.fused && (errs & (ERR_FUSED | ERR_LDS_SPILL | ERR_VPOOL_CAP | ERR_STEP_LIMIT))) {
+        // the fused dense kernel gave up (LDS lists, spin limit, pools): the multi-kernel dense path
+        guard.unlock();
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, no_par, true);
     }
     if ((errs & ERR_LDS_SPILL) && !force_global) {
         // a working column outgrew LDS: redo the batch with global-memory tables
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par, no_fused);
     }
     if ((errs & ERR_WORK_CAP) && !p.big && !test_env_is("TDA_REDUCE", "wave")) {
         // a working column outgrew the one-wave HBM tables: full scans of a
         // large column are the slow case, so switch to the radix-heap kernel
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true, no_par);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true, no_par, no_fused);
     }
     if ((errs & ~(ERR_LDS_SPILL)) == (errs & (ERR_WORK_CAP | ERR_VPOOL_CAP)) && errs && scale < 2) {
         // working column / reduced-column pool too small: retry with larger buffers
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par, no_fused);
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
 #ifdef TDA_PROFILE
@@ -1541,7 +1670,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 #endif
 
-    if (force_global || scale || force_big || no_par) {  // remember what this shape needed
+    if (force_global || scale || force_big || no_par || no_fused) {  // remember what this shape needed
         bool seen = false;
         for (auto& m : w.retry)
             if (m.N == p.N && m.maxdim == p.maxdim && m.input_kind == input_kind) {
@@ -1549,9 +1678,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 m.force_big = m.force_big || force_big;
                 m.no_par = std::max(m.no_par, no_par);
                 m.scale = std::max(m.scale, scale);
+                m.no_fused = m.no_fused || no_fused;
                 seen = true;
             }
-        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale});
+        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale, no_fused});
     }
 
     // ---- result
@@ -1590,12 +1720,23 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             m_add[l * nd + d] = st.n_adds[d];
         }
     }
-    for (size_t e = 0; e < total; ++e) {
-        const OutPair q = w.hout[e];
-        r_bd[e] = q.birth;
-        r_bd[total + e] = q.death;
-        r_idx[e] = q.birth_idx;
-        r_idx[total + e] = q.death_idx;
+    // layer-major result (tda_rips.h); the device wrote each (layer, dim) segment
+    // at houtoff, in layer order (k_emit) or in completion order (k_dense_fused)
+    {
+        size_t e = 0;
+        for (int l = 0; l < L; ++l)
+            for (int d = 0; d < nd; ++d) {
+                const size_t src = (size_t)w.houtoff[l * nd + d];
+                const size_t c = (size_t)m_count[l * nd + d];
+                m_off[l * nd + d] = (int64_t)e;
+                for (size_t i = 0; i < c; ++i, ++e) {
+                    const OutPair q = w.hout[src + i];
+                    r_bd[e] = q.birth;
+                    r_bd[total + e] = q.death;
+                    r_idx[e] = q.birth_idx;
+                    r_idx[total + e] = q.death_idx;
+                }
+            }
     }
     if (a.want_dist) {
         R->dist.resize((size_t)L * n * n);
@@ -1691,7 +1832,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 
 // entry: start from the configuration an earlier call of this shape ended on
 int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_result** out) {
-    bool fg = false, fb = false;
+    bool fg = false, fb = false, nf = false;
     int np = 0;
     int sc = 0;
     // not when a test forces a reducer (the memo would override what it asks for)
@@ -1705,9 +1846,10 @@ int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_
                 fb = m.force_big;
                 np = m.no_par;
                 sc = m.scale;
+                nf = m.no_fused;
             }
     }
-    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np);
+    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np, nf);
 }
 
 int validate(const tda_rips_args* a) {

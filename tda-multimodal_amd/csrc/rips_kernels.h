@@ -156,8 +156,15 @@ __global__ __launch_bounds__(256) void k_distance(const T* __restrict__ X, int n
 // slot 2r + k mod 32), so the ds_read_b64 is conflict-free; each thread
 // stages 4 consecutive k of one row (coalesced global reads, 16-B aligned
 // LDS writes).
-// The squared norms accumulate (sequential k, FMA: the oracle's order) in the
-// same pass from the LDS tile, threads 0-63 for the i rows, 64-127 for j.
+// The squared norms accumulate in the same pass from the LDS tiles, in a
+// fixed but NOT sequential order: each row's K chunks are split into two k
+// halves summed by different threads in a lane-rotated k order, then added
+// (k_gram_layer, N <= 144: sequential k within each K slice, slices added in
+// slice order by k_distance_combine).  So at D >= 32 a few distances differ
+// from the oracle's sequential-k f32 rounding (and between the N <= 144 and
+// N > 144 kernels) by an ulp: parity there is tolerance-based (1e-5, the
+// north_star bound; tests/test_gpu_parity.py test_distance_high_dim_vs_sklearn),
+// pair indices are exact only where no two distances swap order.
 #ifndef TDA_DM_KC  // build-time A/B knob (tools/): K chunk of k_distance_mfma
 #define TDA_DM_KC 32
 #endif
@@ -1204,18 +1211,13 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
 // owns vertex v; Prim's frontier keys live in registers, the arg-min vertex is
 // found by ballot (no index decode); the <= 63 forest edges are sorted with an
 // in-register bitonic network.  Same results as k_h0.
-__global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
-                                                float user_thresh, LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
-                                                uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, v = threadIdx.x;
-    // enclosing radius = min over rows of the row maxima k_distance folded in
-    const uint32_t rmv = v < n ? ld_glb(rowmax + (size_t)l * n, (size_t)v) : 0xFFFFFFFFu;
-    float* D = (float*)smem;              // n*n
-    const float* Dg = dist + (size_t)l * n * n;
-    stage_to_lds(D, Dg, sizeof(float) * n * n, v, 64);
-    __syncthreads();
-    LayerStats* st = stats + l;
+// The body is shared with the fused dense kernel (rips_dense.h), which runs it
+// on one wave of its workgroup: D is the layer's matrix in LDS, thr the
+// resolved threshold; forest edges go to mst_bits (LDS when MST_LDS, else
+// HBM, per-layer pointer), H0 pairs to P, the H0 stats to st.
+template <bool MST_LDS>
+__device__ __forceinline__ void h0_wave_body(const float* D, int n, float thr, LayerStats* st, uint32_t* mst_bits, Pair* P) {
+    const int v = lane_id();
     const bool real = v < n;
 #ifdef TDA_PROFILE
     const uint64_t tp0 = clock64();
@@ -1225,8 +1227,6 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
 #define TDA_H0_MARK(i)
 #endif
     TDA_H0_MARK(0)
-    float thr = user_thresh;
-    if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) thr = n == 1 ? 0.0f : __uint_as_float(wave_min_u32(rmv));
     // D is symmetric: lane v counts column v below the diagonal, 8 loads in flight
     uint64_t ne = 0;
     if (real)
@@ -1300,7 +1300,7 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
     if (has) {
         ea = max_vertex(eidx, 2, n - 1);
         eb = (int)(eidx - binom((uint64_t)ea, 2));
-        atomicOr(&mst_bits[(size_t)l * mst_words + (eidx >> 5)], 1u << (eidx & 31));
+        matomic_or<MST_LDS>(&mst_bits[eidx >> 5], 1u << (eidx & 31));
     }
     // elder-rule union-find in registers: lane u holds the label (= max
     // vertex) of its component; each merge is two readlanes + a select.
@@ -1315,7 +1315,6 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
     }
     TDA_H0_MARK(4)
     // emission: finite bars (d > 0) in Kruskal order, then [0, inf) per root
-    Pair* P = pairs0 + (size_t)l * pcap0;
     const uint64_t posm = __ballot(has && d > 0.0f);
     const int nfin = __popcll(posm);
     if (has && d > 0.0f) P[lanes_below(posm)] = Pair{0.0f, d, (int64_t)young_e, (int64_t)eidx};
@@ -1332,6 +1331,22 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
     }
     TDA_H0_MARK(5)
 #undef TDA_H0_MARK
+}
+
+__global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
+                                                float user_thresh, LayerStats* __restrict__ stats, uint32_t* __restrict__ mst_bits,
+                                                uint64_t mst_words, Pair* __restrict__ pairs0, uint64_t pcap0) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, v = threadIdx.x;
+    // enclosing radius = min over rows of the row maxima k_distance folded in
+    const uint32_t rmv = v < n ? ld_glb(rowmax + (size_t)l * n, (size_t)v) : 0xFFFFFFFFu;
+    float* D = (float*)smem;              // n*n
+    const float* Dg = dist + (size_t)l * n * n;
+    stage_to_lds(D, Dg, sizeof(float) * n * n, v, 64);
+    __syncthreads();
+    float thr = user_thresh;
+    if (isinf(user_thresh) || user_thresh == 3.402823466e+38f) thr = n == 1 ? 0.0f : __uint_as_float(wave_min_u32(rmv));
+    h0_wave_body<false>(D, n, thr, stats + l, mst_bits + (size_t)l * mst_words, pairs0 + (size_t)l * pcap0);
 }
 
 // ------------------------------------------------------------------ apparent

@@ -397,99 +397,67 @@ __global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restri
 //   kChainFast (N <= ~51): rank_of[triangle] + inv32 in LDS.
 //   kChainGeneral: edge records (youngest facet, block mask) + inv16.
 // LDS: [16][D][recs E | rank_of | cobt][inv16 | inv32][W 64K][res 64K][piv][cols][own].
+// The serial chain of k_h1_chain (wave 0 after the staging), shared with the
+// fused dense kernel (rips_dense.h): every table pointer is the layer's (LDS
+// where the MODE reads it from LDS), cols holds the nc non-cleared residual
+// columns in column order, nskip the cleared ones (stats only).
+struct ChainCtx {
+    const float* Dl;
+    const EdgeRec* R;
+    const uint16_t* rof;
+    const uint16_t* cobt;
+    uint16_t* inv;
+    const uint32_t* inv32;
+    uint32_t* W;
+    uint32_t* res;
+    const uint32_t* piv;
+    const uint64_t* cols;
+    uint16_t* own;
+    const float* Dg;
+    const uint32_t* inv32g;
+    uint32_t* res1;
+    uint32_t* pool;
+    uint64_t pool_words;
+    const uint32_t* clsg;
+    Pair* P;
+    uint64_t pcap;
+    LayerStats* st;
+    int n, l;
+    uint32_t nc, nskip;
+    uint64_t step_limit;
+    uint64_t t_entry;
+};
 template <int K, int MODE>
-__global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
-                                                      DimBufs b, Reduce2Bufs rb, DenseBufs db, uint64_t step_limit,
-                                                      Pair* __restrict__ pairs, uint64_t pcap) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void h1_chain_wave(const ChainCtx& c) {
     constexpr bool FAST = MODE == kChainFast, TABLE = MODE == kChainTable, GEN = MODE == kChainGeneral;
     constexpr uint32_t WP = 64u * K;
+    const float* Dl = c.Dl;
+    const EdgeRec* R = c.R;
+    const uint16_t* rof = c.rof;
+    const uint16_t* cobt = c.cobt;
+    uint16_t* inv = c.inv;
+    const uint32_t* inv32 = c.inv32;
+    uint32_t* W = c.W;
+    uint32_t* res = c.res;
+    const uint32_t* piv = c.piv;
+    const uint64_t* cols = c.cols;
+    uint16_t* own = c.own;
+    const float* Dg = c.Dg;
+    const uint32_t* inv32g = c.inv32g;
+    uint32_t* res1 = c.res1;
+    LayerStats* st = c.st;
+    const int n = c.n, l = c.l, ln = lane_id();
+    const uint32_t nc = c.nc, nskip = c.nskip;
+    const uint64_t step_limit = c.step_limit, pcap = c.pcap;
 #ifdef TDA_PROFILE
-    const uint64_t t_entry = clock64();
+    const uint64_t t_entry = c.t_entry;
 #endif
-    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
-    LayerStats* st = stats + l;
-    const int E = n * (n - 1) / 2;
-    unsigned char* p = smem + 16;
-    auto take = [&](size_t bytes) {
-        unsigned char* q = p;
-        p += (bytes + 15) & ~(size_t)15;
-        return q;
-    };
-    float* Dl = TABLE ? nullptr : (float*)take(4ull * n * n);
-    EdgeRec* R = GEN ? (EdgeRec*)take(16ull * E) : nullptr;
-    uint16_t* rof = FAST ? (uint16_t*)take(2ull * db.tri_stride) : nullptr;
-    uint16_t* cobt = TABLE ? (uint16_t*)take(2ull * db.cob_stride) : nullptr;
-    uint16_t* inv = FAST ? nullptr : (uint16_t*)take(2ull * db.inv_stride);
-    uint32_t* inv32 = FAST ? (uint32_t*)take(4ull * db.inv_stride) : nullptr;
-    uint32_t* W = (uint32_t*)take(4ull * WP);
-    uint32_t* res = TABLE ? nullptr : (uint32_t*)take(4ull * WP);  // ranks that are residual pivots
-    uint32_t* piv = (uint32_t*)take(4ull * b.piv_words);  // colex bitmap of apparent pivots (tie classes)
-    uint64_t* cols = (uint64_t*)take(8ull * kChainMaxCols);
-    uint16_t* own = (uint16_t*)take(2ull * kChainMaxCols);
-
-    const uint32_t ntri = (uint32_t)st->ntri;
-    const float* Dg = dist + (size_t)l * n * n;
-    const uint32_t* inv32g = db.inv32 + (size_t)l * db.inv_stride;
-    if constexpr (!TABLE) stage_to_lds(Dl, Dg, 4ull * n * n, t, kChainT);
-    if constexpr (FAST) {
-        stage_to_lds(rof, db.rank_of + (size_t)l * db.tri_stride, 2ull * db.tri_stride, t, kChainT);
-        stage_to_lds(inv32, inv32g, 4ull * ntri, t, kChainT);
-    } else {
-        if constexpr (GEN) stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kChainT);
-        if constexpr (TABLE) stage_to_lds(cobt, db.cobt + (size_t)l * db.cob_stride, 2ull * db.cob_stride, t, kChainT);  // whole words
-        stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kChainT);
-    }
-    const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
-    uint32_t* res1 = db.res1 + (size_t)l * b.piv_words;
-    stage_to_lds(piv, pivg, 4ull * b.piv_words, t, kChainT);
-    for (uint32_t i = t; i < WP; i += kChainT) {
-        st_lds(W, i, 0u);
-        if constexpr (!TABLE) st_lds(res, i, 0u);
-    }
-    uint64_t nres = (uint64_t)st->n_residual[1];
-    if (nres > b.rcap) nres = b.rcap;
-    // drop H0 deaths (spanning-forest edges: cleared columns), keep column
-    // order: ordered compaction over the whole block, kChainT columns a round
-    uint32_t* wcnt = (uint32_t*)own;  // per-wave counts (own is unused until the chain)
-    uint32_t nc = 0, nskip = 0;
-    {
-        const uint64_t* resid = b.resid + (size_t)l * b.rcap;
-        const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
-        for (uint64_t j0 = 0; j0 < nres; j0 += kChainT) {
-            const uint64_t j = j0 + t;
-            uint64_t key = 0;
-            bool keep = false;
-            if (j < nres) {
-                key = ld_glb(resid, j);
-                const uint32_t s = (uint32_t)key_idx(key);
-                keep = !((ld_glb(mst, s >> 5) >> (s & 31)) & 1u);
-            }
-            const uint64_t m = __ballot(keep);
-            if (ln == 0) wcnt[wv] = (uint32_t)__popcll(m);
-            __syncthreads();
-            uint32_t below = 0, tot = 0;
-            for (int q = 0; q < kChainT / 64; ++q) {
-                const uint32_t c = wcnt[q];
-                below += q < wv ? c : 0u;
-                tot += c;
-            }
-            const uint32_t pos = nc + below + lanes_below(m);
-            if (keep && pos < (uint32_t)kChainMaxCols) st_lds(cols, pos, key);
-            const uint32_t valid = (uint32_t)min<uint64_t>(kChainT, nres - j0);
-            nc += tot;
-            nskip += valid - tot;
-            __syncthreads();
-        }
-    }
-    __syncthreads();  // staging done (also when there are no columns)
-    if (wv != 0) return;
-
+    (void)Dl, (void)R, (void)rof, (void)cobt, (void)inv32, (void)res, (void)Dg, (void)inv32g, (void)l;
     const float r = st->thresh;
-    Pair* P = pairs + (size_t)l * pcap;
-    uint32_t* pool = (uint32_t*)(rb.rpool + (size_t)l * rb.rpool_cap);
-    const uint64_t pool_words = 2ull * rb.rpool_cap;
-    const uint32_t* clsg = db.cls + (size_t)l * db.E;
+    Pair* P = c.P;
+    uint32_t* pool = c.pool;
+    const uint64_t pool_words = c.pool_words;
+    const uint32_t* clsg = c.clsg;
     uint64_t ecnt = 0, cs = 0, npairs = 0, nadds = 0;
     uint32_t nown = 0;
     int err = nc > (uint32_t)kChainMaxCols ? 1 : 0;
@@ -838,6 +806,125 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
         atomicAdd((unsigned long long*)&st->n_columns[1], (unsigned long long)(0ull - nskip));
         st->nskip[1] = nskip;
     }
+}
+
+template <int K, int MODE>
+__global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                      DimBufs b, Reduce2Bufs rb, DenseBufs db, uint64_t step_limit,
+                                                      Pair* __restrict__ pairs, uint64_t pcap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool FAST = MODE == kChainFast, TABLE = MODE == kChainTable, GEN = MODE == kChainGeneral;
+    constexpr uint32_t WP = 64u * K;
+#ifdef TDA_PROFILE
+    const uint64_t t_entry = clock64();
+#endif
+    const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+    LayerStats* st = stats + l;
+    const int E = n * (n - 1) / 2;
+    unsigned char* p = smem + 16;
+    auto take = [&](size_t bytes) {
+        unsigned char* q = p;
+        p += (bytes + 15) & ~(size_t)15;
+        return q;
+    };
+    float* Dl = TABLE ? nullptr : (float*)take(4ull * n * n);
+    EdgeRec* R = GEN ? (EdgeRec*)take(16ull * E) : nullptr;
+    uint16_t* rof = FAST ? (uint16_t*)take(2ull * db.tri_stride) : nullptr;
+    uint16_t* cobt = TABLE ? (uint16_t*)take(2ull * db.cob_stride) : nullptr;
+    uint16_t* inv = FAST ? nullptr : (uint16_t*)take(2ull * db.inv_stride);
+    uint32_t* inv32 = FAST ? (uint32_t*)take(4ull * db.inv_stride) : nullptr;
+    uint32_t* W = (uint32_t*)take(4ull * WP);
+    uint32_t* res = TABLE ? nullptr : (uint32_t*)take(4ull * WP);  // ranks that are residual pivots
+    uint32_t* piv = (uint32_t*)take(4ull * b.piv_words);  // colex bitmap of apparent pivots (tie classes)
+    uint64_t* cols = (uint64_t*)take(8ull * kChainMaxCols);
+    uint16_t* own = (uint16_t*)take(2ull * kChainMaxCols);
+
+    const uint32_t ntri = (uint32_t)st->ntri;
+    const float* Dg = dist + (size_t)l * n * n;
+    const uint32_t* inv32g = db.inv32 + (size_t)l * db.inv_stride;
+    if constexpr (!TABLE) stage_to_lds(Dl, Dg, 4ull * n * n, t, kChainT);
+    if constexpr (FAST) {
+        stage_to_lds(rof, db.rank_of + (size_t)l * db.tri_stride, 2ull * db.tri_stride, t, kChainT);
+        stage_to_lds(inv32, inv32g, 4ull * ntri, t, kChainT);
+    } else {
+        if constexpr (GEN) stage_to_lds(R, db.recs + (size_t)l * db.E, 16ull * E, t, kChainT);
+        if constexpr (TABLE) stage_to_lds(cobt, db.cobt + (size_t)l * db.cob_stride, 2ull * db.cob_stride, t, kChainT);  // whole words
+        stage_to_lds(inv, db.inv + (size_t)l * db.inv_stride, 4ull * ((ntri + 1) / 2), t, kChainT);
+    }
+    const uint32_t* pivg = b.pivbits + (size_t)l * b.piv_words;
+    uint32_t* res1 = db.res1 + (size_t)l * b.piv_words;
+    stage_to_lds(piv, pivg, 4ull * b.piv_words, t, kChainT);
+    for (uint32_t i = t; i < WP; i += kChainT) {
+        st_lds(W, i, 0u);
+        if constexpr (!TABLE) st_lds(res, i, 0u);
+    }
+    uint64_t nres = (uint64_t)st->n_residual[1];
+    if (nres > b.rcap) nres = b.rcap;
+    // drop H0 deaths (spanning-forest edges: cleared columns), keep column
+    // order: ordered compaction over the whole block, kChainT columns a round
+    uint32_t* wcnt = (uint32_t*)own;  // per-wave counts (own is unused until the chain)
+    uint32_t nc = 0, nskip = 0;
+    {
+        const uint64_t* resid = b.resid + (size_t)l * b.rcap;
+        const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
+        for (uint64_t j0 = 0; j0 < nres; j0 += kChainT) {
+            const uint64_t j = j0 + t;
+            uint64_t key = 0;
+            bool keep = false;
+            if (j < nres) {
+                key = ld_glb(resid, j);
+                const uint32_t s = (uint32_t)key_idx(key);
+                keep = !((ld_glb(mst, s >> 5) >> (s & 31)) & 1u);
+            }
+            const uint64_t m = __ballot(keep);
+            if (ln == 0) wcnt[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t below = 0, tot = 0;
+            for (int q = 0; q < kChainT / 64; ++q) {
+                const uint32_t c = wcnt[q];
+                below += q < wv ? c : 0u;
+                tot += c;
+            }
+            const uint32_t pos = nc + below + lanes_below(m);
+            if (keep && pos < (uint32_t)kChainMaxCols) st_lds(cols, pos, key);
+            const uint32_t valid = (uint32_t)min<uint64_t>(kChainT, nres - j0);
+            nc += tot;
+            nskip += valid - tot;
+            __syncthreads();
+        }
+    }
+    __syncthreads();  // staging done (also when there are no columns)
+    if (wv != 0) return;
+    ChainCtx c;
+    c.Dl = Dl;
+    c.R = R;
+    c.rof = rof;
+    c.cobt = cobt;
+    c.inv = inv;
+    c.inv32 = inv32;
+    c.W = W;
+    c.res = res;
+    c.piv = piv;
+    c.cols = cols;
+    c.own = own;
+    c.Dg = Dg;
+    c.inv32g = inv32g;
+    c.res1 = res1;
+    c.pool = (uint32_t*)(rb.rpool + (size_t)l * rb.rpool_cap);
+    c.pool_words = 2ull * rb.rpool_cap;
+    c.clsg = db.cls + (size_t)l * db.E;
+    c.P = pairs + (size_t)l * pcap;
+    c.pcap = pcap;
+    c.st = st;
+    c.n = n;
+    c.l = l;
+    c.nc = nc;
+    c.nskip = nskip;
+    c.step_limit = step_limit;
+#ifdef TDA_PROFILE
+    c.t_entry = t_entry;
+#endif
+    h1_chain_wave<K, MODE>(c);
 }
 // bitmap words per lane supported by k_h1_chain instantiations (FAST / TABLE: up to 12)
 constexpr int kChainKs[] = {1, 2, 3, 4, 6, 9, 12, 16, 21};

@@ -572,17 +572,29 @@ __global__ __launch_bounds__(kUmapT) void k_umap_transform(UmapBufs u, const flo
     __syncthreads();
     // init_graph_transform on the unpruned graph (zeros eliminated): the
     // membership-weighted mean of the neighbours' embeddings in f32 -- or a
-    // neighbour's own embedding when its membership is exactly 1 -- NaN without neighbours
+    // neighbour's own embedding when its membership is exactly 1 -- NaN without
+    // neighbours.  umap-learn walks graph.tocsr() rows, whose entries are in
+    // ascending column (training index) order: the row sum, the weighted sum
+    // and which membership-1 entry wins all follow that order (the k neighbour
+    // slots are visited by ascending index, O(k^2) selection: k <= 64)
+    auto next_col = [&](int i, int prev) -> int {  // slot of the smallest training index > prev, -1 if none
+        int best = 0x7FFFFFFF, bj = -1;
+        for (int j = 0; j < k; ++j) {
+            const int col = ki[(size_t)i * k + j];
+            if (col > prev && col < best) best = col, bj = j;
+        }
+        return bj;
+    };
     for (int i = t; i < M; i += kUmapT) {
         float rs = 0.0f;
         int nnz = 0;
-        for (int j = 0; j < k; ++j) {
+        for (int j = next_col(i, -1); j >= 0; j = next_col(i, ki[(size_t)i * k + j])) {
             const float v = V[(size_t)i * k + j];
             if (v != 0.0f) rs += v, ++nnz;
         }
         float r[kUmapMaxC];
         for (int dd = 0; dd < c; ++dd) r[dd] = nnz ? 0.0f : __builtin_nanf("");
-        for (int j = 0; j < k && nnz; ++j) {
+        for (int j = nnz ? next_col(i, -1) : -1; j >= 0; j = next_col(i, ki[(size_t)i * k + j])) {
             const float v = V[(size_t)i * k + j];
             if (v == 0.0f) continue;
             const int col = ki[(size_t)i * k + j];

@@ -27,7 +27,11 @@ def compute_effective_dimensionality(activations_batch):
     every (n_samples, embed_dim) item of ``activations_batch`` (batch, n, d),
     S = its singular values (metrics.py:5-44; the input is taken as float32,
     metrics.py:25).  Returns (batch,) float32: a torch tensor on the input's
-    device for torch input, else a numpy array."""
+    device for torch input, else a numpy array.
+
+    Limit: min(n, d) <= 1024 (the f64 Gram matrix of the smaller side is
+    eigen-solved in one workgroup); a full-sequence call with more than 1024
+    tokens at D = 4096 (metrics.py:86) raises NotImplementedError."""
     is_t = _is_torch(activations_batch)
     stream, on_dev, device = None, 0, 0
     x = activations_batch
@@ -47,6 +51,8 @@ def compute_effective_dimensionality(activations_batch):
         x = np.ascontiguousarray(np.asarray(x), dtype=np.float32)
         if x.ndim == 3 and not np.all(np.isfinite(x)):
             raise ValueError("Input contains NaN or infinity")
+    if x.ndim == 3 and min(int(x.shape[1]), int(x.shape[2])) > 1024:
+        raise NotImplementedError("compute_effective_dimensionality: min(n_samples, embed_dim) <= 1024 is supported")
     if x.ndim != 3:
         raise ValueError("activations_batch must be (batch_size, n_samples, embed_dim)")
     ptr = x.data_ptr() if on_dev else x.ctypes.data

@@ -393,14 +393,35 @@ class SweepPipeline:
 
         if not 1 <= depth <= _lib.TDA_MAX_SLOTS:
             raise ValueError(f"depth must be in [1, {_lib.TDA_MAX_SLOTS}]")
+        self._check_kw(kw)
         self.depth, self.device, self.kw = depth, device, kw
         self._ex = [ThreadPoolExecutor(max_workers=1) for _ in range(depth)]  # one thread per slot: calls on a slot stay ordered
         self._n = 0
 
+    @staticmethod
+    def _check_kw(kw):
+        for k in ("slot", "device"):
+            if k in kw:
+                raise TypeError(f"SweepPipeline picks the {k} itself; do not pass {k}=")
+
     def submit(self, X, **kw):
+        self._check_kw(kw)
         s = self._n % self.depth
         self._n += 1
-        return self._ex[s].submit(ripser_batch, X, device=self.device, slot=s, **dict(self.kw, **kw))
+        args = dict(self.kw, **kw)
+        if _is_torch(X) and X.is_cuda:
+            # the worker thread's current stream is its own default stream: order the
+            # read after the SUBMITTING thread's current stream (where X was produced)
+            import torch
+
+            caller = torch.cuda.current_stream(X.device)
+
+            def call():
+                with torch.cuda.stream(caller):
+                    return ripser_batch(X, device=self.device, slot=s, **args)
+
+            return self._ex[s].submit(call)
+        return self._ex[s].submit(ripser_batch, X, device=self.device, slot=s, **args)
 
     def close(self):
         for e in self._ex:

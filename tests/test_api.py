@@ -155,3 +155,18 @@ def test_adversarial_record_keys_and_values(oracle):
     assert rec["n_h1_features"] == int(fin.sum())
     assert rec["max_h1_persistence"] == float(np.max(h1[fin, 1] - h1[fin, 0]))
     assert rec["silhouette_txt_shape"] == 0.4
+
+
+def test_sweep_pipeline_rejects_slot_and_device_kwargs(pkg):
+    """SweepPipeline picks each call's workspace slot and its device itself:
+    passing them raises a clear TypeError (not a duplicate-keyword error from
+    inside a worker thread) -- ADVICE r03."""
+    with pytest.raises(TypeError):
+        pkg.SweepPipeline(depth=2, slot=1)
+    with pytest.raises(TypeError):
+        pkg.SweepPipeline(depth=2, maxdim=1, slot=0)
+    with pkg.SweepPipeline(depth=2, maxdim=1) as pipe:
+        with pytest.raises(TypeError):
+            pipe.submit(np.zeros((1, 4, 3), np.float32), slot=3)
+        with pytest.raises(TypeError):
+            pipe.submit(np.zeros((1, 4, 3), np.float32), device=0)

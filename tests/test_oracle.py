@@ -225,3 +225,39 @@ def test_oracle_f64_distances_match_sklearn_f64_goldens(oracle):
         iu = np.triu_indices(X.shape[0], 1)
         got = oracle.distances(X)[iu]
         assert np.array_equal(got, z[name + "__condensed"].astype(np.float32)), name
+
+
+def test_oracle_under_asan_ubsan(oracle, ref_clouds):
+    """SURVEY §5 sanitizer row: the oracle's naive-reduction goldens,
+    known-answer cases and two reference layers at maxdim 2 run through
+    rips_oracle.c built with -fsanitize=address,undefined (and leak checks)
+    as a standalone driver (oracle/Makefile asan_driver); it exits clean and
+    reports the regular build's pair counts and checksums."""
+    import shutil
+    import subprocess
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    here = os.path.join(os.path.dirname(GOLDEN), "..", "oracle")
+    subprocess.run(["make", "-s", "-C", here, "asan_driver"], check=True)
+    drv = os.path.join(here, "_build", "asan_driver")
+    clouds = [np.array(c["X"], dtype=np.float32) for c in _load_naive()]
+    mds = [c["maxdim"] for c in _load_naive()]
+    t = np.linspace(0, 2 * np.pi, 40, endpoint=False)
+    clouds += [np.stack([np.cos(t), np.sin(t), np.zeros_like(t)], 1).astype(np.float32),
+               np.array([[0, 0, 0], [0, 0, 0], [1, 0, 0]], np.float32),
+               np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float32),
+               ref_clouds[5], ref_clouds[17]]
+    mds += [1, 1, 1, 2, 2]
+    text, want = [], []
+    for X, md in zip(clouds, mds):
+        Dm = oracle.distances(X)
+        text.append(f"{len(X)} {md} inf\n" + " ".join(repr(float(v)) for v in Dm.ravel()) + "\n")
+        r = oracle.rips(X, maxdim=md)
+        want.append("edges %d" % r["num_edges"] + "".join(
+            " | %d %d %d" % (len(r["dgms"][d]), r["n_all_pairs"][d], r["checksum"][d]) for d in range(md + 1)))
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    p = subprocess.run([drv], input="".join(text), capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "ERROR" not in p.stderr and "runtime error" not in p.stderr, p.stderr[-3000:]
+    assert p.stdout.split("\n")[:-1] == want

@@ -126,6 +126,28 @@ def test_transform_init_vs_restatement(pkg, built_lib, metric, d):
 
 
 @pytest.mark.gpu
+def test_transform_init_duplicate_points_vs_restatement(pkg, built_lib):
+    """Several memberships exactly 1: query points that duplicate training
+    points which are themselves duplicated (rows 2 and 5 identical).  The
+    restatement walks each graph row in ascending training index, as
+    umap-learn's init_graph_transform does over graph.tocsr(); the GPU must
+    pick the same neighbour's embedding."""
+    umap = __import__("importlib").import_module("tda-multimodal_amd.umap")
+    X, _ = clustered(2, d=64, seed=12)
+    train = X[1].copy()
+    train[5] = train[2]
+    train[9] = train[2]
+    red = umap.UMAP(n_neighbors=12, n_components=3, min_dist=0.1, random_state=42, metric="euclidean").fit(train)
+    Y = X[0].copy()
+    Y[:4] = train[[2, 5, 9, 3]]
+    got = umap.umap_transform_batch(train, red.embedding_, Y[None], n_neighbors=12, metric="euclidean", n_epochs=100,
+                                    learning_rate=0.0, a=red._a, b=red._b)
+    want = umap_ref.transform_init(train, red.embedding_, Y, 12, "euclidean", np.inf)
+    assert np.all(np.isfinite(got[0]))
+    assert np.max(np.abs(got[0] - want)) < 1e-3
+
+
+@pytest.mark.gpu
 def test_transform_reference_flow_fit_last_layer(pkg, built_lib):
     """analyze_tda_over_layers.py:38-44, :67-92: one reducer (n_neighbors =
     max(2, N // 2), cosine, random_state 42) fitted on the last layer, every
