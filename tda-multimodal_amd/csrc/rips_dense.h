@@ -33,7 +33,7 @@
 //       order; then B emits dims 0..2 into the host-mapped output.
 // The apparent-pair, tie and clearing rules are exactly those of the
 // multi-kernel dense path (rips_reduce_small.h, rips_kernels.h k_apparent),
-// which the parity tests pin against the oracle (oracle/rips_oracle.c).
+// which the parity tests pin against the CPU checker under oracle/.
 //
 // Cross-workgroup hand-off (MI355X_MICROARCH.md "inter-workgroup visibility"):
 // A's stores drain (vmcnt(0)), the workgroup barrier precedes wave 0's chain,

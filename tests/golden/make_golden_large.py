@@ -23,7 +23,14 @@ the GPU tests read the committed files and never run the oracle at this size).
   (seed 0, ~18 s of oracle) and torus1024 (configs[3]'s cloud at maxdim 2,
   ~90 s).  Same layout as large_cases.npz.
 
-Usage: python tests/golden/make_golden_large.py [--dist-only | --h2-only]
+* large_h2_2048.npz -- the oracle on H0-H2 at the top of the north_star N
+  range: torus2048 (seed 3) at the finite threshold 1.6 (ripser's `thresh`
+  argument; ~45 s of oracle, 272,670 H1 and 15.3 M H2 pairs in all, seven
+  of them with positive persistence), and at 1.2 (~14 s).  At the enclosing
+  radius the oracle would need hours.  Same layout as large_cases.npz plus
+  `<name>__user_thresh`.
+
+Usage: python tests/golden/make_golden_large.py [--dist-only | --h2-only | --h2-2048-only]
 """
 from __future__ import annotations
 
@@ -117,7 +124,28 @@ def h2_golden():
     np.savez_compressed(os.path.join(HERE, "large_h2.npz"), **out)
 
 
+H2_2048_CASES = {"torus2048_t16": 1.6, "torus2048_t12": 1.2}
+
+
+def h2_2048_golden():
+    from oracle import oracle
+
+    syn = __import__("importlib").import_module("tda-multimodal_amd.synthetic")
+    X = syn.torus(2048, seed=3)[None]
+    out = {}
+    for name, t in H2_2048_CASES.items():
+        t0 = time.time()
+        res = oracle.rips_batch_f32(X, 2, thresh=t)
+        print(f"{name} H0-H2 at thresh {t}: {time.time() - t0:.1f} s", flush=True)
+        out.update(case_arrays(name, X, 2, res))
+        out[f"{name}__user_thresh"] = np.array(t, np.float32)
+    np.savez_compressed(os.path.join(HERE, "large_h2_2048.npz"), **out)
+
+
 if __name__ == "__main__":
+    if "--h2-2048-only" in sys.argv:
+        h2_2048_golden()
+        sys.exit(0)
     if "--h2-only" in sys.argv:
         h2_golden()
         sys.exit(0)
@@ -125,3 +153,4 @@ if __name__ == "__main__":
     if "--dist-only" not in sys.argv:
         large_golden()
         h2_golden()
+        h2_2048_golden()

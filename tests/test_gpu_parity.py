@@ -425,6 +425,20 @@ def test_h2_above_568_vs_committed_oracle(gpu, monkeypatch, name, par2):
     assert pers[0] > 2.0 * pers[1]
 
 
+@pytest.mark.parametrize("name", ["torus2048_t16", "torus2048_t12"])
+def test_h2_n2048_finite_thresh_vs_committed_oracle(gpu, monkeypatch, name):
+    """Top of the north_star N range at maxdim 2 against the oracle: torus2048
+    at a finite `thresh` (ripser's argument; make_golden_large.py
+    --h2-2048-only), every pair with its indices, n_all_pairs (15.3 M H2 pairs
+    at 1.6) and checksums.  Wide edge-code keys (N > 568) on the parallel H2
+    reduction, no silent serial re-run (TDA_PAR_STRICT)."""
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")
+    z = np.load(os.path.join(GOLDEN, "large_h2_2048.npz"))
+    X = z[f"{name}__X"]
+    res = gpu.ripser_batch(X, maxdim=2, thresh=float(z[f"{name}__user_thresh"]))
+    assert_same_golden(res[0], z, name, 0, 2)
+
+
 @pytest.mark.parametrize("wide,par2", [("0", "1"), ("1", "1"), ("0", "0"), ("1", "0")])
 def test_h2_wide_keys_forced_vs_oracle(gpu, oracle, monkeypatch, wide, par2):
     """The wide edge-code keys forced below N = 568 (TDA_H2_WIDE=1) must give
