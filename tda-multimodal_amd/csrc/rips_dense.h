@@ -85,6 +85,7 @@ struct FusedBufs {
     LayerStats* hstats;
     uint64_t step_limit;
     uint32_t tri_stride, inv_stride, piv_words1;  // carve sizes (host mirrors)
+    int stop;                 // dev aid (TDA_FUSED_STOP, test overrides only): role B gives up after that phase
 };
 
 // ---------------------------------------------------------------- LDS carves
@@ -103,7 +104,7 @@ __host__ __device__ inline uint32_t fpow2(uint32_t x) {
 __host__ __device__ inline FCarve fused_carve_b(int n, uint32_t piv_words1) {
     FCarve c{};
     const uint32_t E = (uint32_t)(n * (n - 1) / 2), P2 = fpow2(E < 2 ? 2 : E);
-    uint32_t o = 64;
+    uint32_t o = 128;  // header: 32 words (flags, counters, block_excl scratch at [8, 25))
     auto take = [&](uint64_t b) {
         const uint32_t r = o;
         o += fal16(b);
@@ -138,7 +139,7 @@ __host__ __device__ inline FCarve fused_carve_b(int n, uint32_t piv_words1) {
 __host__ __device__ inline FCarve fused_carve_a(int n, int K, uint32_t ts, uint32_t is, uint32_t pw) {
     FCarve c{};
     const uint32_t E = (uint32_t)(n * (n - 1) / 2), P2 = fpow2(E < 2 ? 2 : E);
-    uint32_t o = 64;
+    uint32_t o = 128;  // header: 32 words (flags, counters, block_excl scratch at [8, 25))
     auto take = [&](uint64_t b) {
         const uint32_t r = o;
         o += fal16(b);
@@ -686,6 +687,10 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     for (uint32_t i = t; i < F.piv_words1; i += kFT) st_lds(h1app, i, 0u);
     __syncthreads();
     lds_bitonic(keys, P2, t, kFT, []() { __syncthreads(); });
+    if (F.stop == 1) {
+        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        return;
+    }
     // ---- B2: length class of every edge <= thr (rank of the first edge of its length)
     for (uint32_t q = t; q < E; q += kFT) {
         const uint64_t k = ld_lds(keys, q);
@@ -734,6 +739,10 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         if (ln == 0) st_lds(pm, (size_t)w * (n + 1), (uint64_t)0);
     }
     __syncthreads();
+    if (F.stop == 2) {
+        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        return;
+    }
     // ---- B4: H2 columns (thread per triangle): cleared / apparent / residual
     uint64_t acs = 0, napp = 0, ncol = 0;
     for (uint32_t base = 0; base < T3; base += kFT) {
@@ -804,6 +813,10 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
         return;
     }
+    if (F.stop == 3) {
+        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        return;
+    }
     // ---- B5: residual columns in column order (diam desc, idx asc)
     {
         const uint32_t P = fpow2(nres < 2 ? 2 : nres);
@@ -812,6 +825,10 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         lds_bitonic(resk, P, t, kFT, []() { __syncthreads(); });
     }
     if (t == 0) st->n_residual[2] = (int64_t)nres;
+    if (F.stop == 4) {
+        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        return;
+    }
     // ---- B6: phase 1 on every wave: apparent-only additions per column
     const uint32_t* res1 = F.res1 + (size_t)l * F.res1_words;
     auto cleared = [&](uint32_t tx) -> bool {
@@ -896,6 +913,10 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         }
     }
     __syncthreads();  // phase-1 results (HBM) are complete for wave 0
+    if (F.stop == 5) {
+        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        return;
+    }
     if (wv != 0) return;
     // ---- B7: wait for A (H1 residual pivots, dims 0-1 stats and pairs)
     if (ln == 0) {
@@ -907,6 +928,10 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     if (ld_lds(hdr, 5u)) {
+        if (ln == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        return;
+    }
+    if (F.stop == 6) {
         if (ln == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
         return;
     }
@@ -1031,6 +1056,7 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         }
         return true;
     };
+    uint64_t tsteps = 0;  // every column's steps together: a non-cancelling pivot ends in ERR_FUSED, not a hang
     for (uint32_t j = jc; j < nres && !err; ++j) {
         const uint32_t rk = ld_lds(resk, j), tx = rk & 0xFFFFu, sc = 2047u - (rk >> 16);
         const float sd = __uint_as_float(ld_lds(lenq, sc));
@@ -1073,7 +1099,7 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
             Wf.toggle(key, pk, ok);
         }
         for (uint64_t step = 0;; ++step) {
-            if (step >= F.step_limit || !room()) {
+            if (step >= F.step_limit || ++tsteps >= F.step_limit || !room()) {
                 err = 1;
                 break;
             }
@@ -1139,6 +1165,8 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         st->nskip[2] = (int64_t)nskip;
     }
     wave_sync();
+    if (F.stop == 7) err = 1;
+    if (ln == 0 && err) atomicOr(&st->err, (int32_t)ERR_FUSED);
     if (!err) fused_emit(F, l, 3, st);
 }
 
