@@ -21,7 +21,6 @@
 #include "rips_kernels.h"
 #include "rips_reduce_big.h"
 #include "rips_reduce_par.h"
-#include "rips_reduce_ls.h"
 #include "rips_reduce_small.h"
 #include "rips_dense.h"
 
@@ -79,7 +78,6 @@ constexpr unsigned kParGrid = 512;           // k_reduce_par workgroups at most 
 // faster without a second workgroup on its CU (r02, tools/ab_pargrid.sh:
 // grid144 10.5 -> 8.5 ms, torus1024 61 -> 58.5 ms at 256 vs 512)
 constexpr unsigned kParGridDefault = 256;
-constexpr bool kParLsDefault = false;  // k_reduce_ls (rips_reduce_ls.h) until it is GPU-validated
 unsigned par_grid_size() {
     const char* g = test_env("TDA_PAR_GRID");
     const unsigned v = g ? (unsigned)atoi(g) : kParGridDefault;
@@ -650,11 +648,7 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
-#define TDA_ATTR_LS(D, PK, W, RV) \
-    HIPC(hipFuncSetAttribute((const void*)k_reduce_ls<D, PK, W, RV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(LsLds)));
-    TDA_ATTR_LS(1, true, false, 3) TDA_ATTR_LS(1, false, false, 3) TDA_ATTR_LS(1, false, false, 7)
-    TDA_ATTR_LS(2, true, false, 3) TDA_ATTR_LS(2, false, false, 3) TDA_ATTR_LS(2, false, true, 3) TDA_ATTR_LS(2, false, true, 7)
-#undef TDA_ATTR_LS
+
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_edge_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEdgeSortLds));
     HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
@@ -1429,20 +1423,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 MARK("k_par_init");
                 // persistent workers (one 71-KB-LDS workgroup per CU by default); the surplus exits at once
                 const unsigned par_grid = par_grid_size();
-                // TDA_PAR_LS=0/1 (test overrides): the leader-wave column engine (k_reduce_ls) or k_reduce_par
-                const bool use_ls = test_env("TDA_PAR_LS") ? test_env_is("TDA_PAR_LS", "1") : kParLsDefault;
                 const uint32_t* no_clr = nullptr;
-                if (use_ls) {  // leader-wave column engine (rips_reduce_ls.h)
-                    if (p.packed)
-                        hipLaunchKernelGGL((k_reduce_ls<1, true, false, 3>), dim3(par_grid), dim3(kLsT), sizeof(LsLds), s, dist, n, L, stats, db[1],
-                                           no_clr, (uint64_t)0, rb, pb, gb.dcode, gb.dsort, gb.ecap);
-                    else if (n <= 64 * kLsWorkers * 3)
-                        hipLaunchKernelGGL((k_reduce_ls<1, false, false, 3>), dim3(par_grid), dim3(kLsT), sizeof(LsLds), s, dist, n, L, stats, db[1],
-                                           no_clr, (uint64_t)0, rb, pb, gb.dcode, gb.dsort, gb.ecap);
-                    else
-                        hipLaunchKernelGGL((k_reduce_ls<1, false, false, 7>), dim3(par_grid), dim3(kLsT), sizeof(LsLds), s, dist, n, L, stats, db[1],
-                                           no_clr, (uint64_t)0, rb, pb, gb.dcode, gb.dsort, gb.ecap);
-                } else if (p.packed)
+                if (p.packed)
                     hipLaunchKernelGGL((k_reduce_par<1, true>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats, db[1], no_clr,
                                        (uint64_t)0, rb, pb, gb.dcode, gb.dsort, gb.ecap);
                 else
@@ -1461,21 +1443,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                     HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                     hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[2], pb, 2);
                     HIPC(hipGetLastError());
-                    const uint32_t* c1 = (const uint32_t*)db[1].pivbits;
-                    if (use_ls) {
-                        if (p.wide && n <= 64 * kLsWorkers * 3)
-                            hipLaunchKernelGGL((k_reduce_ls<2, false, true, 3>), dim3(par_grid), dim3(kLsT), sizeof(LsLds), s, dist, n, L, stats,
-                                               db[2], c1, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
-                        else if (p.wide)
-                            hipLaunchKernelGGL((k_reduce_ls<2, false, true, 7>), dim3(par_grid), dim3(kLsT), sizeof(LsLds), s, dist, n, L, stats,
-                                               db[2], c1, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
-                        else if (n <= kPar2PackedMaxN)
-                            hipLaunchKernelGGL((k_reduce_ls<2, true, false, 3>), dim3(par_grid), dim3(kLsT), sizeof(LsLds), s, dist, n, L, stats,
-                                               db[2], c1, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
-                        else
-                            hipLaunchKernelGGL((k_reduce_ls<2, false, false, 3>), dim3(par_grid), dim3(kLsT), sizeof(LsLds), s, dist, n, L, stats,
-                                               db[2], c1, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
-                    } else if (p.wide)  // N > 568: edge-code keys (k_edge_codes ran above)
+                    if (p.wide)  // N > 568: edge-code keys (k_edge_codes ran above)
                         hipLaunchKernelGGL((k_reduce_par<2, false, true>), dim3(par_grid), dim3(kParT), sizeof(ParLds), s, dist, n, L, stats,
                                            db[2], (const uint32_t*)db[1].pivbits, db[1].piv_words, rb, pb, gb.dcode, gb.dsort, gb.ecap);
                     else if (n <= kPar2PackedMaxN)
@@ -1665,16 +1633,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)h[0], (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
                 (unsigned long long)h[4]);
     }
-    if (p.par && (test_env("TDA_PAR_LS") ? test_env_is("TDA_PAR_LS", "1") : kParLsDefault)) {
-        const uint64_t* q = w.hstats[0].prof[2];
-        const uint64_t* u = w.hstats[0].prof[3];
-        fprintf(stderr, "[tda-prof] k_reduce_ls longest column: %llu steps, %llu cycles: leader steps %llu (load wait %llu, LS toggles %llu; "
-                        "LS size sum %llu), refill syncs %llu, owner path %llu; pulls %llu (%llu cycles; %llu live of %llu raw keys), "
-                        "bucket refills %llu (%llu cycles), low keys %llu\n",
-                (unsigned long long)q[6], (unsigned long long)q[0], (unsigned long long)q[2], (unsigned long long)q[3], (unsigned long long)q[1],
-                (unsigned long long)q[7], (unsigned long long)q[4], (unsigned long long)q[5], (unsigned long long)u[0], (unsigned long long)u[1],
-                (unsigned long long)u[4], (unsigned long long)u[5], (unsigned long long)u[2], (unsigned long long)u[3], (unsigned long long)u[6]);
-    } else if (p.par) {
+    if (p.par) {
         const uint64_t* q = w.hstats[0].prof[2];
         fprintf(stderr, "[tda-prof] k_reduce_par longest column: %llu steps, %llu cycles: front_min %llu, pivot+rows %llu, apparent adds %llu, refills %llu (%llu), owner path %llu; avg front log %llu, compactions %llu, spills %llu\n",
                 (unsigned long long)q[6], (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[2], (unsigned long long)q[3],

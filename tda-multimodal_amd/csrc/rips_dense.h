@@ -467,6 +467,19 @@ __device__ __forceinline__ void fused_emit(const FusedBufs& F, int l, int nd, La
     for (int i = ln; i < (int)(sizeof(LayerStats) / 8); i += 64) dst[i] = src[i];
 }
 
+// the fused path gave up on layer l (one wave): the error has to reach the
+// host-mapped stats, which the host reads instead of the device copy (it then
+// re-runs the batch on the multi-kernel path)
+__device__ __forceinline__ void fused_fail(const FusedBufs& F, int l, LayerStats* st) {
+    const int ln = lane_id();
+    if (ln == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    const uint64_t* src = (const uint64_t*)st;
+    uint64_t* dst = (uint64_t*)(F.hstats + l);
+    for (int i = ln; i < (int)(sizeof(LayerStats) / 8); i += 64) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------- role A: H0 + H1
 template <int K>
 __device__ void fused_role_a(const FusedBufs& F, int l, int n, int maxdim, unsigned char* smem) {
@@ -688,7 +701,7 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     __syncthreads();
     lds_bitonic(keys, P2, t, kFT, []() { __syncthreads(); });
     if (F.stop == 1) {
-        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        if (wv == 0) fused_fail(F, l, st);
         return;
     }
     // ---- B2: length class of every edge <= thr (rank of the first edge of its length)
@@ -740,7 +753,7 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     }
     __syncthreads();
     if (F.stop == 2) {
-        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        if (wv == 0) fused_fail(F, l, st);
         return;
     }
     // ---- B4: H2 columns (thread per triangle): cleared / apparent / residual
@@ -810,11 +823,11 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     __syncthreads();
     const uint32_t nres = ld_lds(hdr, 1u);
     if (nres > kF2Cap) {  // too many H2 columns for the LDS lists: the multi-kernel path takes the batch
-        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        if (wv == 0) fused_fail(F, l, st);
         return;
     }
     if (F.stop == 3) {
-        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        if (wv == 0) fused_fail(F, l, st);
         return;
     }
     // ---- B5: residual columns in column order (diam desc, idx asc)
@@ -826,7 +839,7 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     }
     if (t == 0) st->n_residual[2] = (int64_t)nres;
     if (F.stop == 4) {
-        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        if (wv == 0) fused_fail(F, l, st);
         return;
     }
     // ---- B6: phase 1 on every wave: apparent-only additions per column
@@ -845,10 +858,13 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         S.pk = S.k + kFSet;
         S.cap = kFSet;
         S.clear();
-        for (;;) {
+#ifdef TDA_FUSED_DEBUG
+        uint32_t dbg_it = 0;
+#endif
+        for (uint32_t it = 0; it <= nres; ++it) {  // a wave takes at most nres columns
             uint32_t j = 0;
             if (ln == 0) j = __hip_atomic_fetch_add((TDA_LDS uint32_t*)hdr + 3, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+            j = (uint32_t)__builtin_amdgcn_readlane((int)j, 0);  // lane 0's counter, whatever the exec mask
             if (j >= nres) break;
             const uint32_t rk = ld_lds(resk, j), tx = rk & 0xFFFFu, sc = 2047u - (rk >> 16);
             uint32_t out_key = kFEmpty, info = 0;
@@ -862,7 +878,14 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
                 (void)f_cob(cls2, n, vs[0], vs[1], vs[2], sc, key, pk, ok);
                 S.toggle(key, pk, ok);
                 uint32_t adds = 0;
-                for (uint32_t step = 0;; ++step) {
+                for (uint32_t step = 0; step <= kP1MaxAdds + 1; ++step) {  // every pass either ends or adds
+#ifdef TDA_FUSED_DEBUG
+                    if (++dbg_it > 100000u) {
+                        if (ln == 0) printf("[fused dbg] layer %d wave %d phase1 stuck: col %u/%u step %u adds %u used %u\n", l, wv, j, nres, step, adds, S.used);
+                        info = kP1Overflow;
+                        break;
+                    }
+#endif
                     if (adds >= kP1MaxAdds || ((step & 7) == 7 && cleared(tx))) {
                         info = kP1Overflow;
                         break;
@@ -890,7 +913,7 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
                     nlive = (uint32_t)wave_sum_u64(nlive);
                     uint32_t o = 0;
                     if (ln == 0) o = __hip_atomic_fetch_add((TDA_LDS uint32_t*)hdr + 4, nlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    o = (uint32_t)__builtin_amdgcn_readfirstlane((int)o);
+                    o = (uint32_t)__builtin_amdgcn_readlane((int)o, 0);
                     if ((uint64_t)o + nlive > F.rpool2_cap) {
                         info = kP1Overflow;
                         break;
@@ -914,7 +937,7 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     }
     __syncthreads();  // phase-1 results (HBM) are complete for wave 0
     if (F.stop == 5) {
-        if (t == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        if (wv == 0) fused_fail(F, l, st);
         return;
     }
     if (wv != 0) return;
@@ -928,11 +951,11 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     if (ld_lds(hdr, 5u)) {
-        if (ln == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        fused_fail(F, l, st);
         return;
     }
     if (F.stop == 6) {
-        if (ln == 0) atomicOr(&st->err, (int32_t)ERR_FUSED);
+        fused_fail(F, l, st);
         return;
     }
     // ---- B8: phase 2 (serial, column order) on wave 0
@@ -1155,7 +1178,6 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
         Wf.clear();
     }
     if (ln == 0) {
-        if (err) atomicOr(&st->err, (int32_t)ERR_FUSED);
         if (ecnt > F.pcap[2]) atomicOr(&st->err, ERR_PAIR_CAP);
         st->count[2] = (int64_t)ecnt;
         atomicAdd((unsigned long long*)&st->checksum[2], (unsigned long long)cs);
@@ -1166,8 +1188,8 @@ __device__ void fused_role_b(const FusedBufs& F, int l, int n, unsigned char* sm
     }
     wave_sync();
     if (F.stop == 7) err = 1;
-    if (ln == 0 && err) atomicOr(&st->err, (int32_t)ERR_FUSED);
-    if (!err) fused_emit(F, l, 3, st);
+    if (err) fused_fail(F, l, st);
+    else fused_emit(F, l, 3, st);
 }
 
 // grid: maxdim 2: [0, L8) role A of layer l0 + b, [L8, 2 L8) role B; maxdim 1: role A only

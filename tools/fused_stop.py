@@ -25,4 +25,7 @@ for l in range(X.shape[0]):
     for d in range(3):
         if res[l].checksum[d] != o["checksum"][d] or len(res[l].dgms[d]) != len(o["dgms"][d]):
             bad += 1
+            print(f"  layer {l} dim {d}: {len(res[l].dgms[d])} vs {len(o['dgms'][d])} pairs, all {res[l].n_all_pairs[d]} vs "
+                  f"{o['n_all_pairs'][d]}, cols {res[l].n_columns[d]}, thresh {res[l].thresh} edges {res[l].num_edges} vs {o['num_edges']}",
+                  flush=True)
 print(f"stop {stop}: returned in {time.time() - t0:.3f} s, mismatches vs oracle {bad}", flush=True)
