@@ -261,7 +261,11 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     # resident in HBM before the timed region -- except the host-in record, which passes the numpy array
     X = X_host if host_in else torch.from_numpy(X_host).to(dev)
     torch.cuda.synchronize()
-    kw = CALL_KW.get(name, {})
+    kw = dict(CALL_KW.get(name, {}))
+    if os.environ.get("TDA_BENCH_ONE_STREAM") == "1":
+        kw["one_stream"] = True
+    if os.environ.get("TDA_BENCH_READY") == "1" and not host_in:  # X was synchronised above
+        kw["input_ready"] = True
     depth = int(os.environ.get("TDA_BENCH_DEPTH", PIPE_DEPTH[name])) if name in PIPE_DEPTH else 1
     dev_index = dev.index if dev.index is not None else 0
     seq = None

@@ -157,6 +157,11 @@ typedef struct tda_rips_result {
  * num_edges are 0.  What metrics.compute_intrinsic_dimensionality needs
  * (reference metrics.py:113-208 computes no persistence). */
 #define TDA_FLAG_NO_PERSISTENCE 8
+/* every kernel of the call on the slot's one stream (no side streams): the
+ * call's own latency grows, but a slot that only runs such calls holds one
+ * hardware queue, so several slots driven from their own host threads
+ * (args.slot) run their batches side by side (ripser.SweepPipeline) */
+#define TDA_FLAG_ONE_STREAM 16
 
 /* Batched point clouds (or distance matrices) -> persistence diagrams. */
 int tda_rips_batch(const tda_rips_args *args, tda_rips_result **out);

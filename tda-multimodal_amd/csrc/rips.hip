@@ -554,12 +554,19 @@ void drop_graphs(Workspace& w) {
     ++w.gen;
 }
 
+int ws_side_streams(Workspace& w) {
+    if (w.stream2) return 0;
+    HIPC(hipStreamCreateWithFlags(&w.stream2, hipStreamNonBlocking));
+    HIPC(hipStreamCreateWithFlags(&w.stream3, hipStreamNonBlocking));
+    HIPC(hipStreamCreateWithFlags(&w.stream4, hipStreamNonBlocking));
+    return 0;
+}
+
 int ws_prepare(Workspace& w, const Plan& p) {
     if (!w.init) {
+        // the side streams are created on the first multi-stream call (ws_side_streams):
+        // a slot that only runs TDA_FLAG_ONE_STREAM calls holds one hardware queue
         HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
-        HIPC(hipStreamCreateWithFlags(&w.stream2, hipStreamNonBlocking));
-        HIPC(hipStreamCreateWithFlags(&w.stream3, hipStreamNonBlocking));
-        HIPC(hipStreamCreateWithFlags(&w.stream4, hipStreamNonBlocking));
         HIPC(hipEventCreateWithFlags(&w.evh, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evs, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evp, hipEventDisableTiming));
@@ -801,12 +808,17 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         w.htn_cap = std::max(L, 64);
     }
 
+    // TDA_FLAG_STAGE_SERIAL (with stage times) or TDA_FLAG_ONE_STREAM: every
+    // stage on the main stream -- each pair of stage events then brackets one
+    // kernel only, and a slot keeps to one hardware queue (several slots in
+    // flight each get their own: SweepPipeline)
+    const bool serial_stages = ((a.flags & TDA_FLAG_STAGE_TIMES) && (a.flags & TDA_FLAG_STAGE_SERIAL)) || (a.flags & TDA_FLAG_ONE_STREAM);
+    if (!serial_stages)
+        if (int rc = ws_side_streams(w)) return rc;
+
     rt_lock.unlock();  // host buffers are in place; the capture below re-takes it
 
-    // TDA_FLAG_STAGE_SERIAL: every stage on the main stream, so each pair of
-    // events brackets one kernel only (no time spent queued behind the side
-    // streams' kernels); the side streams are restored on return
-    const bool serial_stages = (a.flags & TDA_FLAG_STAGE_TIMES) && (a.flags & TDA_FLAG_STAGE_SERIAL);
+    // serial_stages: the side streams are aliased to the main one here and restored on return
     struct StreamSwap {
         Workspace& w;
         hipStream_t s2, s3, s4;
@@ -1161,7 +1173,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         const int app_lds_max = test_env("TDA_APP_LDS_MAXN") ? atoi(test_env("TDA_APP_LDS_MAXN")) : kAppLdsMaxN;
         const bool dl = n <= app_lds_max && 16 + (size_t)n * n * 4 <= (size_t)kLdsMax;
         const size_t alds = 16 + (dl ? (size_t)n * n * 4 : 0);
-        if (d == 1) {
+        // N <= 64: the small-N pass (32-bit decode, 4 vertices per LDS read); TDA_APP_SMALL=0 -> k_apparent
+        if (n <= 64 && dl && !test_env_is("TDA_APP_SMALL", "0")) {
+            const size_t slds = 16 + (size_t)n * ((n + 3) & ~3) * 4;
+            if (d == 1)
+                hipLaunchKernelGGL((k_apparent_small<1>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh);
+            else
+                hipLaunchKernelGGL((k_apparent_small<2>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh);
+        } else if (d == 1) {
             if (dl)
                 hipLaunchKernelGGL((k_apparent<1, true>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
             else

@@ -56,6 +56,10 @@ __device__ __forceinline__ int max_vertex(uint64_t idx, int k, int top) {
     return v;
 }
 
+// 32-bit binomials for small vertex counts (N <= 64: C(N, 3) < 2^16)
+__device__ __forceinline__ uint32_t c2u(uint32_t x) { return x * (x - 1) / 2; }
+__device__ __forceinline__ uint32_t c3u(uint32_t x) { return x * (x - 1) * (x - 2) / 6; }
+
 // index -> vertices, descending (vs[0] largest), DIM+1 vertices
 template <int DIM>
 __device__ __forceinline__ void decode(uint64_t idx, int n, int (&vs)[DIM + 1]) {

@@ -1469,6 +1469,177 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
     }
 }
 
+// Small-N apparent pass (N <= 64, the reference's clouds): same columns,
+// pairs and residual lists as k_apparent<DIM, true>, with the per-simplex
+// instruction count cut ~3x (PMC r04: k_apparent<2> issued 2.1 K VALU per wave
+// and was VALU-bound): 32-bit index decode (every binomial < 2^18), the
+// matrix staged with rows padded to a multiple of 4 (+inf pads), and the
+// oldest-cofacet scan reading four vertices per ds_read_b128 from the rows of
+// the simplex's own vertices (D symmetric), branch-free inside a group.  Scan
+// order and tie rule are k_apparent's: vertices descending, a strictly smaller
+// diameter wins (so the largest vertex among equal minima), stop at
+// diam == diam(s) -- no later vertex can beat it, as every cofacet diameter is
+// >= diam(s).
+template <int DIM>
+__device__ __forceinline__ void decode_small(uint32_t s, int n, int (&vs)[DIM + 1]) {
+    uint32_t rem = s;
+    int top = n - 1;
+    if (DIM == 2) {  // largest a <= n - 1 with C(a, 3) <= s
+        const float x = 6.0f * (float)rem;
+        int a = (x > 0.0f ? (int)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf(x) * (1.0f / 3.0f)) : 0) + 1;
+        a = min(max(a, 2), top);
+        while (a > 2 && c3u((uint32_t)a) > rem) --a;
+        while (a < top && c3u((uint32_t)a + 1u) <= rem) ++a;
+        vs[0] = a;
+        rem -= c3u((uint32_t)a);
+        top = a - 1;
+    }
+    {  // largest b <= top with C(b, 2) <= rem
+        int b = (int)(0.5f * (1.0f + __fsqrt_rn(1.0f + 8.0f * (float)rem)));
+        b = min(max(b, 1), top);
+        while (b > 1 && c2u((uint32_t)b) > rem) --b;
+        while (b < top && c2u((uint32_t)b + 1u) <= rem) ++b;
+        vs[DIM - 1] = b;
+        rem -= c2u((uint32_t)b);
+        vs[DIM] = (int)min(rem, (uint32_t)(b - 1));
+    }
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                        DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.y;
+    const float* Dg = dist + (size_t)l * n * n;
+    const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
+    const int ns = (n + 3) & ~3;  // padded row stride (16-B rows)
+    TDA_LDS float* Dsh = (TDA_LDS float*)(smem + 16);
+    if (ns == n) {
+        stage_to_lds((float*)Dsh, Dg, sizeof(float) * n * n, threadIdx.x, blockDim.x);
+    } else {  // padded rows: (i, j) advanced incrementally (no division per element)
+        const int T = blockDim.x, di = T / ns, dj = T - di * ns;
+        int i = threadIdx.x / ns, j = threadIdx.x - i * ns;
+        for (int e = threadIdx.x; e < n * ns; e += T) {
+            Dsh[e] = j < n ? ld_glb(Dg, (size_t)i * n + j) : INFINITY;
+            i += di;
+            j += dj;
+            if (j >= ns) j -= ns, ++i;
+        }
+    }
+    __syncthreads();
+    LayerStats* st = stats + l;
+    const uint32_t* cleared = b.cleared ? b.cleared + (size_t)l * b.cleared_words : nullptr;
+    uint32_t* piv = b.pivbits + (size_t)l * b.piv_words;
+    uint64_t* resid = b.resid + (size_t)l * b.rcap;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t ncand = (uint32_t)b.ncand;
+    uint64_t acc_cs = 0, acc_app = 0, acc_cols = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < ncand; base += stride) {
+        const uint32_t s = base + threadIdx.x;
+        int kind = 0;  // 0 skip, 1 apparent, 2 residual (incl. empty coboundary)
+        int vs[DIM + 1];
+        float sd = 0.0f;
+        if (s < ncand && !(cleared && ((ld_glb(cleared, (size_t)(s >> 5)) >> (s & 31)) & 1u))) {
+            decode_small<DIM>(s, n, vs);
+            float pd[DIM + 1][DIM + 1];  // the simplex's edge lengths (registers after unrolling)
+#pragma unroll
+            for (int i = 0; i <= DIM; ++i)
+#pragma unroll
+                for (int j = i + 1; j <= DIM; ++j) {
+                    pd[i][j] = pd[j][i] = Dsh[vs[i] * ns + vs[j]];
+                    sd = fmaxf(sd, pd[i][j]);
+                }
+            if (sd <= r) {
+                uint64_t mm = 0;
+#pragma unroll
+                for (int i = 0; i <= DIM; ++i) mm |= 1ull << vs[i];
+                float bcd = INFINITY;
+                int bv = -1;
+                // eight vertices per iteration: both groups' reads are in flight together
+                for (int g = ns - 4; g >= 0; g -= 8) {
+                    const int g2 = max(g - 4, 0);
+                    v4f x[2][DIM + 1];
+#pragma unroll
+                    for (int i = 0; i <= DIM; ++i) {
+                        x[0][i] = *(const TDA_LDS v4f*)(Dsh + vs[i] * ns + g);
+                        x[1][i] = *(const TDA_LDS v4f*)(Dsh + vs[i] * ns + g2);
+                    }
+                    // the second group is void past vertex 0 (all four marked as members)
+                    const uint32_t mb = ((uint32_t)(mm >> g) & 0xFu) | (((g >= 4 ? (uint32_t)(mm >> g2) : 0xFu) & 0xFu) << 4);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int q = 3; q >= 0; --q) {
+                            float cd = sd;
+#pragma unroll
+                            for (int i = 0; i <= DIM; ++i) cd = fmaxf(cd, x[h][i][q]);
+                            const bool ok = !((mb >> (4 * h + q)) & 1u) && cd <= r && cd < bcd;
+                            bcd = ok ? cd : bcd;
+                            bv = ok ? (h ? g2 : g) + q : bv;
+                        }
+                    if (bcd == sd) break;
+                }
+                kind = 2;  // residual unless apparent (an empty coboundary is decided by the reduction)
+                if (bv >= 0 && bcd == sd) {
+                    float dv[DIM + 1];
+#pragma unroll
+                    for (int i = 0; i <= DIM; ++i) dv[i] = Dsh[bv * ns + vs[i]];
+                    bool app = true;
+#pragma unroll
+                    for (int u = 0; u <= DIM; ++u) {
+                        if (vs[u] < bv) continue;
+                        // diam of (s u {bv}) \ {vs[u]}
+                        float fd = 0.0f;
+#pragma unroll
+                        for (int i = 0; i <= DIM; ++i) {
+                            if (i == u) continue;
+                            fd = fmaxf(fd, dv[i]);
+#pragma unroll
+                            for (int j = i + 1; j <= DIM; ++j)
+                                if (j != u) fd = fmaxf(fd, pd[i][j]);
+                        }
+                        app &= fd < sd;
+                    }
+                    if (app) {
+                        kind = 1;
+                        const uint64_t tix = cofacet_index<DIM>(vs, bv);
+                        matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
+                        acc_cs += pair_hash(s, tix);
+                        acc_app += 1;
+                    }
+                }
+            }
+        }
+        acc_cols += (kind != 0);
+        // residual append (wave aggregated)
+        const uint64_t m = __ballot(kind == 2);
+        if (m) {
+            uint64_t basepos = 0;
+            if (lane_id() == __builtin_ctzll(m))
+                basepos = atomicAdd((unsigned long long*)&st->n_residual[DIM], (unsigned long long)__popcll(m));
+            basepos = shfl_u64(basepos, __builtin_ctzll(m));
+            if (kind == 2) {
+                const uint64_t pos = basepos + lanes_below(m);
+                if (pos < b.rcap)
+                    st_glb(resid, pos, col_key(sd, s));
+                else
+                    atomicOr(&st->err, ERR_RESID_CAP);
+            }
+        }
+    }
+    acc_cs = wave_sum_u64(acc_cs);
+    acc_app = wave_sum_u64(acc_app);
+    acc_cols = wave_sum_u64(acc_cols);
+    if (lane_id() == 0) {
+        if (acc_app) {
+            atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)acc_cs);
+            atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)acc_app);
+        }
+        if (acc_cols) atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)acc_cols);
+    }
+}
+
 // ------------------------------------------------------------------ sort residual
 struct SortArgs {
     uint64_t* resid[3];

@@ -48,8 +48,6 @@ constexpr uint32_t kP1WCap = 512;         // phase-1 toggle-set capacity
 constexpr int kChainMaxCols = 512;        // non-cleared H1 residual columns / stored R_j per layer
 constexpr int kMaxK = 21;                 // bitmap words per lane: ceil(C(64,3) / 32 / 64)
 
-__device__ __forceinline__ uint32_t c2u(uint32_t x) { return x * (x - 1) / 2; }
-__device__ __forceinline__ uint32_t c3u(uint32_t x) { return x * (x - 1) * (x - 2) / 6; }
 __device__ __forceinline__ uint32_t edge_id(int a, int b) { return a > b ? c2u(a) + b : c2u(b) + a; }
 __device__ __forceinline__ uint32_t tri_id(int a, int b, int c) {
     const int x = max(a, max(b, c)), z = min(a, min(b, c)), y = a + b + c - x - z;

@@ -221,7 +221,8 @@ def encode_labels(label_sets, n: int) -> np.ndarray:
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
                  want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None,
                  stage_serial: bool = False, twonn: bool = False, discard_fraction: float = 0.1, eps: float = 1e-10,
-                 want_dist64: bool = False, slot: int = 0, persistence: bool = True):
+                 want_dist64: bool = False, slot: int = 0, persistence: bool = True,
+                 one_stream: bool = False, input_ready: bool = False):
     """Persistence of L layers in one call.
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
@@ -242,6 +243,11 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     slot: the device workspace (0 .. 7) the call runs in; calls from different
     host threads on different slots run concurrently on the GPU (see
     :class:`SweepPipeline`).
+    input_ready: a CUDA tensor X is already complete (the caller synchronised
+    after producing it): the call skips its event on torch's current stream.
+    one_stream: every kernel of the call on the slot's one stream
+    (TDA_FLAG_ONE_STREAM): slower alone, but each slot then holds one hardware
+    queue, so several slots in flight run side by side.
     persistence=False (maxdim 0 only): distances and the side metrics asked for
     (``twonn``, ``labels``) without any persistence; every diagram is empty.
     """
@@ -260,7 +266,10 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
         device = keep.device.index if keep.device.index is not None else torch.cuda.current_device()
         # torch's current stream on that device (raw handle: no Stream object per call)
         raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
-        a.stream = raw_stream(device) if raw_stream else torch.cuda.current_stream(keep.device).cuda_stream
+        # input_ready: the caller has synchronised after producing X, so no
+        # device-side ordering on its stream (whose queue a pipeline slot may share)
+        if not input_ready:
+            a.stream = raw_stream(device) if raw_stream else torch.cuda.current_stream(keep.device).cuda_stream
         dtype_is64 = keep.dtype == torch.float64
     else:
         if _is_torch(X):
@@ -289,6 +298,8 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     a.slot = int(slot)
     a.want_dist = 1 if want_dist else 0
     a.flags = (_lib.TDA_FLAG_STAGE_TIMES | (_lib.TDA_FLAG_STAGE_SERIAL if stage_serial else 0)) if stage_times else 0
+    if one_stream:
+        a.flags |= _lib.TDA_FLAG_ONE_STREAM
     if not persistence:
         if maxdim != 0:
             raise ValueError("persistence=False needs maxdim=0")

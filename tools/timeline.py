@@ -44,5 +44,17 @@ for s in steps[3:]:
     for a, b, name, q in s:
         dur[name].append((b - a) / 1e3)
 print(f"median step span {statistics.median(spans):.1f} us")
+# median start / end of each kernel relative to its step's start, over the
+# timed steps (the bench's later one-stream stage pass excluded: first 60 %)
+off = defaultdict(list)
+for s in steps[3:max(4, int(len(steps) * 0.6))]:
+    t0 = s[0][0]
+    seen = defaultdict(int)
+    for a, b, name, q in s:
+        seen[name] += 1
+        off[f"{name}#{seen[name]}" if seen[name] > 1 else name].append(((a - t0) / 1e3, (b - t0) / 1e3))
+print("median start .. end (us) over the timed steps")
+for k, v in sorted(off.items(), key=lambda kv: statistics.median(x[0] for x in kv[1])):
+    print(f"  {statistics.median(x[0] for x in v):7.1f} .. {statistics.median(x[1] for x in v):7.1f}  {k}")
 for k, v in sorted(dur.items(), key=lambda kv: -statistics.median(kv[1])):
     print(f"  {statistics.median(v):8.1f} us  {k}")
