@@ -72,12 +72,14 @@ DATA = {
 NPOINTS = {"torus1024x32": 1024, "sweep48": 48, "sweep48x4": 48, "sweep48_host": 48, "sweep48_L4": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
 DIMS = {w: (4096 if w == "raw4096" else 3) for w in WORKLOADS}  # point dimension D of each workload (make_workload)
 CALL_KW = {"raw4096": {"twonn": True}}
-# consecutive sweeps in flight at once (ripser.SweepPipeline: one device workspace slot per in-flight
-# call): the dense N <= 64 path is a chain of latency-bound kernels that leaves most of the 256 CUs idle
-# (measured r03: 2-4 sweeps in flight on 4 hardware queues gave 0.9-1.2x the one-call-at-a-time rate
-# from box to box -- noise-level -- so the default bench times one call at a time; TDA_BENCH_DEPTH=n
-# with these workloads times n in flight)
-PIPE_DEPTH = {"sweep48": 1, "sweep48_host": 1, "sweep48_L4": 1}
+# dynamic batching of consecutive steps (ripser.SweepPipeline): every step submits one 32-layer sweep;
+# up to `coalesce` queued sweeps run as one call over their concatenated layers and `depth` calls are in
+# flight on separate workspace slots, one stream (hardware queue) each.  The dense N <= 64 path is a
+# chain of latency-bound kernels that leaves most of the 256 CUs idle; wider calls and several calls in
+# flight fill them (r04, tools/ab_coalesce.sh: 148 K layers/s one call at a time -> 217 K coalescing 4,
+# 305 K with 2 in flight, 455 K with 4).  Every record also carries the one-call-at-a-time figure
+# (pipeline.sequential).  sweep48_L4 stays one call at a time: it is the per-call latency record.
+PIPE = {"sweep48": (4, 4), "sweep48_host": (4, 4), "sweep48_L4": (1, 1)}  # workload -> (depth, coalesce)
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
 CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
 
@@ -214,9 +216,10 @@ def cpu_baseline(pool, P: int, name: str, X, maxdim: int, seconds: float) -> dic
 
 
 # ---------------------------------------------------------------- GPU measurement
-def _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_index):
-    """K steps (sequential, or `depth` in flight on separate workspace slots) between two syncs;
-    returns (elapsed s, device ms per call)."""
+def _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_index, coalesce=1):
+    """K steps (sequential, or through ripser.SweepPipeline: `depth` calls in flight on separate
+    workspace slots, each call covering up to `coalesce` consecutive steps' sweeps) between two
+    syncs; returns (elapsed s, device ms per step)."""
     import collections
 
     dev_ms = []
@@ -225,9 +228,9 @@ def _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_i
         if host_in:  # debug_tda_pipeline.py:110: dgms = result['dgms'] for every layer
             for r in res:
                 r.dgms
-        dev_ms.append(info["device_ms"])
+        dev_ms.append(info["device_ms"] / info.get("coalesced", 1))
 
-    if depth <= 1:
+    if depth <= 1 and coalesce <= 1:
         for _ in range(warmup):
             pkg.ripser_batch(X, maxdim=maxdim, **kw)
         torch.cuda.synchronize()
@@ -236,14 +239,16 @@ def _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_i
             done(*pkg.ripser_batch(X, maxdim=maxdim, return_time=True, **kw))
         torch.cuda.synchronize()
         return time.perf_counter() - t0, dev_ms
-    with pkg.SweepPipeline(depth=depth, device=dev_index, maxdim=maxdim, return_time=True, **kw) as pipe:
-        for f in [pipe.submit(X) for _ in range(max(warmup, 1) * depth)]:  # every slot captures its graph
+    inflight = depth * coalesce  # steps submitted and not yet waited on
+    with pkg.SweepPipeline(depth=depth, device=dev_index, coalesce=coalesce, maxdim=maxdim, return_time=True, **kw) as pipe:
+        for f in [pipe.submit(X) for _ in range(max(warmup, 1) * inflight)]:  # every slot captures its graph
             f.result()
         torch.cuda.synchronize()
+        dev_ms.clear()
         t0 = time.perf_counter()
         q = collections.deque()
         for _ in range(steps):
-            if len(q) == depth:
+            if len(q) == inflight:
                 done(*q.popleft().result())
             q.append(pipe.submit(X))
         while q:
@@ -262,17 +267,21 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     X = X_host if host_in else torch.from_numpy(X_host).to(dev)
     torch.cuda.synchronize()
     kw = dict(CALL_KW.get(name, {}))
-    if os.environ.get("TDA_BENCH_ONE_STREAM") == "1":
-        kw["one_stream"] = True
     if os.environ.get("TDA_BENCH_READY") == "1" and not host_in:  # X was synchronised above
         kw["input_ready"] = True
-    depth = int(os.environ.get("TDA_BENCH_DEPTH", PIPE_DEPTH[name])) if name in PIPE_DEPTH else 1
+    depth, coalesce = PIPE.get(name, (1, 1))
+    depth = int(os.environ.get("TDA_BENCH_DEPTH", depth)) if name in PIPE else 1
+    coalesce = int(os.environ.get("TDA_BENCH_COALESCE", coalesce)) if name in PIPE else 1
+    kw_pipe = dict(kw)
+    if os.environ.get("TDA_BENCH_ONE_STREAM") in ("0", "1"):  # else SweepPipeline's default (one stream when depth > 1)
+        kw_pipe["one_stream"] = os.environ["TDA_BENCH_ONE_STREAM"] == "1"
     dev_index = dev.index if dev.index is not None else 0
     seq = None
-    if depth > 1:  # the one-call-at-a-time figure next to the pipelined one
+    piped = depth > 1 or coalesce > 1
+    if piped:  # the one-call-at-a-time figure next to the pipelined one
         el_s, dm_s = _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, 1, host_in, dev_index)
         seq = {"value": L * steps / el_s, "ms_per_step": el_s / steps * 1e3, "device_ms_per_step": sum(dm_s) / len(dm_s)}
-    el, dev_ms = _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_index)
+    el, dev_ms = _timed_steps(pkg, torch, X, maxdim, kw_pipe if piped else kw, steps, warmup, depth, host_in, dev_index, coalesce)
     # per-kernel durations: HIP events around every kernel with all stages on
     # ONE stream (each interval brackets exactly one kernel), same batch,
     # after the timed region; the dominant kernel has the largest mean
@@ -319,9 +328,11 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
                                       "stream, after the timed region (same batch)"},
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},
         "roofline_mfma": mfma_roof,
-        "pipeline": {"depth": depth, "sequential": seq,
-                     "note": "value: `depth` consecutive steps in flight (ripser.SweepPipeline, one workspace slot each); "
-                             "sequential: one call at a time"} if depth > 1 else None,
+        "pipeline": {"depth": depth, "coalesce": coalesce, "one_stream": kw_pipe.get("one_stream", depth > 1), "sequential": seq,
+                     "note": "value: every step submits one sweep to ripser.SweepPipeline; up to `coalesce` consecutive "
+                             "sweeps run as one call over their concatenated layers (each step's future returns its own "
+                             "sweep), `depth` calls in flight on separate workspace slots; sequential: one "
+                             "ripser_batch call per step, one at a time"} if piped else None,
     }
 
 
@@ -404,16 +415,27 @@ def main():
         value, el_ms = prim["value"], prim["ms_per_step"]
     else:
         X = torch.from_numpy(make_workload(args.workload, L)).to(dev)
+        # the same dynamic batching as the one-GPU record (bench PIPE): each rank's steps through a SweepPipeline
+        slots, coalesce = PIPE.get(args.workload, (1, 1))
+        slots = int(os.environ.get("TDA_BENCH_DEPTH", slots))
+        coalesce = int(os.environ.get("TDA_BENCH_COALESCE", coalesce))
 
         def run_multi(shard: bool):
             torch.cuda.synchronize()
             for _ in range(args.warmup):
                 pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=coll_dev, shard=shard)
+            if slots > 1 or coalesce > 1:  # every slot captures its graphs before the timed region
+                warm = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
+                                                      coalesce=coalesce)
+                for _ in range(max(args.warmup, 1) * slots * coalesce):
+                    warm.step()
+                warm.close()
             dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            # every step's records are exchanged; the exchange of step i overlaps the GPU work of step i + 1
-            pipe = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard)
+            # every step's records are exchanged; the exchange of step i overlaps the GPU work of later steps
+            pipe = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
+                                                  coalesce=coalesce)
             for _ in range(args.steps):
                 pipe.step()
             pipe.close()
@@ -452,6 +474,9 @@ def main():
             out["pipeline"] = prim["pipeline"]
         if strong:
             out["strong"] = strong
+        if world > 1 and (slots > 1 or coalesce > 1):
+            out["pipeline"] = {"depth": slots, "coalesce": coalesce, "note": "each rank's steps through ripser.SweepPipeline "
+                               "(as the one-GPU record); records exchanged per step, in step order"}
     if rank == 0 and world == 1:
         cpu_done = {}
         if do_cpu:

@@ -143,10 +143,14 @@ class PipelinedSweep:
     strictly in step order, so every rank issues the same collective sequence.
     ``close()`` waits for the last exchange and returns its rows (rank 0).
     Same arguments and per-step result as :func:`sharded_sweep_step`.
+    slots / coalesce > 1: each step's shard goes through a
+    :class:`~ripser.SweepPipeline` (``coalesce`` consecutive steps per call,
+    ``slots`` calls in flight) -- what the one-GPU bench times -- and the
+    worker exchanges the steps' records in step order as their calls finish.
     """
 
     def __init__(self, X, maxdim: int, rank: int, world: int, dist=None, device=None, layer_base: int = 0,
-                 shard: bool = True, run=None, depth: int = 2):
+                 shard: bool = True, run=None, depth: int = 2, slots: int = 1, coalesce: int = 1):
         import queue
         import threading
 
@@ -162,7 +166,15 @@ class PipelinedSweep:
             self.lo, self.hi = 0, L
             self.total = L * world
         self.ids = np.arange(self.lo, self.hi) + (layer_base if shard else rank * L)
-        self.q = queue.Queue(maxsize=max(1, depth))
+        self.pipe = None
+        if slots > 1 or coalesce > 1:
+            from .ripser import SweepPipeline
+
+            gpu = getattr(X, "is_cuda", False)
+            prun = None if run is None else (lambda Xs, maxdim, **_: run(Xs, maxdim))
+            self.pipe = SweepPipeline(depth=slots, device=X.device.index if gpu else 0, coalesce=coalesce, maxdim=maxdim,
+                                      run=prun)
+        self.q = queue.Queue(maxsize=max(1, depth) + (slots * coalesce if self.pipe else 0))
         self.last, self.err, self.steps = (None, None), None, 0
         self.thread = threading.Thread(target=self._worker, daemon=True)
         self.thread.start()
@@ -179,6 +191,8 @@ class PipelinedSweep:
             if self.err is not None:  # after a failure: keep draining, so step() / close() never block on a full queue
                 continue
             try:
+                if hasattr(res, "result"):  # a SweepPipeline future: this step's own layers, in step order
+                    res = res.result()
                 packed, cap = pack_results(res, self.ids, self.maxdim)
                 out = gather_packed(packed, cap, self.total, self.dist, self.device)
                 self.last = out if out is not None else (None, None)
@@ -188,13 +202,20 @@ class PipelinedSweep:
     def step(self):
         if self.err is not None:
             raise self.err
-        res = self.run(self.X[self.lo:self.hi], maxdim=self.maxdim) if self.hi > self.lo else []
-        self.q.put(res)  # blocks while the worker is `depth` exchanges behind
+        if self.hi <= self.lo:
+            res = []
+        elif self.pipe is not None:
+            res = self.pipe.submit(self.X[self.lo:self.hi])
+        else:
+            res = self.run(self.X[self.lo:self.hi], maxdim=self.maxdim)
+        self.q.put(res)  # blocks while the worker is `depth` exchanges (+ the pipeline's steps in flight) behind
         self.steps += 1
 
     def close(self):
         self.q.put(None)
         self.thread.join()
+        if self.pipe is not None:
+            self.pipe.close()
         if self.err is not None:
             raise self.err
         return self.last

@@ -389,25 +389,66 @@ def silhouette_score(X, labels) -> float:
     return ripser_batch(X[None], maxdim=0, labels=[labels])[0].silhouette[0]
 
 
+class _SweepFuture:
+    """One submitted sweep of a SweepPipeline: ``result()`` is its own
+    ``ripser_batch`` result (its layers of the coalesced call)."""
+
+    def __init__(self, pipe, lo, hi):
+        self._pipe, self._lo, self._hi = pipe, lo, hi
+        self._call = None  # concurrent future of the coalesced call, once dispatched
+
+    def result(self, timeout=None):
+        if self._call is None:
+            self._pipe._dispatch_pending(self)
+        out = self._call.result(timeout)
+        if isinstance(out, tuple):  # return_time: (results, info)
+            res, info = out
+            return res[self._lo:self._hi], dict(info, coalesced=self._n)
+        return out[self._lo:self._hi]
+
+    def done(self):
+        return self._call is not None and self._call.done()
+
+
 class SweepPipeline:
     """Consecutive layer-loop batches in flight at once: ``depth`` host threads,
     each on its own device workspace slot (streams, buffers, graphs), so batch
     i + 1 runs on the GPU while batch i finishes -- the dense small-N path is a
-    chain of latency-bound kernels that leaves most CUs idle, and two
-    independent sweeps fill them.  ``submit(X)`` returns a future whose
-    ``result()`` is ``ripser_batch(X, **kw)``'s; results come back in
-    submission order when waited on in order.  The ctypes call releases the
-    GIL, so the threads overlap their GPU waits."""
+    chain of latency-bound kernels that leaves most CUs idle, and independent
+    sweeps fill them.  ``submit(X)`` returns a future whose ``result()`` is
+    ``ripser_batch(X, **kw)``'s; results come back in submission order when
+    waited on in order.  The ctypes call releases the GIL, so the threads
+    overlap their GPU waits.
 
-    def __init__(self, depth: int = 2, device: int = 0, **kw):
+    coalesce=c (dynamic batching): up to c consecutive submissions of the same
+    shape, dtype and arguments run as ONE call over their concatenated layers
+    (a layer's result does not depend on the batch it is in:
+    tests/test_gpu_parity.py batch-invariance tests); each future still returns
+    its own sweep's layers.  A batch is dispatched when it holds c sweeps, when
+    a different submission arrives, when one of its futures is waited on, or
+    at flush() / close().
+    run: the batch call (default :func:`ripser_batch`).
+    one_stream: run each call on its slot's one stream (TDA_FLAG_ONE_STREAM),
+    so every slot keeps to one hardware queue; the default is one_stream when
+    depth > 1."""
+
+    def __init__(self, depth: int = 2, device: int = 0, coalesce: int = 1, one_stream=None, run=None, **kw):
+        import threading
         from concurrent.futures import ThreadPoolExecutor
 
         if not 1 <= depth <= _lib.TDA_MAX_SLOTS:
             raise ValueError(f"depth must be in [1, {_lib.TDA_MAX_SLOTS}]")
+        if coalesce < 1:
+            raise ValueError("coalesce must be >= 1")
         self._check_kw(kw)
-        self.depth, self.device, self.kw = depth, device, kw
+        self.depth, self.device, self.coalesce = depth, device, int(coalesce)
+        self.kw = dict(kw, one_stream=depth > 1 if one_stream is None else bool(one_stream))
         self._ex = [ThreadPoolExecutor(max_workers=1) for _ in range(depth)]  # one thread per slot: calls on a slot stay ordered
         self._n = 0
+        self._lock = threading.Lock()
+        self._pending = []  # (X, args, future) not yet dispatched
+        self._pkey = None
+        self._run = run  # the batch call (default ripser_batch; CPU tests pass a stand-in)
 
     @staticmethod
     def _check_kw(kw):
@@ -415,26 +456,74 @@ class SweepPipeline:
             if k in kw:
                 raise TypeError(f"SweepPipeline picks the {k} itself; do not pass {k}=")
 
+    @staticmethod
+    def _key(X, args):
+        dev = (X.device.type, X.device.index) if _is_torch(X) else None
+        return (type(X).__module__, dev, tuple(X.shape[1:]), str(X.dtype), tuple(sorted((k, repr(v)) for k, v in args.items())))
+
     def submit(self, X, **kw):
         self._check_kw(kw)
+        args = dict(self.kw, **kw)
+        if not (_is_torch(X) and X.is_cuda):
+            X = np.asarray(X)
+        if X.ndim != 3:
+            raise ValueError("X must be (L, N, D)")
+        with self._lock:
+            key = self._key(X, args)
+            if self._pending and (key != self._pkey or self.coalesce == 1):
+                self._dispatch_locked()
+            lo = sum(int(p[0].shape[0]) for p in self._pending)
+            f = _SweepFuture(self, lo, lo + int(X.shape[0]))
+            self._pending.append((X, args, f))
+            self._pkey = key
+            if len(self._pending) >= self.coalesce:
+                self._dispatch_locked()
+            return f
+
+    def flush(self):
+        """Dispatch the sweeps still waiting for a full batch."""
+        with self._lock:
+            if self._pending:
+                self._dispatch_locked()
+
+    def _dispatch_pending(self, fut):
+        with self._lock:
+            if fut._call is None:
+                self._dispatch_locked()
+
+    def _dispatch_locked(self):
+        batch, self._pending = self._pending, []
+        run = self._run or ripser_batch
         s = self._n % self.depth
         self._n += 1
-        args = dict(self.kw, **kw)
-        if _is_torch(X) and X.is_cuda:
+        args = dict(batch[0][1])
+        Xs = [b[0] for b in batch]
+        if _is_torch(Xs[0]) and Xs[0].is_cuda:
             # the worker thread's current stream is its own default stream: order the
-            # read after the SUBMITTING thread's current stream (where X was produced)
+            # read after the SUBMITTING thread's current stream (where X -- and the
+            # concatenation below -- were produced)
             import torch
 
-            caller = torch.cuda.current_stream(X.device)
+            caller = torch.cuda.current_stream(Xs[0].device)
+            if len(Xs) > 1:
+                X = torch.cat([x.contiguous() for x in Xs])
+                args["input_ready"] = False  # the concatenation is still in flight on the caller's stream
+            else:
+                X = Xs[0]
 
             def call():
                 with torch.cuda.stream(caller):
-                    return ripser_batch(X, device=self.device, slot=s, **args)
+                    return run(X, device=self.device, slot=s, **args)
 
-            return self._ex[s].submit(call)
-        return self._ex[s].submit(ripser_batch, X, device=self.device, slot=s, **args)
+            cf = self._ex[s].submit(call)
+        else:
+            X = Xs[0] if len(Xs) == 1 else np.concatenate(Xs)
+            cf = self._ex[s].submit(run, X, device=self.device, slot=s, **args)
+        for _, _, f in batch:
+            f._call, f._n = cf, len(batch)
 
     def close(self):
+        self.flush()
         for e in self._ex:
             e.shutdown(wait=True)
 

@@ -1,4 +1,5 @@
 """CPU tests of the host-side mirror of the reference interface (no GPU)."""
+import importlib
 import numpy as np
 import pytest
 
@@ -170,3 +171,45 @@ def test_sweep_pipeline_rejects_slot_and_device_kwargs(pkg):
             pipe.submit(np.zeros((1, 4, 3), np.float32), slot=3)
         with pytest.raises(TypeError):
             pipe.submit(np.zeros((1, 4, 3), np.float32), device=0)
+
+
+def test_sweep_pipeline_coalesces_and_slices(pkg, monkeypatch):
+    """Dynamic batching (SweepPipeline(coalesce=c)): consecutive sweeps of the
+    same shape and arguments become one call over their concatenated layers,
+    each future returns exactly its own layers, a different shape or a wait
+    on a pending future dispatches the batch early.  The library call is
+    replaced by a recorder here (no GPU): layer results are the layers' ids."""
+    rip = importlib.import_module("tda-multimodal_amd.ripser")
+    calls = []
+
+    def fake(X, device=0, slot=0, return_time=False, **kw):
+        calls.append((X.shape[0], slot, kw.get("one_stream")))
+        out = [float(x[0, 0]) for x in X]
+        return (out, {"device_ms": 1.0}) if return_time else out
+
+    monkeypatch.setattr(rip, "ripser_batch", fake)
+
+    def sweep(i, L=3, N=5):
+        X = np.zeros((L, N, 3), np.float32)
+        X[:, 0, 0] = 100 * i + np.arange(L)
+        return X
+
+    with pkg.SweepPipeline(depth=2, coalesce=3, maxdim=1) as pipe:
+        futs = [pipe.submit(sweep(i)) for i in range(7)]          # 3 + 3 dispatched, 1 pending
+        odd = pipe.submit(sweep(9, L=2, N=6))                       # new shape: the pending one goes alone
+        outs = [f.result() for f in futs]
+        assert odd.result() == [900.0, 901.0]
+        f_last = pipe.submit(sweep(10))
+        assert f_last.result() == [1000.0, 1001.0, 1002.0]         # a wait dispatches a partial batch
+    for i, o in enumerate(outs):
+        assert o == [100.0 * i + k for k in range(3)]
+    assert [c[0] for c in calls] == [9, 9, 3, 2, 3]
+    assert [c[1] for c in calls] == [0, 1, 0, 1, 0]                 # batches go round the slots
+    assert all(c[2] is True for c in calls)                          # depth > 1: one stream per slot
+    with pkg.SweepPipeline(depth=1, coalesce=2, maxdim=1, return_time=True) as pipe:
+        a, b = pipe.submit(sweep(1)), pipe.submit(sweep(2))
+        (ra, ia), (rb, ib) = a.result(), b.result()
+        assert ra == [100.0, 101.0, 102.0] and rb == [200.0, 201.0, 202.0] and ia["coalesced"] == 2
+    assert calls[-1] == (6, 0, False)
+    with pytest.raises(ValueError):
+        pkg.SweepPipeline(depth=2, coalesce=0)

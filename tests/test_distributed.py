@@ -71,6 +71,14 @@ def _worker(rank, world, port, q, case):
         rows, cap = sweep.close()
         if rank == 0:
             out["pipelined"] = ([pipe.unpack_record(v, cap) for v in rows], sweep.steps)
+    elif case == "coalesced":  # the same loop with each step's shard through a 2-slot, 2-step SweepPipeline
+        clouds = pkg.synthetic.reference_clouds()
+        sweep = pkg.distributed.PipelinedSweep(clouds, 1, rank, world, run=_oracle_run, slots=2, coalesce=2)
+        for _ in range(3):
+            sweep.step()
+        rows, cap = sweep.close()
+        if rank == 0:
+            out["coalesced"] = ([pipe.unpack_record(v, cap) for v in rows], sweep.steps)
     else:  # many H1 bars on one rank only: the capacity all-reduce re-pads the other
         X = np.stack([pkg.synthetic.torus(260, seed=7), _circle(260)])
         rows, cap = pkg.distributed.sharded_sweep_step(X, 1, rank, world, run=_oracle_run)
@@ -165,3 +173,11 @@ def test_pipelined_sweep_worker_error_does_not_deadlock():
     t.join(60)
     assert not t.is_alive(), "PipelinedSweep deadlocked after a worker error"
     assert done.get("raised"), "the worker's error was swallowed"
+
+
+def test_two_rank_coalesced_pipelined_steps_match_reference(summary_stats):
+    """bench.py's multi-GPU loop with dynamic batching: every rank's steps go
+    through a SweepPipeline (2 slots, 2 steps per call); the exchanges still
+    run in step order and the last one equals the reference's records."""
+    recs, steps = _run("coalesced")["coalesced"]
+    assert steps == 3 and recs == summary_stats

@@ -19,6 +19,12 @@ TOL = 1e-5  # north_star tolerance on filtration values
 
 @pytest.fixture(scope="module")
 def gpu(pkg, built_lib):
+    # torch ships its own HIP runtime: a process that hands torch CUDA tensors to
+    # the library initialises torch's device first (as any torch pipeline does)
+    # -- INTEGRATION.md, "torch and the HIP runtime"
+    import torch
+
+    torch.cuda.init()
     L = pkg.lib()
     assert L.tda_device_ok(0) == 1, "no gfx950 device visible"
     return pkg
@@ -667,6 +673,31 @@ def test_workspace_slots_run_concurrently_with_identical_results(gpu):
                 assert all(np.array_equal(a, b) for a, b in zip(out[l].dgms, ref[l].dgms))
     with pytest.raises(ValueError):
         gpu.ripser_batch(X, maxdim=1, slot=8)
+
+
+def test_coalesced_pipeline_equals_one_call_per_sweep(gpu):
+    """Dynamic batching (SweepPipeline(coalesce=4), the bench's pipelined
+    headline): different sweeps submitted one by one and run as 128-layer
+    calls on one-stream slots return, per future, bit-identical diagrams,
+    indices and checksums to one call per sweep -- for HBM-resident torch
+    inputs (concatenated on the device) and numpy inputs."""
+    import torch
+
+    base = gpu.synthetic.sweep48(32)
+    rng = np.random.default_rng(5)
+    sweeps = [base[rng.permutation(32)] + np.float32(0.01 * i) for i in range(9)]
+    refs = [gpu.ripser_batch(X, maxdim=2) for X in sweeps]
+    for as_torch in (True, False):
+        with gpu.SweepPipeline(depth=3, coalesce=4, maxdim=2) as pipe:
+            futs = [pipe.submit(torch.from_numpy(X).cuda() if as_torch else X) for X in sweeps]
+            outs = [f.result() for f in futs]
+        for out, ref in zip(outs, refs):
+            assert len(out) == 32
+            for l in range(32):
+                assert out[l].checksum == ref[l].checksum
+                assert all(np.array_equal(a, b) for a, b in zip(out[l].dgms, ref[l].dgms))
+                assert all(np.array_equal(a, b) for a, b in zip(out[l].birth_idx, ref[l].birth_idx))
+                assert all(np.array_equal(a, b) for a, b in zip(out[l].death_idx, ref[l].death_idx))
 
 
 def test_slot_growth_while_another_slot_captures(gpu, oracle):
