@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TDA_RIPS_ABI_VERSION 5
+#define TDA_RIPS_ABI_VERSION 6
 
 /* error codes */
 #define TDA_OK 0
@@ -88,9 +88,19 @@ typedef struct tda_rips_args {
      * concurrently on the GPU -- e.g. consecutive sweeps of a layer loop in
      * flight at once; calls on one slot are serialised. */
     int32_t slot;
+    /* ABI >= 6: input in parts (dynamic batching of consecutive sweeps).  When
+     * n_parts > 0, x is ignored and the L layers are the concatenation of the
+     * n_parts arrays x_parts[0 .. n_parts-1], each (L / n_parts, N, D) (or
+     * (L / n_parts, N, N) with is_dist), all in host memory or all on `device`
+     * as x_on_device says.  The library gathers them into its own buffer (one
+     * copy kernel on its stream, after the caller's stream), so the captured
+     * graph reads one stable address whatever the parts' addresses are. */
+    const void *const *x_parts;
+    int32_t n_parts;
 } tda_rips_args;
 
 #define TDA_MAX_SLOTS 8
+#define TDA_MAX_PARTS 16
 
 /* per (layer, dim) emitted persistence pairs, in the reference's emission
  * order: H0 = Kruskal order of the finite deaths then one [0, inf) per

@@ -43,6 +43,8 @@ class RipsArgs(ctypes.Structure):
         ("twonn_eps", ctypes.c_float),
         ("twonn_discard", ctypes.c_double),
         ("slot", ctypes.c_int32),
+        ("x_parts", ctypes.c_void_p),  # ABI 6: const void* const* (dynamic batching)
+        ("n_parts", ctypes.c_int32),
     ]
 
 
@@ -88,6 +90,7 @@ TDA_FLAG_DIST64 = 4
 TDA_FLAG_NO_PERSISTENCE = 8
 TDA_FLAG_ONE_STREAM = 16
 TDA_MAX_SLOTS = 8
+TDA_MAX_PARTS = 16
 
 
 class UmapArgs(ctypes.Structure):  # include/tda_umap.h

@@ -454,6 +454,8 @@ struct Workspace {
     hipEvent_t evin = nullptr;         // caller's stream -> library stream
     char* hin = nullptr;               // pinned staging of host inputs (stable graph source)
     size_t hin_cap = 0;
+    void* xin = nullptr;  // gathered device input parts (ABI 6 x_parts)
+    size_t xin_cap = 0;
     uint64_t gen = 0;                  // bumped whenever a buffer baked into graphs moves
     std::vector<struct GraphEntry> graphs;
     // the configuration a retry ended on (larger pools / another reducer), per
@@ -749,6 +751,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 
     // host inputs go through a pinned staging buffer: a stable graph source
     const void* xsrc = host_or_dev;
+    const int nparts = input_kind == 2 ? 0 : a.n_parts;
     if (!a.x_on_device || input_kind == 2) {
         const size_t xbytes = input_kind == 2 ? binom((uint64_t)n, 2) * 4
                                               : (size_t)L * n * (input_kind == 1 ? (size_t)n : (size_t)p.D) * esz;
@@ -759,8 +762,31 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipHostMalloc((void**)&w.hin, std::max<size_t>(xbytes, 1 << 16), hipHostMallocDefault));
             w.hin_cap = std::max<size_t>(xbytes, 1 << 16);
         }
-        if (xbytes) std::memcpy(w.hin, host_or_dev, xbytes);
+        if (nparts > 0) {  // parts: one after the other into the staging buffer
+            const size_t pb = xbytes / nparts;
+            for (int i = 0; i < nparts; ++i) std::memcpy((char*)w.hin + i * pb, a.x_parts[i], pb);
+        } else if (xbytes) {
+            std::memcpy(w.hin, host_or_dev, xbytes);
+        }
         xsrc = w.hin;
+    } else if (nparts > 0) {
+        // device parts: gathered into the workspace's own input buffer by one kernel on the
+        // library stream (ordered after the caller's stream above, outside any captured graph)
+        const size_t xbytes = (size_t)L * n * (input_kind == 1 ? (size_t)n : (size_t)p.D) * esz;
+        if (w.xin_cap < xbytes) {
+            drop_graphs(w);
+            if (w.xin) HIPC(hipFree(w.xin));
+            w.xin = nullptr;
+            HIPC(hipMalloc(&w.xin, xbytes));
+            w.xin_cap = xbytes;
+        }
+        PartList pl = {};
+        for (int i = 0; i < nparts; ++i) pl.p[i] = a.x_parts[i];
+        const uint64_t words = xbytes / nparts / 4;
+        const unsigned gx = (unsigned)std::min<uint64_t>(64, (words + 255) / 256);
+        hipLaunchKernelGGL(k_gather_parts, dim3(std::max(1u, gx), nparts), dim3(256), 0, s, pl, words, (uint32_t*)w.xin);
+        HIPC(hipGetLastError());
+        xsrc = w.xin;
     }
 
     // silhouette labels -> host-mapped buffer (stable address: a graph source)
@@ -1878,7 +1904,15 @@ int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_
 
 int validate(const tda_rips_args* a) {
     if (!a) return fail(TDA_E_INVALID, "args is NULL");
-    if (!a->x && a->L * a->N > 0) return fail(TDA_E_INVALID, "x is NULL");
+    if (a->n_parts < 0 || a->n_parts > TDA_MAX_PARTS) return fail(TDA_E_INVALID, "n_parts must be in [0, TDA_MAX_PARTS]");
+    if (a->n_parts > 0) {
+        if (!a->x_parts) return fail(TDA_E_INVALID, "x_parts is NULL");
+        for (int i = 0; i < a->n_parts; ++i)
+            if (!a->x_parts[i]) return fail(TDA_E_INVALID, "x_parts[" + std::to_string(i) + "] is NULL");
+        if (a->L % a->n_parts) return fail(TDA_E_INVALID, "L must be a multiple of n_parts");
+    } else if (!a->x && a->L * a->N > 0) {
+        return fail(TDA_E_INVALID, "x is NULL");
+    }
     if (a->L < 1) return fail(TDA_E_INVALID, "L must be >= 1");
     if (a->N < 1) return fail(TDA_E_INVALID, "N must be >= 1");
     if (!a->is_dist && a->D < 1) return fail(TDA_E_INVALID, "D must be >= 1");

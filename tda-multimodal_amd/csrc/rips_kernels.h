@@ -1640,6 +1640,20 @@ __global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict_
     }
 }
 
+// ------------------------------------------------------------------ input parts
+// ABI 6 x_parts: the parts of a dynamically batched call, gathered into the
+// workspace's input buffer (part k -> words [k * part_words, (k + 1) * part_words))
+struct PartList {
+    const void* p[TDA_MAX_PARTS];
+};
+__global__ __launch_bounds__(256) void k_gather_parts(PartList pl, uint64_t part_words, uint32_t* __restrict__ dst) {
+    const int k = blockIdx.y;
+    const uint32_t* src = (const uint32_t*)pl.p[k];
+    uint32_t* d = dst + (size_t)k * part_words;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < part_words; i += (uint64_t)gridDim.x * blockDim.x)
+        st_glb(d, i, ld_glb(src, i));
+}
+
 // ------------------------------------------------------------------ sort residual
 struct SortArgs {
     uint64_t* resid[3];

@@ -59,10 +59,11 @@ def _global_cap(local_cap: int, dist, device) -> int:
     return int(t.item())
 
 
-def gather_packed(packed: np.ndarray, local_cap: int, n_layers: int, dist=None, device=None):
+def gather_packed(packed: np.ndarray, local_cap: int, n_layers: int, dist=None, device=None, per: int | None = None):
     """All-reduce the value capacity, then gather every rank's packed rows
     (``pipeline.pack_results`` output) to rank 0; returns the (n_layers, ...)
-    rows sorted by layer on rank 0, None elsewhere."""
+    rows sorted by layer on rank 0, None elsewhere.  per: rows per rank in
+    the gather buffer (default ceil(n_layers / world))."""
     import torch.distributed as tdist
 
     dist = dist or tdist
@@ -70,7 +71,7 @@ def gather_packed(packed: np.ndarray, local_cap: int, n_layers: int, dist=None, 
     cap = _global_cap(local_cap, dist, device)
     if packed.shape[1] != rec_len(cap):  # re-pad to the global capacity
         packed = _repad(packed, local_cap, cap)
-    per = -(-n_layers // world)
+    per = per or -(-n_layers // world)
     rows = _gather_packed(packed, per, cap, dist, device)
     if rows is None:
         return None
@@ -146,7 +147,9 @@ class PipelinedSweep:
     slots / coalesce > 1: each step's shard goes through a
     :class:`~ripser.SweepPipeline` (``coalesce`` consecutive steps per call,
     ``slots`` calls in flight) -- what the one-GPU bench times -- and the
-    worker exchanges the steps' records in step order as their calls finish.
+    worker exchanges the records of every ``coalesce`` consecutive steps in
+    one capacity all-reduce + gather (layer ids offset by the step's place in
+    the group; every rank groups the same steps), in step order.
     """
 
     def __init__(self, X, maxdim: int, rank: int, world: int, dist=None, device=None, layer_base: int = 0,
@@ -171,10 +174,19 @@ class PipelinedSweep:
             from .ripser import SweepPipeline
 
             gpu = getattr(X, "is_cuda", False)
-            prun = None if run is None else (lambda Xs, maxdim, **_: run(Xs, maxdim))
+            def prun(Xs, maxdim, **_):  # a stand-in batch call takes one array: join the parts
+                if isinstance(Xs, list):
+                    Xs = np.concatenate([np.asarray(x) for x in Xs]) if not getattr(Xs[0], "is_cuda", False) else \
+                        __import__("torch").cat(Xs)
+                return run(Xs, maxdim)
+
+            prun = None if run is None else prun
             self.pipe = SweepPipeline(depth=slots, device=X.device.index if gpu else 0, coalesce=coalesce, maxdim=maxdim,
                                       run=prun)
         self.q = queue.Queue(maxsize=max(1, depth) + (slots * coalesce if self.pipe else 0))
+        self.group = coalesce if self.pipe else 1  # steps per exchange
+        self.world = world
+        self.layer_base = layer_base if shard else 0
         self.last, self.err, self.steps = (None, None), None, 0
         self.thread = threading.Thread(target=self._worker, daemon=True)
         self.thread.start()
@@ -184,20 +196,38 @@ class PipelinedSweep:
             import torch
 
             torch.cuda.set_device(self.device)  # the current device is per thread
+        group, gids = [], []
         while True:
             res = self.q.get()
             if res is None:
+                if group and self.err is None:
+                    self._exchange(group, gids)
                 return
             if self.err is not None:  # after a failure: keep draining, so step() / close() never block on a full queue
                 continue
             try:
                 if hasattr(res, "result"):  # a SweepPipeline future: this step's own layers, in step order
                     res = res.result()
-                packed, cap = pack_results(res, self.ids, self.maxdim)
-                out = gather_packed(packed, cap, self.total, self.dist, self.device)
-                self.last = out if out is not None else (None, None)
+                gids.append(self.ids + len(gids) * self.total)  # the step's place in its exchange group
+                group.extend(res)
+                if len(gids) == self.group:
+                    self._exchange(group, gids)
+                    group, gids = [], []
             except BaseException as e:  # re-raised by the next step() or close()
                 self.err = e
+
+    def _exchange(self, group, gids):
+        k = len(gids)
+        packed, cap = pack_results(group, np.concatenate(gids), self.maxdim)
+        out = gather_packed(packed, cap, k * self.total, self.dist, self.device,
+                            per=k * -(-self.total // self.world))
+        if out is None:
+            self.last = (None, None)
+            return
+        rows, cap = out
+        last = rows[rows[:, 0] >= self.layer_base + (k - 1) * self.total].copy()  # the group's last step
+        last[:, 0] -= (k - 1) * self.total
+        self.last = (last, cap)
 
     def step(self):
         if self.err is not None:

@@ -218,6 +218,43 @@ def encode_labels(label_sets, n: int) -> np.ndarray:
     return np.ascontiguousarray(np.stack(rows)) if rows else np.zeros((0, n), np.int32)
 
 
+def _prep_input(X, input_ready: bool):
+    """One input array -> (contiguous array kept alive, on_device, device,
+    is_f64, caller stream handle or 0)."""
+    if _is_torch(X) and X.is_cuda:
+        import torch
+
+        if X.dim() != 3:
+            raise ValueError("X must be (L, N, D)")
+        if X.dtype not in (torch.float32, torch.float64):
+            X = X.to(torch.float64)
+        keep = X.contiguous()
+        device = keep.device.index if keep.device.index is not None else torch.cuda.current_device()
+        stream = 0
+        # input_ready: the caller has synchronised after producing X, so no
+        # device-side ordering on its stream (whose queue a pipeline slot may share)
+        if not input_ready:
+            # torch's current stream on that device (raw handle: no Stream object per call)
+            raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+            stream = raw_stream(device) if raw_stream else torch.cuda.current_stream(keep.device).cuda_stream
+        return keep, True, device, keep.dtype == torch.float64, stream
+    if _is_torch(X):
+        X = X.detach().cpu().numpy()
+    X = np.asarray(X)
+    if X.ndim != 3:
+        raise ValueError("X must be (L, N, D)")
+    if X.dtype not in (np.float32, np.float64):
+        X = X.astype(np.float64)
+    keep = np.ascontiguousarray(X)
+    if not np.all(np.isfinite(keep)):
+        raise ValueError("Input contains NaN or infinity.")
+    return keep, False, None, keep.dtype == np.float64, 0
+
+
+def _data_ptr(keep):
+    return keep.data_ptr() if _is_torch(keep) else keep.ctypes.data
+
+
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
                  want_dist: bool = False, return_time: bool = False, stage_times: bool = False, labels=None,
                  stage_serial: bool = False, twonn: bool = False, discard_fraction: float = 0.1, eps: float = 1e-10,
@@ -227,7 +264,10 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
 
     X: (L, N, D) point clouds or (L, N, N) distance matrices (distance_matrix=True);
        numpy array on the host, or a contiguous torch CUDA tensor (consumed in
-       place, ordered on torch's current stream).
+       place, ordered on torch's current stream); or a list of up to
+       TDA_MAX_PARTS such arrays of one shape (consecutive sweeps of a
+       dynamically batched call): their layers are processed as one batch
+       (the library gathers them on the device; ABI 6 ``x_parts``).
     Returns a list of ``LayerResult``; with return_time also a dict
     {"device_ms", "stages": [(name, ms), ...]} (stages filled when stage_times,
     timed with HIP events on the library's stream).
@@ -253,43 +293,40 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     """
     _check_common(maxdim, 2, False, None, "euclidean")
     a = _lib.RipsArgs()
-    if _is_torch(X) and X.is_cuda:
-        import torch
-
-        if X.dim() != 3:
-            raise ValueError("X must be (L, N, D)")
-        if X.dtype not in (torch.float32, torch.float64):
-            X = X.to(torch.float64)
-        keep = X.contiguous()
-        a.x = keep.data_ptr()
-        a.x_on_device = 1
-        device = keep.device.index if keep.device.index is not None else torch.cuda.current_device()
-        # torch's current stream on that device (raw handle: no Stream object per call)
-        raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
-        # input_ready: the caller has synchronised after producing X, so no
-        # device-side ordering on its stream (whose queue a pipeline slot may share)
-        if not input_ready:
-            a.stream = raw_stream(device) if raw_stream else torch.cuda.current_stream(keep.device).cuda_stream
-        dtype_is64 = keep.dtype == torch.float64
+    parts = list(X) if isinstance(X, (list, tuple)) else None
+    if parts is not None:  # ABI 6 x_parts: consecutive sweeps of one dynamically batched call
+        if not 1 <= len(parts) <= _lib.TDA_MAX_PARTS:
+            raise ValueError(f"X as parts needs 1 .. {_lib.TDA_MAX_PARTS} arrays")
+        kept = [_prep_input(x, input_ready) for x in parts]
+        k0 = kept[0]
+        for k in kept[1:]:
+            if k[0].shape != k0[0].shape or k[1:4] != k0[1:4]:
+                raise ValueError("parts must share shape, dtype and device")
+        keep_parts = [k[0] for k in kept]
+        ptrs = (ctypes.c_void_p * len(parts))(*[_data_ptr(k) for k in keep_parts])
+        a.x_parts = ctypes.cast(ptrs, ctypes.c_void_p)
+        a.n_parts = len(parts)
+        keep = k0[0]
+        on_dev, device_p, dtype_is64, stream = k0[1], k0[2], k0[3], k0[4]
+        a.x_on_device = 1 if on_dev else 0
+        if on_dev:
+            device = device_p
+            a.stream = stream or None
+        Lp = int(keep.shape[0])
+        shape = (Lp * len(parts),) + tuple(keep.shape[1:])
     else:
-        if _is_torch(X):
-            X = X.detach().cpu().numpy()
-        X = np.asarray(X)
-        if X.ndim != 3:
-            raise ValueError("X must be (L, N, D)")
-        if X.dtype not in (np.float32, np.float64):
-            X = X.astype(np.float64)
-        keep = np.ascontiguousarray(X)
-        if not np.all(np.isfinite(keep)):
-            raise ValueError("Input contains NaN or infinity.")
-        a.x = keep.ctypes.data
-        a.x_on_device = 0
-        dtype_is64 = keep.dtype == np.float64
-    L, N = int(keep.shape[0]), int(keep.shape[1])
-    if distance_matrix and keep.shape[2] != N:
+        keep, on_dev, device_p, dtype_is64, stream = _prep_input(X, input_ready)
+        a.x = _data_ptr(keep)
+        a.x_on_device = 1 if on_dev else 0
+        if on_dev:
+            device = device_p
+            a.stream = stream or None
+        shape = tuple(keep.shape)
+    L, N = int(shape[0]), int(shape[1])
+    if distance_matrix and shape[2] != N:
         raise ValueError("Distance matrix is not square")
     a.dtype = _lib.TDA_F64 if dtype_is64 else _lib.TDA_F32
-    a.L, a.N, a.D = L, N, int(keep.shape[2])
+    a.L, a.N, a.D = L, N, int(shape[2])
     a.is_dist = 1 if distance_matrix else 0
     a.maxdim = int(maxdim)
     a.thresh = float(thresh) if np.isfinite(thresh) else float("inf")
@@ -422,6 +459,8 @@ class SweepPipeline:
 
     coalesce=c (dynamic batching): up to c consecutive submissions of the same
     shape, dtype and arguments run as ONE call over their concatenated layers
+    (passed as parts: the library gathers them into its own input buffer, so
+    the slot's captured graph is reused whatever the inputs' addresses)
     (a layer's result does not depend on the batch it is in:
     tests/test_gpu_parity.py batch-invariance tests); each future still returns
     its own sweep's layers.  A batch is dispatched when it holds c sweeps, when
@@ -438,8 +477,8 @@ class SweepPipeline:
 
         if not 1 <= depth <= _lib.TDA_MAX_SLOTS:
             raise ValueError(f"depth must be in [1, {_lib.TDA_MAX_SLOTS}]")
-        if coalesce < 1:
-            raise ValueError("coalesce must be >= 1")
+        if not 1 <= coalesce <= _lib.TDA_MAX_PARTS:
+            raise ValueError(f"coalesce must be in [1, {_lib.TDA_MAX_PARTS}]")
         self._check_kw(kw)
         self.depth, self.device, self.coalesce = depth, device, int(coalesce)
         self.kw = dict(kw, one_stream=depth > 1 if one_stream is None else bool(one_stream))
@@ -505,11 +544,7 @@ class SweepPipeline:
             import torch
 
             caller = torch.cuda.current_stream(Xs[0].device)
-            if len(Xs) > 1:
-                X = torch.cat([x.contiguous() for x in Xs])
-                args["input_ready"] = False  # the concatenation is still in flight on the caller's stream
-            else:
-                X = Xs[0]
+            X = Xs[0] if len(Xs) == 1 else Xs  # parts: gathered on the device by the library (ABI 6)
 
             def call():
                 with torch.cuda.stream(caller):
@@ -517,7 +552,7 @@ class SweepPipeline:
 
             cf = self._ex[s].submit(call)
         else:
-            X = Xs[0] if len(Xs) == 1 else np.concatenate(Xs)
+            X = Xs[0] if len(Xs) == 1 else Xs
             cf = self._ex[s].submit(run, X, device=self.device, slot=s, **args)
         for _, _, f in batch:
             f._call, f._n = cf, len(batch)

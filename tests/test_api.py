@@ -183,6 +183,8 @@ def test_sweep_pipeline_coalesces_and_slices(pkg, monkeypatch):
     calls = []
 
     def fake(X, device=0, slot=0, return_time=False, **kw):
+        if isinstance(X, list):  # a coalesced call hands its sweeps over as parts (ABI 6 x_parts)
+            X = np.concatenate(X)
         calls.append((X.shape[0], slot, kw.get("one_stream")))
         out = [float(x[0, 0]) for x in X]
         return (out, {"device_ms": 1.0}) if return_time else out
@@ -213,3 +215,20 @@ def test_sweep_pipeline_coalesces_and_slices(pkg, monkeypatch):
     assert calls[-1] == (6, 0, False)
     with pytest.raises(ValueError):
         pkg.SweepPipeline(depth=2, coalesce=0)
+    with pytest.raises(ValueError):
+        pkg.SweepPipeline(depth=2, coalesce=17)
+
+
+def test_ripser_batch_parts_validation(pkg):
+    """ABI 6 input parts: a list of arrays is one dynamically batched call;
+    parts of different shapes or dtypes, or more than TDA_MAX_PARTS of them,
+    are refused before any device work."""
+    a = np.zeros((2, 5, 3), np.float32)
+    with pytest.raises(ValueError):
+        pkg.ripser_batch([a, np.zeros((3, 5, 3), np.float32)], maxdim=1)
+    with pytest.raises(ValueError):
+        pkg.ripser_batch([a, a.astype(np.float64)], maxdim=1)
+    with pytest.raises(ValueError):
+        pkg.ripser_batch([a] * 17, maxdim=1)
+    with pytest.raises(ValueError):
+        pkg.ripser_batch([a, np.full((2, 5, 3), np.nan, np.float32)], maxdim=1)
