@@ -79,7 +79,10 @@ CALL_KW = {"raw4096": {"twonn": True}}
 # flight fill them (r04, tools/ab_coalesce.sh: 148 K layers/s one call at a time -> 217 K coalescing 4,
 # 305 K with 2 in flight, 455 K with 4).  Every record also carries the one-call-at-a-time figure
 # (pipeline.sequential).  sweep48_L4 stays one call at a time: it is the per-call latency record.
-PIPE = {"sweep48": (4, 4), "sweep48_host": (4, 4), "sweep48_L4": (1, 1)}  # workload -> (depth, coalesce)
+# grid144 (parallel reducer) and raw4096 (distance + H0 + TwoNN) gain from calls in flight but not from wider
+# calls (r04: grid144 5.60 K -> 7.54 K layers/s with 3 in flight; raw4096 120 K -> 148 K with 4).
+PIPE = {"sweep48": (4, 4), "sweep48_host": (4, 4), "sweep48_L4": (1, 1), "grid144": (3, 1), "raw4096": (4, 1),
+        "torus1024x32": (1, 1)}  # workload -> (depth, coalesce); (1, 1): one call at a time (env A/B only)
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
 CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
 
@@ -267,7 +270,9 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     X = X_host if host_in else torch.from_numpy(X_host).to(dev)
     torch.cuda.synchronize()
     kw = dict(CALL_KW.get(name, {}))
-    if os.environ.get("TDA_BENCH_READY") == "1" and not host_in:  # X was synchronised above
+    if os.environ.get("TDA_BENCH_READY", "1") == "1" and not host_in:
+        # X was synchronised above (resident in HBM before the timed region): no per-call event on
+        # torch's stream, whose hardware queue a pipeline slot may share (TDA_BENCH_READY=0: with it)
         kw["input_ready"] = True
     depth, coalesce = PIPE.get(name, (1, 1))
     depth = int(os.environ.get("TDA_BENCH_DEPTH", depth)) if name in PIPE else 1
@@ -278,29 +283,33 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     dev_index = dev.index if dev.index is not None else 0
     seq = None
     piped = depth > 1 or coalesce > 1
-    if piped:  # the one-call-at-a-time figure next to the pipelined one
+    if piped and os.environ.get("TDA_BENCH_NO_SEQ") != "1":  # the one-call-at-a-time figure next to the pipelined one
+        # (TDA_BENCH_NO_SEQ=1: profiling runs, so every launch in the trace is the pipeline's batch)
         el_s, dm_s = _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, 1, host_in, dev_index)
         seq = {"value": L * steps / el_s, "ms_per_step": el_s / steps * 1e3, "device_ms_per_step": sum(dm_s) / len(dm_s)}
     el, dev_ms = _timed_steps(pkg, torch, X, maxdim, kw_pipe if piped else kw, steps, warmup, depth, host_in, dev_index, coalesce)
     # per-kernel durations: HIP events around every kernel with all stages on
     # ONE stream (each interval brackets exactly one kernel), same batch,
     # after the timed region; the dominant kernel has the largest mean
+    # (a coalesced pipeline launches every kernel over `coalesce` sweeps: the stage pass runs that batch too)
+    Xst, Lk = ([X] * coalesce, L * coalesce) if coalesce > 1 else (X, L)
     acc: dict = {}
+    pkg.ripser_batch(Xst, maxdim=maxdim, stage_times=True, stage_serial=True, **kw)  # untimed: first use of this schedule
     for _ in range(max(1, min(steps, 10))):
-        _, info = pkg.ripser_batch(X, maxdim=maxdim, return_time=True, stage_times=True, stage_serial=True, **kw)
+        _, info = pkg.ripser_batch(Xst, maxdim=maxdim, return_time=True, stage_times=True, stage_serial=True, **kw)
         for k, ms in info["stages"]:
             acc.setdefault(k, []).append(ms)
-    stages = {k: sum(v) / len(v) for k, v in acc.items()}
+    stages = {k: float(np.median(v)) for k, v in acc.items()}  # median: one slow outlier (a profiler hiccup) no longer sets it
     kern = {k: v for k, v in stages.items() if k.startswith("k_")}
     dom = max(kern, key=kern.get)
     bpl = algo_bytes_per_layer(n, d, maxdim)
-    achieved = bpl * L / (kern[dom] * 1e-3) / 1e9
+    achieved = bpl * Lk / (kern[dom] * 1e-3) / 1e9
     bound, peak, unit, per_layer = "hbm", HBM_PEAK_GBS, "GB/s", {"algo_bytes_per_layer": bpl}
     if dom in ("k_distance_mfma", "k_gram_layer"):  # 2 N^2 D FP64 FLOPs per layer (Gram) against the FP64 MFMA peak
         fpl = 2 * n * n * d
-        achieved = fpl * L / (kern[dom] * 1e-3) / 1e12
+        achieved = fpl * Lk / (kern[dom] * 1e-3) / 1e12
         bound, peak, unit, per_layer = "mfma", FP64_MFMA_PEAK_TFS, "TFLOP/s", {"algo_flops_per_layer": fpl,
-                                                                              **mfma_executed(n, d, L, kern[dom])}
+                                                                              **mfma_executed(n, d, Lk, kern[dom])}
     traffic = None
     pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
@@ -312,18 +321,18 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     mfma_roof = None
     if gram and gram != dom:  # the FP64 Gram kernel when another kernel dominates (e.g. raw4096: H0)
         fpl = 2 * n * n * d
-        a_tf = fpl * L / (kern[gram] * 1e-3) / 1e12
+        a_tf = fpl * Lk / (kern[gram] * 1e-3) / 1e12
         mfma_roof = {"bound": "mfma", "kernel": gram, "achieved": a_tf, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": a_tf / FP64_MFMA_PEAK_TFS, "traffic": pmc.get(gram, {}).get("hbm_bytes_per_launch"),
-                     "algo_flops_per_layer": fpl, "layers_per_launch": L, "kernel_avg_ms": kern[gram],
-                     **mfma_executed(n, d, L, kern[gram])}
+                     "algo_flops_per_layer": fpl, "layers_per_launch": Lk, "kernel_avg_ms": kern[gram],
+                     **mfma_executed(n, d, Lk, kern[gram])}
     return {
         "value": L * steps / el, "unit": "layers/s", "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warmup,
         "device_ms_per_step": sum(dev_ms) / len(dev_ms), "X_host": X_host, "maxdim": maxdim,
         "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim},
         "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
                      "frac": achieved / peak, "traffic": traffic, **per_layer,
-                     "layers_per_launch": L, "kernel_avg_ms": kern[dom],
+                     "layers_per_launch": Lk, "kernel_avg_ms": kern[dom],
                      "kernel_timing": "HIP events around each kernel on its stream, all stages serialised on one "
                                       "stream, after the timed region (same batch)"},
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},

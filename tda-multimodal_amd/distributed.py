@@ -181,8 +181,14 @@ class PipelinedSweep:
                 return run(Xs, maxdim)
 
             prun = None if run is None else prun
+            extra = {}
+            if gpu and run is None:  # X is fixed for every step: complete it once, then no per-call stream event
+                import torch
+
+                torch.cuda.current_stream(X.device).synchronize()
+                extra["input_ready"] = True
             self.pipe = SweepPipeline(depth=slots, device=X.device.index if gpu else 0, coalesce=coalesce, maxdim=maxdim,
-                                      run=prun)
+                                      run=prun, **extra)
         self.q = queue.Queue(maxsize=max(1, depth) + (slots * coalesce if self.pipe else 0))
         self.group = coalesce if self.pipe else 1  # steps per exchange
         self.world = world

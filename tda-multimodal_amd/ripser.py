@@ -469,7 +469,12 @@ class SweepPipeline:
     run: the batch call (default :func:`ripser_batch`).
     one_stream: run each call on its slot's one stream (TDA_FLAG_ONE_STREAM),
     so every slot keeps to one hardware queue; the default is one_stream when
-    depth > 1."""
+    depth > 1.  The calls run on the top ``depth`` workspace slots (slot 0,
+    where plain ripser_batch calls run, is left alone).
+    input_ready=True (a ripser_batch argument, passed through ``**kw``) is
+    worth giving when the inputs are complete before submission: each call
+    then skips its event on the caller's stream, whose hardware queue a slot
+    may share."""
 
     def __init__(self, depth: int = 2, device: int = 0, coalesce: int = 1, one_stream=None, run=None, **kw):
         import threading
@@ -482,6 +487,9 @@ class SweepPipeline:
         self._check_kw(kw)
         self.depth, self.device, self.coalesce = depth, device, int(coalesce)
         self.kw = dict(kw, one_stream=depth > 1 if one_stream is None else bool(one_stream))
+        # the top `depth` workspace slots: slot 0 (every plain ripser_batch call) keeps its
+        # streams to itself, and the slots' streams each get a hardware queue of their own
+        self.slots = list(range(_lib.TDA_MAX_SLOTS - depth, _lib.TDA_MAX_SLOTS))
         self._ex = [ThreadPoolExecutor(max_workers=1) for _ in range(depth)]  # one thread per slot: calls on a slot stay ordered
         self._n = 0
         self._lock = threading.Lock()
@@ -533,7 +541,8 @@ class SweepPipeline:
     def _dispatch_locked(self):
         batch, self._pending = self._pending, []
         run = self._run or ripser_batch
-        s = self._n % self.depth
+        e = self._n % self.depth  # executor (host thread) of this call
+        s = self.slots[e]
         self._n += 1
         args = dict(batch[0][1])
         Xs = [b[0] for b in batch]
@@ -550,10 +559,10 @@ class SweepPipeline:
                 with torch.cuda.stream(caller):
                     return run(X, device=self.device, slot=s, **args)
 
-            cf = self._ex[s].submit(call)
+            cf = self._ex[e].submit(call)
         else:
             X = Xs[0] if len(Xs) == 1 else Xs
-            cf = self._ex[s].submit(run, X, device=self.device, slot=s, **args)
+            cf = self._ex[e].submit(run, X, device=self.device, slot=s, **args)
         for _, _, f in batch:
             f._call, f._n = cf, len(batch)
 

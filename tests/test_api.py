@@ -206,13 +206,13 @@ def test_sweep_pipeline_coalesces_and_slices(pkg, monkeypatch):
     for i, o in enumerate(outs):
         assert o == [100.0 * i + k for k in range(3)]
     assert [c[0] for c in calls] == [9, 9, 3, 2, 3]
-    assert [c[1] for c in calls] == [0, 1, 0, 1, 0]                 # batches go round the slots
+    assert [c[1] for c in calls] == [6, 7, 6, 7, 6]                 # batches go round the top slots
     assert all(c[2] is True for c in calls)                          # depth > 1: one stream per slot
     with pkg.SweepPipeline(depth=1, coalesce=2, maxdim=1, return_time=True) as pipe:
         a, b = pipe.submit(sweep(1)), pipe.submit(sweep(2))
         (ra, ia), (rb, ib) = a.result(), b.result()
         assert ra == [100.0, 101.0, 102.0] and rb == [200.0, 201.0, 202.0] and ia["coalesced"] == 2
-    assert calls[-1] == (6, 0, False)
+    assert calls[-1] == (6, 7, False)
     with pytest.raises(ValueError):
         pkg.SweepPipeline(depth=2, coalesce=0)
     with pytest.raises(ValueError):

@@ -8,6 +8,7 @@ set -o pipefail
 WL=${1:-sweep48}
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT" || exit 1
+export TDA_BENCH_NO_SEQ=1  # traces hold only the pipelined batch (and its stage pass), not the one-call-at-a-time pass
 mkdir -p gpurun_out
 for C in FETCH_SIZE WRITE_SIZE; do
     rm -rf gpurun_out/pmc_$C

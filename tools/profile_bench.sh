@@ -6,6 +6,7 @@ WL=${1:-sweep48}
 shift
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT" || exit 1
+export TDA_BENCH_NO_SEQ=1  # traces hold only the pipelined batch (and its stage pass), not the one-call-at-a-time pass
 mkdir -p gpurun_out
 rm -rf gpurun_out/prof_$WL
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$WL -o run -- \

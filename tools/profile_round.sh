@@ -8,6 +8,7 @@ set -o pipefail
 TAG=${1:-r03}
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT" || exit 1
+export TDA_BENCH_NO_SEQ=1  # traces hold only the pipelined batch (and its stage pass), not the one-call-at-a-time pass
 mkdir -p gpurun_out/$TAG
 for WL in ${WLS_STATS:-sweep48 grid144 torus1024 torus1024x32 raw4096 sweep48_L4}; do
     rm -rf gpurun_out/prof_$WL
