@@ -41,8 +41,8 @@ METRIC = "layers/sec (pairwise-dist + VR persistence H0-H2) at 1/2/4/8 MI355X"
 
 WORKLOADS = {
     # name: (layers, maxdim, description, default steps, default warmup)
-    "sweep48": (32, 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2", 50, 5),
-    "grid144": (32, 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2", 10, 2),
+    "sweep48": (32, 2, "qwen-vl 32-layer sweep x 48 points (configs[1] per layer), D=3, H0-H2", 400, 5),
+    "grid144": (32, 2, "12x12 torus grid x 32 layers (configs[4]), N=144, D=3, H0-H2", 30, 2),
     "torus1024": (1, 1, "S1xS1 torus N=1024 (configs[3]), D=3, H0-H1", 5, 2),
     # configs[3]'s cloud as a sweep: 32 tori (seeds 0..31) per call, like the reference's 32-layer loop --
     # the GPU's layers in flight against the CPU baseline's layers in flight (one per worker process)
@@ -52,12 +52,12 @@ WORKLOADS = {
     "sweep48x4": (128, 2, "4 x the qwen-vl 32-layer sweep x 48 points in one call (128 layers), D=3, H0-H2", 50, 5),
     # SURVEY 8(d) as written: host numpy array in, every layer's dgms list materialised on the host in the timed loop
     "sweep48_host": (32, 2, "qwen-vl 32-layer sweep x 48 points, D=3, H0-H2: numpy (32, 48, 3) in, per-layer dgms lists out "
-                            "(host-array-in -> diagrams-on-host-out, debug_tda_pipeline.py:104-110)", 50, 5),
+                            "(host-array-in -> diagrams-on-host-out, debug_tda_pipeline.py:104-110)", 400, 5),
     # configs[2]'s per-GPU share: 4 of the 32 layers in one call (8 GPUs, strong scaling)
     "sweep48_L4": (4, 2, "4 layers x 48 points per call (configs[2]'s per-GPU share at 8 GPUs), D=3, H0-H2", 100, 10),
     # raw hidden states (no UMAP): distance on the FP64 matrix cores + TwoNN + H0
     "raw4096": (32, 0, "32 layers x 144 tokens x 4096 raw hidden-state features: distance (FP64 MFMA) + H0 + TwoNN "
-                       "intrinsic dimension (metrics.py:113-208)", 20, 3),
+                       "intrinsic dimension (metrics.py:113-208)", 100, 3),
 }
 DATA = {
     "sweep48": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
@@ -372,8 +372,8 @@ def measure_umap(pkg, torch, dev, steps: int = 10, warmup: int = 2) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None, help="default: the workload's own (WORKLOADS)")
+    ap.add_argument("--warmup", type=int, default=None, help="default: the workload's own (WORKLOADS)")
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
     ap.add_argument("--extra", default="sweep48_host,sweep48_L4,grid144,torus1024,torus1024x32,raw4096,umap36,sweep48x4",
@@ -383,6 +383,10 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: every rank runs its own L-layer batch; strong: the L layers are sharded over ranks")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = WORKLOADS[args.workload][3]
+    if args.warmup is None:
+        args.warmup = WORKLOADS[args.workload][4]
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
