@@ -249,7 +249,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par,
         p.n2p = (uint32_t)align_up(N * N, 8);
         p.bm_words = (uint32_t)((binom(N, 4) + 31) / 32 + 1);
         p.p1_lds = (uint32_t)(pre + al(2ull * p.n2p) + al(4ull * p.bm_words) + 2 * al(4ull * kP1LogCap));
-        p.prep_lds = (uint32_t)(pre + al(8 * ((E + 1) & ~1ull)) + 4 * 64 * 4 + 64 * 4);
+        p.prep_lds = (uint32_t)(pre + al(8 * std::max<uint64_t>(2, next_pow2(E))));  // k_prep_edges' rank sort keys
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
     }
@@ -1160,8 +1160,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             dnb.eM = (uint64_t*)(B + p.o_eM);
             dnb.cpos = (uint32_t*)(B + p.o_cpos);
             dnb.necnt = (uint32_t*)(B + p.o_necnt);
-            const dim3 pg((unsigned)L, (unsigned)((dnb.E + kPrepEdges - 1) / kPrepEdges));
-            hipLaunchKernelGGL(k_prep_edges, pg, dim3(256), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode);
+            const dim3 pg((unsigned)L, (unsigned)((dnb.E + kPrepEdges - 1) / kPrepEdges + 1));  // + the rank-sort block
+            hipLaunchKernelGGL(k_prep_edges, pg, dim3(kPrepT), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_edges")) return rc;
             hipLaunchKernelGGL(k_prep_tables, dim3(L, kPrepTabBlocks), dim3(kPrepTabT), prep_tables_lds(n), s2, dist, n, dnb, p.cmode, stats);

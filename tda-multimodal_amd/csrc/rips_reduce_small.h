@@ -132,78 +132,87 @@ struct DenseBufs {
 //                  w << 12 | first << 18 | tie << 19; FAST: rank_of[triangle]
 //                  (0xFFFF above thresh); TABLE: cobt[e][v] = rank of
 //                  {a, b, v} from its youngest facet's block
-constexpr int kPrepEdges = 64;   // edges per block (counting: 4 slices of the edge list per edge)
+constexpr int kPrepEdges = 256;  // edges per k_prep_edges mask block (16 per wave)
 constexpr uint32_t kNoRank = 0xFFFFFFFFu;
 // inv16[rank] = edge | flags (edge < 2048 for N <= 64)
 constexpr uint32_t kInvEdge = 0x7FFu, kInvFirst = 1u << 11, kInvTie = 1u << 12, kInvRes = 1u << 13;
 // k_h1_chain variants (template MODE)
 constexpr int kChainGeneral = 0, kChainFast = 1, kChainTable = 2;
 
-__global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
-                                                    float user_thresh, DenseBufs db, int cmode) {
+// Grid (L, nb + 1), nb = ceil(E / kPrepEdges), kPrepT threads.  Blocks
+// y < nb: the block masks M_e of their kPrepEdges edges (wave per edge, lane
+// = third vertex).  Block y == nb: the ranks -- one bitonic sort of the
+// layer's (length bits, edge index) keys in LDS; rank = position among the
+// edges <= thresh (they sort first; keys are unique, so this equals the count
+// of smaller keys that r03 computed with E x E comparisons in every block).
+// Sort stages with j <= 64 stay inside one wave's 128 keys and need no
+// block barrier.  k_prep_tables derives the per-rank block sizes and lengths
+// from M_e and the ranks.
+constexpr int kPrepT = 1024;
+__global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
+                                                       float user_thresh, DenseBufs db, int cmode) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NW = kPrepT / 64, EPW = kPrepEdges / NW;  // waves, edges per wave
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
-    const int e0 = blockIdx.y * kPrepEdges;
     const int E = n * (n - 1) / 2;
+    const int nb = (E + kPrepEdges - 1) / kPrepEdges;
     const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
     float* D = (float*)(smem + 16);
-    uint64_t* keys = (uint64_t*)(D + ((n * n + 3) & ~3));   // [E rounded to 2] (length bits, edge)
-    uint32_t* part = (uint32_t*)(keys + ((E + 1) & ~1));   // [4 slices][64]
-    uint32_t* rk_sh = part + 4 * 64;                        // [64]
-    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, 256);
+    stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, kPrepT);
+    __syncthreads();
+    if ((int)blockIdx.y == nb) {  // ranks
+        TDA_LDS uint64_t* keys = (TDA_LDS uint64_t*)(D + ((n * n + 3) & ~3));  // [P]
+        int P = 2;
+        while (P < E) P <<= 1;
+        for (int i = t; i < P; i += kPrepT) {
+            uint64_t k = ~0ull;
+            if (i < E) {
+                int a, b;
+                edge_verts((uint32_t)i, a, b);
+                k = ((uint64_t)__float_as_uint(D[a * n + b]) << 32) | (uint32_t)i;
+            }
+            keys[i] = k;
+        }
+        __syncthreads();  // a wave's 128-key window was filled by two waves
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                if (j >= 128) __syncthreads();  // pairs span waves: every earlier stage's writes first
+                else __builtin_amdgcn_wave_barrier();
+                for (int q = t; q < (P >> 1); q += kPrepT) {
+                    const int i = 2 * q - (q & (j - 1)), x = i + j;  // i has bit j clear
+                    const uint64_t u = keys[i], v = keys[x];
+                    if ((u > v) == ((i & k) == 0)) {
+                        keys[i] = v;
+                        keys[x] = u;
+                    }
+                }
+                if (j >= 128) __syncthreads();
+            }
+        __syncthreads();
+        uint32_t* ep = db.epos + (size_t)l * db.E;
+        for (int q = t; q < E; q += kPrepT) {
+            const uint64_t k = keys[q];
+            const bool in = __uint_as_float((uint32_t)(k >> 32)) <= r;
+            st_glb(ep, (size_t)(uint32_t)k, in ? (uint32_t)q : kNoRank);
+            // edges <= thresh sort first: the last of them writes their count
+            if (in && (q + 1 == E || !(__uint_as_float((uint32_t)(keys[q + 1] >> 32)) <= r))) st_glb(db.necnt, (size_t)l, (uint32_t)(q + 1));
+        }
+        return;
+    }
+    const int e0 = blockIdx.y * kPrepEdges;
     if (cmode == kChainFast) {  // this block's share of "every triangle above the threshold"
         uint32_t* ro = (uint32_t*)(db.rank_of + (size_t)l * db.tri_stride);
-        const uint32_t words = db.tri_stride / 2, per = (words + gridDim.y - 1) / gridDim.y;
+        const uint32_t words = db.tri_stride / 2, per = (words + nb - 1) / nb;
         const uint32_t w0 = blockIdx.y * per, w1 = min(words, w0 + per);
-        for (uint32_t i = w0 + t; i < w1; i += 256) st_glb(ro, i, 0xFFFFFFFFu);
+        for (uint32_t i = w0 + t; i < w1; i += kPrepT) st_glb(ro, i, 0xFFFFFFFFu);
     }
-    __syncthreads();
-    for (int e = t; e < E; e += 256) {
-        int a, b;
-        edge_verts((uint32_t)e, a, b);
-        keys[e] = ((uint64_t)__float_as_uint(D[a * n + b]) << 32) | (uint32_t)e;
-    }
-    if (t == 0 && (E & 1)) keys[E] = ~0ull;
-    __syncthreads();
-    // rank = #{keys below}: edges above thresh have larger keys than any edge
-    // <= thresh, so counting over all edges is exact for the edges that rank
-    {
-        const int e = e0 + ln, sl = wv;
-        const uint64_t ke = e < E ? keys[e] : ~0ull;
-        const int np = (E + 1) >> 1;  // key pairs
-        const int c0 = (np * sl) / 4, c1 = (np * (sl + 1)) / 4;
-        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-        const TDA_LDS u64x2* kp = (const TDA_LDS u64x2*)keys;
-        uint32_t cnt = 0;
-#pragma unroll 4
-        for (int q = c0; q < c1; ++q) {
-            const u64x2 x = kp[q];
-            cnt += (uint64_t)x.x < ke;
-            cnt += (uint64_t)x.y < ke;
-        }
-        part[sl * 64 + ln] = cnt;
-    }
-    __syncthreads();
-    if (t < 64) {
-        const int e = e0 + t;
-        uint32_t rank = kNoRank;
-        if (e < E && __uint_as_float((uint32_t)(keys[e] >> 32)) <= r) {
-            rank = part[t] + part[64 + t] + part[128 + t] + part[192 + t];
-            st_glb(db.lenr + (size_t)l * (db.E + 8), (size_t)rank, (uint32_t)(keys[e] >> 32));
-        }
-        if (e < E) st_glb(db.epos + (size_t)l * db.E, (size_t)e, rank);
-        rk_sh[t] = rank;
-        const uint64_t m = __ballot(rank != kNoRank);
-        if (t == 0 && m) atomicAdd(&db.necnt[l], (uint32_t)__popcll(m));
-    }
-    __syncthreads();
     // block masks: wave per edge (4 in flight), lane = third vertex
-    for (int i0 = 0; i0 < kPrepEdges / 4; i0 += 4) {
+    for (int i0 = 0; i0 < EPW; i0 += 4) {
         float dav[4], dbv[4], lev[4];
         int av[4], bv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int e = e0 + wv * (kPrepEdges / 4) + i0 + u;
+            const int e = e0 + wv * EPW + i0 + u;
             int a = 0, b = 0;
             if (e < E) edge_verts((uint32_t)e, a, b);
             av[u] = a;
@@ -214,18 +223,14 @@ __global__ __launch_bounds__(256) void k_prep_edges(const float* __restrict__ di
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int li = wv * (kPrepEdges / 4) + i0 + u, e = e0 + li;
+            const int e = e0 + wv * EPW + i0 + u;
             const int a = av[u], b = bv[u], v = ln;
             const float le = lev[u];
             bool ok = e < E && le <= r && v < n && v != a && v != b && dav[u] <= le && dbv[u] <= le;
             if (ok && dav[u] == le && edge_id(a, v) < (uint32_t)e) ok = false;  // (a, v) is the younger facet
             if (ok && dbv[u] == le && edge_id(b, v) < (uint32_t)e) ok = false;
             const uint64_t m = __ballot(ok);
-            if (ln == 0 && e < E) {
-                st_glb(db.eM + (size_t)l * db.E, (size_t)e, m);
-                const uint32_t rk = rk_sh[li];
-                if (rk != kNoRank) st_glb(db.cpos + (size_t)l * (db.E + 8), (size_t)rk, (uint32_t)__popcll(m));
-            }
+            if (ln == 0 && e < E) st_glb(db.eM + (size_t)l * db.E, (size_t)e, m);
         }
     }
 }
@@ -261,22 +266,29 @@ __global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restri
     uint32_t* qt = cl + ES;                                                          // [nE] rank -> class start | tie << 16
     uint32_t* lens = qt + ES;                                                        // [nE] rank -> length bits
     uint32_t* wsum = lens + ES;                                                      // [NW]
-    const size_t lE = (size_t)l * db.E, lS = (size_t)l * (db.E + 8);
+    const size_t lE = (size_t)l * db.E;
     stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, kPrepTabT);
     const uint32_t nE = ld_glb(db.necnt, (size_t)l);
     for (int e = t; e < E; e += kPrepTabT) {
         Ms[e] = ld_glb(db.eM + lE, (size_t)e);
         ep[e] = ld_glb(db.epos + lE, (size_t)e);
     }
-    // scan: raw block sizes by rank -> exclusive prefix (fr[nE] = triangles <= thresh)
+    __syncthreads();
+    // by rank: block size |M_e| and length bits of the ranked edges
+    for (int e = t; e < E; e += kPrepTabT) {
+        const uint32_t rk = ep[e];
+        if (rk != kNoRank) {
+            int a, b;
+            edge_verts((uint32_t)e, a, b);
+            fr[rk] = (uint32_t)__popcll(Ms[e]);
+            lens[rk] = __float_as_uint(D[a * n + b]);
+        }
+    }
+    __syncthreads();
+    // scan: block sizes by rank -> exclusive prefix (fr[nE] = triangles <= thresh)
     const uint32_t per = (nE + kPrepTabT - 1) / kPrepTabT, q0 = t * per, q1 = min(nE, q0 + per);
     uint32_t loc = 0;
-    for (uint32_t q = q0; q < q1; ++q) {
-        const uint32_t v = ld_glb(db.cpos + lS, (size_t)q);
-        fr[q] = v;
-        lens[q] = ld_glb(db.lenr + lS, (size_t)q);
-        loc += v;
-    }
+    for (uint32_t q = q0; q < q1; ++q) loc += fr[q];
     uint32_t x = loc;
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);

@@ -5,6 +5,7 @@ Bar (north_star): pair indices bit-exact, filtration values bit-exact (the
 stated tolerance is 1e-5; we assert equality of the f32 values and check the
 1e-5 bound separately where a value is compared to a float64 reference).
 """
+import importlib
 import json
 import os
 
@@ -747,3 +748,32 @@ def test_mfma_distance_batch_invariance(gpu, n):
             assert np.array_equal(one.dgms[d], full[l].dgms[d])
             assert np.array_equal(one.birth_idx[d], full[l].birth_idx[d])
             assert np.array_equal(one.death_idx[d], full[l].death_idx[d])
+
+
+def test_dist64_flag_with_want_dist_toggled_at_the_c_abi(gpu):
+    """a C-ABI caller keeps TDA_FLAG_DIST64 set with float64
+    points and toggles want_dist between calls on one slot.  The plan's
+    offsets differ between the two (the f64 distance block), so each must
+    replay its own graph (p.want64 is in the graph key): pairs, checksums and
+    the f32 distances stay identical, and dist64 is returned only when asked."""
+    rip = importlib.import_module("tda-multimodal_amd.ripser")
+    lib = importlib.import_module("tda-multimodal_amd._lib")
+    X = np.ascontiguousarray(gpu.synthetic.sweep48(4).astype(np.float64))
+
+    def call(want):
+        a = lib.RipsArgs()
+        a.x, a.x_on_device, a.dtype = X.ctypes.data, 0, lib.TDA_F64
+        a.L, a.N, a.D = X.shape
+        a.maxdim, a.thresh, a.modulus, a.device, a.slot = 2, float("inf"), 2, 0, 5
+        a.want_dist, a.flags = want, lib.TDA_FLAG_DIST64
+        return rip._call_batch(a, bool(want))[0]
+
+    outs = [call(w) for w in (1, 0, 1, 0, 1)]
+    for o in outs[1:]:
+        for l in range(4):
+            assert o[l].checksum == outs[0][l].checksum
+            assert all(np.array_equal(a, b) for a, b in zip(o[l].dgms, outs[0][l].dgms))
+    for w, o in zip((1, 0, 1, 0, 1), outs):
+        assert (o[0].dist64 is not None) == bool(w)
+    d = X[0][:, None, :] - X[0][None, :, :]
+    np.testing.assert_allclose(outs[2][0].dist64, np.sqrt((d * d).sum(-1)), rtol=1e-9, atol=1e-9)
