@@ -560,7 +560,7 @@ __device__ __forceinline__ float block_thresh(const uint32_t* __restrict__ rowma
     __syncthreads();
     uint32_t m = 0xFFFFFFFFu;
     for (int i = threadIdx.x; i < n; i += blockDim.x) m = min(m, rowmax[i]);
-    atomicMin(s_min, m);
+    if (threadIdx.x < n) atomicMin(s_min, m);  // only lanes that read a row (1024-thread blocks: no 1024-way LDS conflict)
     __syncthreads();
     const float r = __uint_as_float(*s_min);
     __syncthreads();

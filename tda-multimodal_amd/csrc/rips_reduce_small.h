@@ -140,13 +140,13 @@ constexpr uint32_t kInvEdge = 0x7FFu, kInvFirst = 1u << 11, kInvTie = 1u << 12, 
 constexpr int kChainGeneral = 0, kChainFast = 1, kChainTable = 2;
 
 // Grid (L, nb + 1), nb = ceil(E / kPrepEdges), kPrepT threads.  Blocks
-// y < nb: the block masks M_e of their kPrepEdges edges (wave per edge, lane
-// = third vertex).  Block y == nb: the ranks -- one bitonic sort of the
+// y >= 1: the block masks M_e of their kPrepEdges edges (wave per edge, lane
+// = third vertex).  Block y == 0: the ranks -- one bitonic sort of the
 // layer's (length bits, edge index) keys in LDS; rank = position among the
 // edges <= thresh (they sort first; keys are unique, so this equals the count
 // of smaller keys that r03 computed with E x E comparisons in every block).
-// Sort stages with j <= 64 stay inside one wave's 128 keys and need no
-// block barrier.  k_prep_tables derives the per-rank block sizes and lengths
+// Sort stages with j <= 64 stay inside one wave's 128 keys: register
+// shuffles, no LDS and no block barrier.  k_prep_tables derives the per-rank block sizes and lengths
 // from M_e and the ranks.
 constexpr int kPrepT = 1024;
 __global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
@@ -160,34 +160,50 @@ __global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__
     float* D = (float*)(smem + 16);
     stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, kPrepT);
     __syncthreads();
-    if ((int)blockIdx.y == nb) {  // ranks
+    if (blockIdx.y == 0) {  // ranks (y = 0: dispatched first, the long pole overlaps the mask blocks)
         TDA_LDS uint64_t* keys = (TDA_LDS uint64_t*)(D + ((n * n + 3) & ~3));  // [P]
         int P = 2;
         while (P < E) P <<= 1;
-        for (int i = t; i < P; i += kPrepT) {
-            uint64_t k = ~0ull;
-            if (i < E) {
-                int a, b;
-                edge_verts((uint32_t)i, a, b);
-                k = ((uint64_t)__float_as_uint(D[a * n + b]) << 32) | (uint32_t)i;
-            }
-            keys[i] = k;
-        }
-        __syncthreads();  // a wave's 128-key window was filled by two waves
+        // thread t holds keys 2t and 2t + 1 in registers; a stage's partner is
+        // in the same thread (j = 1), in lane t ^ j/2 of the same wave (j <= 64:
+        // a wave holds 128 consecutive keys) or, for j >= 128, read through LDS
+        auto key_of = [&](int i) -> uint64_t {
+            if (i >= E) return ~0ull;
+            int a, b;
+            edge_verts((uint32_t)i, a, b);
+            return ((uint64_t)__float_as_uint(D[a * n + b]) << 32) | (uint32_t)i;
+        };
+        const int i0 = 2 * t;
+        const bool mine = i0 < P;
+        uint64_t x0 = key_of(i0), x1 = key_of(i0 + 1);
         for (int k = 2; k <= P; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
-                if (j >= 128) __syncthreads();  // pairs span waves: every earlier stage's writes first
-                else __builtin_amdgcn_wave_barrier();
-                for (int q = t; q < (P >> 1); q += kPrepT) {
-                    const int i = 2 * q - (q & (j - 1)), x = i + j;  // i has bit j clear
-                    const uint64_t u = keys[i], v = keys[x];
-                    if ((u > v) == ((i & k) == 0)) {
-                        keys[i] = v;
-                        keys[x] = u;
+                uint64_t y0, y1;
+                if (j >= 128) {
+                    if (mine) {
+                        keys[i0] = x0;
+                        keys[i0 + 1] = x1;
                     }
+                    __syncthreads();
+                    y0 = mine ? keys[i0 ^ j] : ~0ull;
+                    y1 = mine ? keys[(i0 + 1) ^ j] : ~0ull;
+                    __syncthreads();  // every read done before the next stage's writes
+                } else if (j >= 2) {
+                    y0 = shfl_xor_u64(x0, j >> 1);
+                    y1 = shfl_xor_u64(x1, j >> 1);
+                } else {
+                    y0 = x1;
+                    y1 = x0;
                 }
-                if (j >= 128) __syncthreads();
+                const bool asc = (i0 & k) == 0;                   // the same for i0 and i0 + 1 (k >= 2)
+                const bool lo0 = (i0 & j) == 0, lo1 = ((i0 + 1) & j) == 0;
+                x0 = (lo0 == asc) ? (x0 < y0 ? x0 : y0) : (x0 < y0 ? y0 : x0);
+                x1 = (lo1 == asc) ? (x1 < y1 ? x1 : y1) : (x1 < y1 ? y1 : x1);
             }
+        if (mine) {
+            keys[i0] = x0;
+            keys[i0 + 1] = x1;
+        }
         __syncthreads();
         uint32_t* ep = db.epos + (size_t)l * db.E;
         for (int q = t; q < E; q += kPrepT) {
@@ -199,11 +215,12 @@ __global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__
         }
         return;
     }
-    const int e0 = blockIdx.y * kPrepEdges;
+    const int mb = blockIdx.y - 1;  // mask block 0 .. nb-1
+    const int e0 = mb * kPrepEdges;
     if (cmode == kChainFast) {  // this block's share of "every triangle above the threshold"
         uint32_t* ro = (uint32_t*)(db.rank_of + (size_t)l * db.tri_stride);
         const uint32_t words = db.tri_stride / 2, per = (words + nb - 1) / nb;
-        const uint32_t w0 = blockIdx.y * per, w1 = min(words, w0 + per);
+        const uint32_t w0 = mb * per, w1 = min(words, w0 + per);
         for (uint32_t i = w0 + t; i < w1; i += kPrepT) st_glb(ro, i, 0xFFFFFFFFu);
     }
     // block masks: wave per edge (4 in flight), lane = third vertex
