@@ -1263,7 +1263,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // appear); in the one-stream timing mode it runs right after the chain,
     // so it sees what it sees when it runs beside it
     auto launch_phase1 = [&](hipStream_t st) -> int {
-        hipLaunchKernelGGL(k_h2_phase1, dim3(L, kP1Grid), dim3(64), p.p1_lds, st, dist, n, stats, db[2], sb, (const uint16_t*)dnb.cls2,
+        // blocks per layer: each holds ~46 KB of LDS (one wave), so the whole grid is occupancy-bound:
+        // ~1 K blocks over all layers (r04, sweep48 serial stage: L = 32: 96 -> 32 blocks 35 -> 28 us;
+        // L = 128: 96 -> 16 blocks 108 -> 73 us); small batches keep up to kP1Grid
+        const int p1g = test_env("TDA_P1_GRID") ? std::max(1, atoi(test_env("TDA_P1_GRID")))
+                                                : std::min(kP1Grid, std::max(16, 1024 / std::max(1, L)));
+        hipLaunchKernelGGL(k_h2_phase1, dim3(L, p1g), dim3(64), p.p1_lds, st, dist, n, stats, db[2], sb, (const uint16_t*)dnb.cls2,
                            p.n2p, p.bm_words, (const uint32_t*)dnb.res1, (uint32_t)p.piv_words[1], step_limit());
         HIPC(hipGetLastError());
         if (int rc = (st == s ? tm : tm3).mark("k_h2_phase1")) return rc;

@@ -43,7 +43,7 @@ namespace tda {
 
 constexpr int kDenseMaxN = 64;
 constexpr int kChainT = 1024;             // threads per k_h1_chain block (staging; the chain is wave 0)
-constexpr int kP1Grid = 96;               // k_h2_phase1 blocks per layer (one wave each, strided columns)
+constexpr int kP1Grid = 96;               // k_h2_phase1 blocks per layer at most (one wave each, strided columns; rips.hip sizes it by L)
 constexpr uint32_t kP1WCap = 512;         // phase-1 toggle-set capacity
 constexpr int kChainMaxCols = 512;        // non-cleared H1 residual columns / stored R_j per layer
 constexpr int kMaxK = 21;                 // bitmap words per lane: ceil(C(64,3) / 32 / 64)
