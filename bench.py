@@ -77,11 +77,12 @@ CALL_KW = {"raw4096": {"twonn": True}}
 # flight on separate workspace slots, one stream (hardware queue) each.  The dense N <= 64 path is a
 # chain of latency-bound kernels that leaves most of the 256 CUs idle; wider calls and several calls in
 # flight fill them (r04, tools/ab_coalesce.sh: 148 K layers/s one call at a time -> 217 K coalescing 4,
-# 305 K with 2 in flight, 455 K with 4).  Every record also carries the one-call-at-a-time figure
+# 305 K with 2 in flight, 455 K with 4; after the r04 kernel changes 4 x 4: 445-488 K, 4 x 8: 580 K,
+# 6 x 4: 578 K).  Every record also carries the one-call-at-a-time figure
 # (pipeline.sequential).  sweep48_L4 stays one call at a time: it is the per-call latency record.
 # grid144 (parallel reducer) and raw4096 (distance + H0 + TwoNN) gain from calls in flight but not from wider
 # calls (r04: grid144 5.60 K -> 7.54 K layers/s with 3 in flight; raw4096 120 K -> 148 K with 4).
-PIPE = {"sweep48": (4, 4), "sweep48_host": (4, 4), "sweep48_L4": (1, 1), "grid144": (3, 1), "raw4096": (4, 1),
+PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "grid144": (3, 1), "raw4096": (4, 1),
         "torus1024x32": (1, 1)}  # workload -> (depth, coalesce); (1, 1): one call at a time (env A/B only)
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
 CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
