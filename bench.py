@@ -490,7 +490,8 @@ def main():
             out["strong"] = strong
         if world > 1 and (slots > 1 or coalesce > 1):
             out["pipeline"] = {"depth": slots, "coalesce": coalesce, "note": "each rank's steps through ripser.SweepPipeline "
-                               "(as the one-GPU record); records exchanged per step, in step order"}
+                               "(as the one-GPU record); the records of every `coalesce` steps exchanged in one "
+                               "all-reduce + gather, in step order"}
     if rank == 0 and world == 1:
         cpu_done = {}
         if do_cpu:
