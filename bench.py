@@ -81,8 +81,8 @@ CALL_KW = {"raw4096": {"twonn": True}}
 # 6 x 4: 578 K).  Every record also carries the one-call-at-a-time figure
 # (pipeline.sequential).  sweep48_L4 stays one call at a time: it is the per-call latency record.
 # grid144 (parallel reducer) and raw4096 (distance + H0 + TwoNN) gain from calls in flight but not from wider
-# calls (r04: grid144 5.60 K -> 7.54 K layers/s with 3 in flight; raw4096 120 K -> 148 K with 4).
-PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "grid144": (3, 1), "raw4096": (4, 1),
+# calls (r04: grid144 5.60 K -> 7.54 K layers/s with 3 in flight, 7.87 K with 4; raw4096 120 K -> 148 K with 4).
+PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "grid144": (4, 1), "raw4096": (4, 1),
         "torus1024x32": (1, 1)}  # workload -> (depth, coalesce); (1, 1): one call at a time (env A/B only)
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
 CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
