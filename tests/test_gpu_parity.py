@@ -676,6 +676,24 @@ def test_workspace_slots_run_concurrently_with_identical_results(gpu):
         gpu.ripser_batch(X, maxdim=1, slot=8)
 
 
+@pytest.mark.parametrize("case", ["sweep48", "grid144", "torus300"])
+def test_one_stream_schedule_equals_default(gpu, case):
+    """TDA_FLAG_ONE_STREAM (every kernel on the slot's one stream, the
+    pipeline's schedule) gives bit-identical pairs, indices and checksums to
+    the default multi-stream schedule: the dense N = 48 path, the parallel
+    reducer at N = 144 and N = 300 (H0-H2)."""
+    X = {"sweep48": lambda: gpu.synthetic.sweep48(32), "grid144": lambda: gpu.synthetic.sweep144(4),
+         "torus300": lambda: gpu.synthetic.torus(300, seed=3)[None]}[case]()
+    ref = gpu.ripser_batch(X, maxdim=2)
+    got = gpu.ripser_batch(X, maxdim=2, one_stream=True, slot=4)
+    for l in range(X.shape[0]):
+        assert got[l].checksum == ref[l].checksum
+        for d in range(3):
+            assert np.array_equal(got[l].dgms[d], ref[l].dgms[d])
+            assert np.array_equal(got[l].birth_idx[d], ref[l].birth_idx[d])
+            assert np.array_equal(got[l].death_idx[d], ref[l].death_idx[d])
+
+
 def test_coalesced_pipeline_equals_one_call_per_sweep(gpu):
     """Dynamic batching (SweepPipeline(coalesce=4), the bench's pipelined
     headline): different sweeps submitted one by one and run as 128-layer
