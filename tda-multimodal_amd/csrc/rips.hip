@@ -1164,7 +1164,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             hipLaunchKernelGGL(k_prep_edges, pg, dim3(kPrepT), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_edges")) return rc;
-            hipLaunchKernelGGL(k_prep_tables, dim3(L, kPrepTabBlocks), dim3(kPrepTabT), prep_tables_lds(n), s2, dist, n, dnb, p.cmode, stats);
+            // blocks per layer: 8 up to 64 layers (sweep48, 32 layers: 27 -> 18 us), 4 above (256 layers:
+            // 83 us with 4, 96 with 8 -- the per-block staging and scan then cost more than the spread saves)
+            const int ptb = test_env("TDA_PREP_TAB_BLOCKS") ? std::max(1, atoi(test_env("TDA_PREP_TAB_BLOCKS")))
+                                                           : (L <= 64 ? 2 * kPrepTabBlocks : kPrepTabBlocks);
+            hipLaunchKernelGGL(k_prep_tables, dim3(L, ptb), dim3(kPrepTabT), prep_tables_lds(n), s2, dist, n, dnb, p.cmode, stats);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_tables")) return rc;
         }

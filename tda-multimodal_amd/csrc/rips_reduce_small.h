@@ -343,7 +343,7 @@ __global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restri
     uint32_t* inv32 = db.inv32 + (size_t)l * db.inv_stride;
     uint16_t* ro = db.rank_of + (size_t)l * db.tri_stride;
     uint16_t* ct = db.cobt + (size_t)l * db.cob_stride;
-    for (int e = blockIdx.y * NW + wv; e < E; e += kPrepTabBlocks * NW) {
+    for (int e = blockIdx.y * NW + wv; e < E; e += gridDim.y * NW) {
         int a, b;
         edge_verts((uint32_t)e, a, b);
         const uint32_t rk = ep[e];
