@@ -64,6 +64,20 @@ def test_invalid_arguments_rejected_before_device(pkg, built_lib):
     a.thresh, a.flags = float("inf"), _lib.TDA_FLAG_NO_PERSISTENCE
     assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1  # no persistence needs maxdim 0
     a.flags = 0
+    # ABI 6 input parts: count bound, NULL table / entry, L a multiple of the count
+    parts = (ctypes.c_void_p * 2)(X.ctypes.data, X.ctypes.data)
+    a.x_parts, a.n_parts = ctypes.cast(parts, ctypes.c_void_p), 17
+    assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1
+    a.n_parts, a.L = 2, 3
+    assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1  # 3 layers in 2 parts
+    a.x_parts, a.L = None, 2
+    assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1  # no parts table
+    nul = (ctypes.c_void_p * 2)(X.ctypes.data, None)
+    a.x_parts = ctypes.cast(nul, ctypes.c_void_p)
+    assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -1  # a NULL part
+    a.x_parts, a.n_parts, a.L = ctypes.cast(parts, ctypes.c_void_p), 2, 2
+    assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -5  # valid parts: no gfx950 here
+    a.x_parts, a.n_parts, a.L = None, 0, 1
     assert L.tda_rips_batch(ctypes.byref(a), ctypes.byref(res)) == -5  # no gfx950 here
     D = np.zeros(5, np.float32)
     assert L.tda_rips_dm(D.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), 5, 2, 1, float("inf"), 0,
