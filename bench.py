@@ -84,6 +84,20 @@ CALL_KW = {"raw4096": {"twonn": True}}
 # calls (r04: grid144 5.60 K -> 7.54 K layers/s with 3 in flight, 7.87 K with 4; raw4096 120 K -> 148 K with 4).
 PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "grid144": (4, 1), "raw4096": (4, 1),
         "torus1024x32": (1, 1)}  # workload -> (depth, coalesce); (1, 1): one call at a time (env A/B only)
+def pipe_shape(name: str, steps: int) -> tuple:
+    """(depth, coalesce) of a workload's timed loop: its PIPE row, with fewer
+    sweeps per call when the run is short -- the K timed steps include the
+    pipeline's fill and drain, and 32 sweeps in flight do not pay off in 20 steps
+    (r04, sweep48 at --steps 20: 4 x 8 305-324 K layers/s, 4 x 4 417 K).
+    TDA_BENCH_DEPTH / TDA_BENCH_COALESCE override (A/B runs)."""
+    if name not in PIPE:
+        return 1, 1
+    depth, coalesce = PIPE[name]
+    if coalesce > 4 and steps < 32 * depth:
+        coalesce = 4
+    return int(os.environ.get("TDA_BENCH_DEPTH", depth)), int(os.environ.get("TDA_BENCH_COALESCE", coalesce))
+
+
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
 CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
 
@@ -275,9 +289,7 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
         # X was synchronised above (resident in HBM before the timed region): no per-call event on
         # torch's stream, whose hardware queue a pipeline slot may share (TDA_BENCH_READY=0: with it)
         kw["input_ready"] = True
-    depth, coalesce = PIPE.get(name, (1, 1))
-    depth = int(os.environ.get("TDA_BENCH_DEPTH", depth)) if name in PIPE else 1
-    coalesce = int(os.environ.get("TDA_BENCH_COALESCE", coalesce)) if name in PIPE else 1
+    depth, coalesce = pipe_shape(name, steps)
     kw_pipe = dict(kw)
     if os.environ.get("TDA_BENCH_ONE_STREAM") in ("0", "1"):  # else SweepPipeline's default (one stream when depth > 1)
         kw_pipe["one_stream"] = os.environ["TDA_BENCH_ONE_STREAM"] == "1"
@@ -314,17 +326,24 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     traffic = None
     pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{name}.json")
+    pmc_scale = 1.0
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
-            pmc = json.load(f).get("kernels", {})
+            pj = json.load(f)
+        pmc = pj.get("kernels", {})
+        # counters of a run whose launches covered another batch: per-layer bytes x this batch
+        # (every kernel works on its layers independently)
+        pmc_scale = Lk / pj["layers_per_launch"] if pj.get("layers_per_launch") else 1.0
         traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
+        traffic = traffic * pmc_scale if traffic is not None else None
     gram = next((k for k in ("k_gram_layer", "k_distance_mfma") if k in kern), None)
     mfma_roof = None
     if gram and gram != dom:  # the FP64 Gram kernel when another kernel dominates (e.g. raw4096: H0)
         fpl = 2 * n * n * d
         a_tf = fpl * Lk / (kern[gram] * 1e-3) / 1e12
         mfma_roof = {"bound": "mfma", "kernel": gram, "achieved": a_tf, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": a_tf / FP64_MFMA_PEAK_TFS, "traffic": pmc.get(gram, {}).get("hbm_bytes_per_launch"),
+                     "frac": a_tf / FP64_MFMA_PEAK_TFS,
+                     "traffic": (pmc[gram]["hbm_bytes_per_launch"] * pmc_scale) if gram in pmc else None,
                      "algo_flops_per_layer": fpl, "layers_per_launch": Lk, "kernel_avg_ms": kern[gram],
                      **mfma_executed(n, d, Lk, kern[gram])}
     return {
@@ -430,9 +449,7 @@ def main():
     else:
         X = torch.from_numpy(make_workload(args.workload, L)).to(dev)
         # the same dynamic batching as the one-GPU record (bench PIPE): each rank's steps through a SweepPipeline
-        slots, coalesce = PIPE.get(args.workload, (1, 1))
-        slots = int(os.environ.get("TDA_BENCH_DEPTH", slots))
-        coalesce = int(os.environ.get("TDA_BENCH_COALESCE", coalesce))
+        slots, coalesce = pipe_shape(args.workload, args.steps)
 
         def run_multi(shard: bool):
             torch.cuda.synchronize()

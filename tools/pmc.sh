@@ -18,7 +18,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
     echo "pmc $C rc=$rc"
     if [ $rc -ne 0 ]; then tail -20 gpurun_out/pmc_$C.txt; exit $rc; fi
 done
-python3 tools/pmc_parse.py --workload $WL gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE > /dev/null
+python3 tools/pmc_parse.py --workload $WL --bench-out gpurun_out/pmc_FETCH_SIZE.txt gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE > /dev/null
 rc=$?
 cp profiles/pmc_$WL.json gpurun_out/ 2>/dev/null  # gpurun merges gpurun_out/ back, not profiles/
 exit $rc

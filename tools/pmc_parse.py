@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--workload", default="sweep48")
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
+    ap.add_argument("--bench-out", default=None, help="the bench JSON line of a PMC pass: its roofline.layers_per_launch is recorded")
     a = ap.parse_args()
     fetch = load(a.fetch_dir, "FETCH_SIZE")
     write = load(a.write_dir, "WRITE_SIZE")
@@ -57,6 +58,10 @@ def main():
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes; KiB -> bytes; FETCH_SIZE x2 "
                      "(gfx950 correction, MI355X_MICROARCH.md HBM section); mean over dispatches",
            "kernels": {}}
+    if a.bench_out and os.path.exists(a.bench_out):  # the batch the counted launches covered
+        for line in open(a.bench_out):
+            if line.startswith("{"):
+                out["layers_per_launch"] = (json.loads(line).get("roofline") or {}).get("layers_per_launch")
     for k in sorted(set(fetch) | set(write)):
         f = list(fetch.get(k, {}).values())
         w = list(write.get(k, {}).values())

@@ -28,7 +28,7 @@ for WL in ${WLS_PMC:-sweep48 grid144 torus1024 raw4096}; do
         echo "pmc $WL $C rc=$rc"
         [ $rc -ne 0 ] && { tail -5 gpurun_out/pmc_$C.txt; exit $rc; }
     done
-    python3 tools/pmc_parse.py --workload $WL gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE > /dev/null || exit 1
+    python3 tools/pmc_parse.py --workload $WL --bench-out gpurun_out/pmc_FETCH_SIZE.txt gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE > /dev/null || exit 1
     cp profiles/pmc_$WL.json gpurun_out/$TAG/pmc_$WL.json
 done
 i=0
