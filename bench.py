@@ -87,14 +87,15 @@ PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "grid14
 def pipe_shape(name: str, steps: int) -> tuple:
     """(depth, coalesce) of a workload's timed loop: its PIPE row, with fewer
     sweeps per call when the run is short -- the K timed steps include the
-    pipeline's fill and drain, and 32 sweeps in flight do not pay off in 20 steps
-    (r04, sweep48 at --steps 20: 4 x 8 305-324 K layers/s, 4 x 4 417 K).
+    pipeline's fill and drain, so a short run puts all its steps into one wave
+    of `depth` calls (r04, sweep48 at --steps 20, tools/ab_k20.sh: 4 x 8
+    305-324 K layers/s; 4 x 4 mean 354 K over 5 runs; 4 x 5 mean 378 K).
     TDA_BENCH_DEPTH / TDA_BENCH_COALESCE override (A/B runs)."""
     if name not in PIPE:
         return 1, 1
     depth, coalesce = PIPE[name]
-    if coalesce > 4 and steps < 32 * depth:
-        coalesce = 4
+    if steps < 32 * depth:
+        coalesce = min(coalesce, max(1, -(-steps // depth)))
     return int(os.environ.get("TDA_BENCH_DEPTH", depth)), int(os.environ.get("TDA_BENCH_COALESCE", coalesce))
 
 
