@@ -1286,7 +1286,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // apparent<1> at the head of the H2 branch's stream: sweep48 0.182 ->
     // 0.175 ms device, L = 4 0.136 -> 0.131 ms (replayed graph; eager slower)
     // 5 up to 64 layers per call; 3 above (sweep48x4, 128 layers: 0.42 vs 0.48 ms with 5)
-    const int order = test_env("TDA_ORDER") ? atoi(test_env("TDA_ORDER")) : (L <= 64 ? 5 : 3);
+    // r04 (after the §6.4-6.5 kernel changes, graph replay, one call at a time): L = 32 order 2 0.167 ms
+    // device vs 0.174 with 5; L = 4 order 5 0.124 ms vs 0.138 with 2
+    const int order = test_env("TDA_ORDER") ? atoi(test_env("TDA_ORDER")) : (L <= 16 ? 5 : L <= 64 ? 2 : 3);
     if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
     const bool h2_side = !p.dense && p.par && p.par2 && p.maxdim >= 2;
