@@ -115,6 +115,7 @@ struct Plan {
     uint32_t cob_stride = 0;  // per-layer coboundary table (TABLE): E * N rounded up
     uint32_t chain_lds = 0;   // dynamic LDS of k_h1_chain
     uint32_t p1_lds = 0;      // dynamic LDS of k_h2_phase1
+    int p1_waves = 1;         // waves per k_h2_phase1 block
     uint32_t n2p = 0;         // stride of the per-layer edge-class table (N * N rounded up)
     uint32_t bm_words = 0;    // tetrahedron membership bitmap of k_h2_phase1 (words)
     uint32_t prep_lds = 0;    // dynamic LDS of k_prep_edges
@@ -248,7 +249,11 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par,
                                                          : pre + al(16 * E) + al(2ull * p.inv_stride) + tail);
         p.n2p = (uint32_t)align_up(N * N, 8);
         p.bm_words = (uint32_t)((binom(N, 4) + 31) / 32 + 1);
-        p.p1_lds = (uint32_t)(pre + al(2ull * p.n2p) + al(4ull * p.bm_words) + 2 * al(4ull * kP1LogCap));
+        // k_h2_phase1: shared matrix + class table, then one bitmap + log per wave (2 waves when they fit)
+        const uint64_t p1_wave = al(4ull * p.bm_words) + 2 * al(4ull * kP1LogCap);
+        p.p1_waves = (pre + al(2ull * p.n2p) + kP1MaxWaves * p1_wave <= (uint64_t)kLdsMax && !test_env_is("TDA_P1_WAVES", "1"))
+                         ? kP1MaxWaves : 1;
+        p.p1_lds = (uint32_t)(pre + al(2ull * p.n2p) + p.p1_waves * p1_wave);
         p.prep_lds = (uint32_t)(pre + al(8 * std::max<uint64_t>(2, next_pow2(E))));  // k_prep_edges' rank sort keys
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
@@ -1272,7 +1277,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         // L = 128: 96 -> 16 blocks 108 -> 73 us); small batches keep up to kP1Grid
         const int p1g = test_env("TDA_P1_GRID") ? std::max(1, atoi(test_env("TDA_P1_GRID")))
                                                 : std::min(kP1Grid, std::max(16, 1024 / std::max(1, L)));
-        hipLaunchKernelGGL(k_h2_phase1, dim3(L, p1g), dim3(64), p.p1_lds, st, dist, n, stats, db[2], sb, (const uint16_t*)dnb.cls2,
+        hipLaunchKernelGGL(k_h2_phase1, dim3(L, (p1g + p.p1_waves - 1) / p.p1_waves), dim3(64 * p.p1_waves), p.p1_lds, st, dist, n, stats, db[2], sb, (const uint16_t*)dnb.cls2,
                            p.n2p, p.bm_words, (const uint32_t*)dnb.res1, (uint32_t)p.piv_words[1], step_limit());
         HIPC(hipGetLastError());
         if (int rc = (st == s ? tm : tm3).mark("k_h2_phase1")) return rc;

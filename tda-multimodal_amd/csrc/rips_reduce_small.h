@@ -984,15 +984,22 @@ __device__ __forceinline__ uint32_t c4u(uint32_t x) { return x < 4 ? 0u : x * (x
 __device__ __forceinline__ uint32_t c3s(uint32_t x) { return x < 3 ? 0u : x * (x - 1) * (x - 2) / 6; }
 __device__ __forceinline__ uint32_t c2s(uint32_t x) { return x < 2 ? 0u : x * (x - 1) / 2; }
 
-__global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats, DimBufs b,
-                                                  SmallBufs sb, const uint16_t* __restrict__ cls2g, uint32_t n2p, uint32_t bm_words,
-                                                  const uint32_t* __restrict__ res1g, uint32_t res1_words, uint64_t step_limit) {
+// Blocks of kP1MaxWaves (or 1, when two waves' bitmaps do not fit the LDS)
+// independent waves: the layer's matrix and class table are staged once per
+// block and shared; each wave has its own bitmap and log and takes its own
+// columns (virtual one-wave block blockIdx.y * waves + wave).
+constexpr int kP1MaxWaves = 2;
+__global__ __launch_bounds__(64 * kP1MaxWaves) void k_h2_phase1(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                                DimBufs b, SmallBufs sb, const uint16_t* __restrict__ cls2g, uint32_t n2p,
+                                                                uint32_t bm_words, const uint32_t* __restrict__ res1g, uint32_t res1_words,
+                                                                uint64_t step_limit) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x, ln = threadIdx.x;
+    const int l = blockIdx.x, ln = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint64_t vb = (uint64_t)blockIdx.y * nw + wv, vstride = (uint64_t)gridDim.y * nw;
     LayerStats* st = stats + l;
     uint64_t nres = (uint64_t)st->n_residual[2];
     if (nres > b.rcap) nres = b.rcap;
-    if (blockIdx.y >= nres) return;
+    if ((uint64_t)blockIdx.y * nw >= nres) return;  // the whole block is idle (uniform exit)
     const uint64_t* resid = b.resid + (size_t)l * b.rcap;
     unsigned char* p = smem + 16;
     auto take = [&](size_t bytes) {
@@ -1002,13 +1009,18 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
     };
     float* Dl = (float*)take(4ull * n * n);
     uint16_t* cls = (uint16_t*)take(2ull * n2p);
+    for (int w = 0; w < wv; ++w) {  // the earlier waves' private regions
+        (void)take(4ull * bm_words);
+        (void)take(4ull * kP1LogCap);
+        (void)take(4ull * kP1LogCap);
+    }
     uint32_t* bm = (uint32_t*)take(4ull * bm_words);
     uint32_t* lk = (uint32_t*)take(4ull * kP1LogCap);
     uint32_t* lv = (uint32_t*)take(4ull * kP1LogCap);
-    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, ln, 64);
-    stage_to_lds(cls, cls2g + (size_t)l * n2p, 2ull * n2p, ln, 64);
+    stage_to_lds(Dl, dist + (size_t)l * n * n, 4ull * n * n, threadIdx.x, blockDim.x);
+    stage_to_lds(cls, cls2g + (size_t)l * n2p, 2ull * n2p, threadIdx.x, blockDim.x);
     for (uint32_t i = ln; i < bm_words; i += 64) st_lds(bm, i, 0u);
-    wave_sync();
+    __syncthreads();  // the shared matrix and class table; below, every wave works alone
 
     uint64_t* p1k = sb.p1_key + (size_t)l * b.rcap;
     uint32_t* p1i = sb.p1_info + (size_t)l * b.rcap;
@@ -1105,7 +1117,7 @@ __global__ __launch_bounds__(64) void k_h2_phase1(const float* __restrict__ dist
 #ifdef TDA_PROFILE
     const uint64_t t_p1 = clock64();
 #endif
-    for (uint64_t j = blockIdx.y; j < nres; j += gridDim.y) {
+    for (uint64_t j = vb; j < nres; j += vstride) {
 #ifdef TDA_PROFILE
         const uint64_t tcol = clock64();
 #endif
