@@ -23,6 +23,8 @@ def short_name(name: str) -> str:
     if "<" in name:
         base, targs = name.split("<", 1)
         args = [a.strip() for a in targs.rstrip(">").split(",")]
+        if base == "k_apparent_small":  # bench.py's stage name for the N <= 64 apparent pass
+            return f"k_apparent<{args[0]}>"
         if base == "k_apparent" or (base == "k_reduce_par" and args[0] == "2"):
             return f"{base}<{args[0]}>"  # bench.py names the H2 launch k_reduce_par<2>
         return base
