@@ -55,6 +55,13 @@ WORKLOADS = {
                             "(host-array-in -> diagrams-on-host-out, debug_tda_pipeline.py:104-110)", 400, 5),
     # configs[2]'s per-GPU share: 4 of the 32 layers in one call (8 GPUs, strong scaling)
     "sweep48_L4": (4, 2, "4 layers x 48 points per call (configs[2]'s per-GPU share at 8 GPUs), D=3, H0-H2", 100, 10),
+    # configs[1] as written: one 48-point layer per call, H0-H2, one call at a time (per-call latency)
+    "sweep48_L1": (1, 2, "1 layer x 48 points per call (configs[1]), D=3, H0-H2, one call at a time", 200, 10),
+    # the top of north_star's N range (N = 48-2048): one layer per call, as configs[3] at N = 1024
+    "torus2048": (1, 1, "S1xS1 torus N=2048 (top of the north_star N range), D=3, H0-H1, one layer per call", 3, 1),
+    # ... and at maxdim 2 with ripser's thresh (tests/golden/large_h2_2048.npz, torus2048_t12)
+    "torus2048_h2": (1, 2, "S1xS1 torus N=2048, D=3, H0-H2 at thresh=1.2 (ripser's thresh argument; "
+                           "tests/golden/large_h2_2048.npz torus2048_t12), one layer per call", 3, 1),
     # raw hidden states (no UMAP): distance on the FP64 matrix cores + TwoNN + H0
     "raw4096": (32, 0, "32 layers x 144 tokens x 4096 raw hidden-state features: distance (FP64 MFMA) + H0 + TwoNN "
                        "intrinsic dimension (metrics.py:113-208)", 100, 3),
@@ -67,11 +74,15 @@ DATA = {
     "grid144": "synthetic: 12x12 grid on the torus + N(0, 0.02^2) + random rotation per layer",
     "torus1024": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 0",
     "torus1024x32": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seeds 0-31",
+    "sweep48_L1": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
+    "torus2048": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 3",
+    "torus2048_h2": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 3",
     "raw4096": "synthetic: activation-like f32 clouds (heavy-tailed feature scales, offsets, outlier features)",
 }
-NPOINTS = {"torus1024x32": 1024, "sweep48": 48, "sweep48x4": 48, "sweep48_host": 48, "sweep48_L4": 48, "grid144": 144, "torus1024": 1024, "raw4096": 144}
+NPOINTS = {"torus1024x32": 1024, "sweep48": 48, "sweep48x4": 48, "sweep48_host": 48, "sweep48_L4": 48, "sweep48_L1": 48,
+           "grid144": 144, "torus1024": 1024, "raw4096": 144, "torus2048": 2048, "torus2048_h2": 2048}
 DIMS = {w: (4096 if w == "raw4096" else 3) for w in WORKLOADS}  # point dimension D of each workload (make_workload)
-CALL_KW = {"raw4096": {"twonn": True}}
+CALL_KW = {"raw4096": {"twonn": True}, "torus2048_h2": {"thresh": 1.2}}
 # dynamic batching of consecutive steps (ripser.SweepPipeline): every step submits one 32-layer sweep;
 # up to `coalesce` queued sweeps run as one call over their concatenated layers and `depth` calls are in
 # flight on separate workspace slots, one stream (hardware queue) each.  The dense N <= 64 path is a
@@ -82,8 +93,8 @@ CALL_KW = {"raw4096": {"twonn": True}}
 # (pipeline.sequential).  sweep48_L4 stays one call at a time: it is the per-call latency record.
 # grid144 (parallel reducer) and raw4096 (distance + H0 + TwoNN) gain from calls in flight but not from wider
 # calls (r04: grid144 5.60 K -> 7.54 K layers/s with 3 in flight, 7.87 K with 4; raw4096 120 K -> 148 K with 4).
-PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "grid144": (4, 1), "raw4096": (4, 1),
-        "torus1024x32": (1, 1)}  # workload -> (depth, coalesce); (1, 1): one call at a time (env A/B only)
+PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "sweep48_L1": (1, 1), "grid144": (4, 1),
+        "raw4096": (4, 1), "torus1024x32": (1, 1)}  # workload -> (depth, coalesce); (1, 1): one call at a time (env A/B only)
 def pipe_shape(name: str, steps: int) -> tuple:
     """(depth, coalesce) of a workload's timed loop: its PIPE row, with fewer
     sweeps per call when the run is short -- the K timed steps include the
@@ -100,7 +111,7 @@ def pipe_shape(name: str, steps: int) -> tuple:
 
 
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
-CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48"}
+CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48", "sweep48_L1": "sweep48"}
 
 
 def algo_bytes_per_layer(n: int, d: int, maxdim: int) -> int:
@@ -125,7 +136,7 @@ def mfma_executed(n: int, d: int, L: int, ms: float) -> dict:
 # (the reference runs one ripser call per layer and ripser is single-threaded);
 # a sweep (many independent layers per step) against the CPU running its
 # layers in parallel, one per worker process (P processes, the box's CPU share).
-BAR_BASIS = {"torus1024": "one_core"}
+BAR_BASIS = {"torus1024": "one_core", "torus2048": "one_core", "torus2048_h2": "one_core", "sweep48_L1": "one_core"}
 
 
 def speedups(value: float, cb: dict, name: str) -> dict:
@@ -143,7 +154,7 @@ def speedups(value: float, cb: dict, name: str) -> dict:
 def make_workload(name: str, layers: int | None = None):
     syn = importlib.import_module("tda-multimodal_amd.synthetic")
     L = layers or WORKLOADS[name][0]
-    if name in ("sweep48", "sweep48x4", "sweep48_host", "sweep48_L4"):
+    if name in ("sweep48", "sweep48x4", "sweep48_host", "sweep48_L4", "sweep48_L1"):
         return syn.sweep48(L)
     if name == "grid144":
         return syn.sweep144(L)
@@ -151,6 +162,8 @@ def make_workload(name: str, layers: int | None = None):
         return syn.torus(1024)[None].repeat(L, 0)
     if name == "torus1024x32":
         return np.stack([syn.torus(1024, seed=s) for s in range(L)])
+    if name in ("torus2048", "torus2048_h2"):
+        return syn.torus(2048, seed=3)[None].repeat(L, 0)
     if name == "raw4096":
         return syn.activations(L, 144, 4096)
     raise ValueError(name)
@@ -170,13 +183,13 @@ def _cpu_layers(task):
     X = _WORKER_CACHE[name]
     oracle.lib()
     if hi > lo:
-        if name in CALL_KW:  # distances + TwoNN restatement (H0 is negligible next to them)
+        if CALL_KW.get(name, {}).get("twonn"):  # distances + TwoNN restatement (H0 is negligible next to them)
             from oracle import twonn
 
             for x in X[lo:hi]:
                 twonn.twonn_from_dist(oracle.distances(x))
         else:
-            oracle.rips_batch_f32(X[lo:hi], maxdim)
+            oracle.rips_batch_f32(X[lo:hi], maxdim, thresh=CALL_KW.get(name, {}).get("thresh", np.inf))
     return hi - lo
 
 
@@ -390,6 +403,55 @@ def measure_umap(pkg, torch, dev, steps: int = 10, warmup: int = 2) -> dict:
             "cpu_baseline": None, "note": "umap-learn is not installed here (no CPU reference to time); layout parity unpinned"}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """``bench.py --gpus N`` started without torchrun: start N ranks (one
+    process per GPU) as ``python -m torch.distributed.run --nproc-per-node N
+    bench.py ...`` in a CHILD process -- before this process touches the GPU
+    -- and return its exit code (BASELINE.json: "at 1/2/4/8 MI355X")."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+def _standin():
+    """TDA_BENCH_STANDIN=module:function -- a CPU rehearsal of the multi-rank
+    loop (tests only): the per-shard batch call is that function (same
+    result interface as ripser_batch), no GPU is touched, gloo carries the
+    collectives.  bench.py itself never imports a stand-in otherwise."""
+    spec = os.environ.get("TDA_BENCH_STANDIN")
+    if not spec:
+        return None
+    mod, fn = spec.split(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+def summary(out: dict) -> dict:
+    """One short row per record, emitted LAST on the line (the driver keeps the
+    line's tail): rate, CPU speed-ups and the 20x bar, roofline fraction."""
+    rows = {}
+    recs = [(out["config"]["workload_name"], out)] + list(out.get("workloads", {}).items())
+    for name, r in recs:
+        sp = r.get("speedup_vs_cpu") or {}
+        rf = r.get("roofline") or {}
+        bar = sp.get("bar_20x") or {}
+        rows[name] = {"value": round(r["value"], 3), "x_1core": round(sp["one_core"], 2) if "one_core" in sp else None,
+                      f"x_{(r.get('cpu_baseline') or {}).get('cores', 'P')}proc": round(sp["all_cores"], 2) if "all_cores" in sp else None,
+                      "bar_20x": bar.get("met"), "bar_basis": bar.get("basis"),
+                      "roofline": (rf.get("kernel"), rf.get("bound"), rf.get("frac")) if rf else None}
+        seq = (r.get("pipeline") or {}).get("sequential")
+        if seq:
+            rows[name]["one_call_at_a_time"] = round(seq["value"], 3)
+    return rows
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -397,7 +459,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=None, help="default: the workload's own (WORKLOADS)")
     ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
-    ap.add_argument("--extra", default="sweep48_host,sweep48_L4,grid144,torus1024,torus1024x32,raw4096,umap36,sweep48x4",
+    ap.add_argument("--extra", default="sweep48_L1,sweep48_L4,grid144,torus1024,torus1024x32,torus2048,torus2048_h2,raw4096,"
+                                       "umap36,sweep48x4,sweep48_host",
                     help="secondary workloads measured at N=1 (comma list, '' for none)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -409,9 +472,16 @@ def main():
     if args.warmup is None:
         args.warmup = WORKLOADS[args.workload][4]
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))  # the ranks print the JSON line (rank 0)
+
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    standin = _standin()
+    backend = os.environ.get("TDA_DIST_BACKEND", "gloo" if standin else "nccl")  # nccl = RCCL over xGMI
+    if standin and (world < 2 or backend != "gloo"):
+        raise SystemExit("TDA_BENCH_STANDIN is a multi-rank CPU rehearsal: it needs WORLD_SIZE > 1 and gloo")
     do_cpu = rank == 0 and world == 1 and not args.no_cpu
     pool, P = None, 0
     if do_cpu:  # worker processes start before this process touches the GPU
@@ -423,12 +493,20 @@ def main():
 
     import torch
 
-    # one GPU per rank; more ranks than GPUs only in a rehearsal (TDA_DIST_BACKEND=gloo on a 1-GPU box)
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    n_dev = 0 if standin else torch.cuda.device_count()
+    if standin:
+        dev = torch.device("cpu")
+    else:
+        # one GPU per rank; more ranks than GPUs only in a gloo rehearsal (TDA_DIST_BACKEND=gloo on a 1-GPU box)
+        if local >= n_dev and backend != "gloo":
+            raise RuntimeError(f"rank {rank} (local {local}) has no GPU of its own: {n_dev} visible; "
+                               "wrapping ranks onto shared GPUs is a rehearsal only (TDA_DIST_BACKEND=gloo)")
+        local = local % max(1, n_dev)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    # distinct devices the job runs on (local ranks 0..world-1 on one node, wrapped only in a rehearsal)
+    n_gpus = min(world, n_dev)
     dist = None
-    backend = os.environ.get("TDA_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
     coll_dev = dev if backend == "nccl" else None         # gloo: collectives on host tensors
     if world > 1:
         import torch.distributed as dist
@@ -438,7 +516,7 @@ def main():
         else:
             dist.init_process_group(backend)
     pkg = importlib.import_module("tda-multimodal_amd")
-    if pkg.lib().tda_device_ok(local) != 1:
+    if not standin and pkg.lib().tda_device_ok(local) != 1:
         raise RuntimeError("no gfx950 device")
 
     L, maxdim, desc, _, _ = WORKLOADS[args.workload]
@@ -448,30 +526,32 @@ def main():
         prim = measure(pkg, torch, dev, args.workload, args.steps, args.warmup, args.layers)
         value, el_ms = prim["value"], prim["ms_per_step"]
     else:
-        X = torch.from_numpy(make_workload(args.workload, L)).to(dev)
+        X_host = make_workload(args.workload, L)
+        X = X_host if standin else torch.from_numpy(X_host).to(dev)
         # the same dynamic batching as the one-GPU record (bench PIPE): each rank's steps through a SweepPipeline
         slots, coalesce = pipe_shape(args.workload, args.steps)
+        sync = (lambda: None) if standin else torch.cuda.synchronize
 
         def run_multi(shard: bool):
-            torch.cuda.synchronize()
+            sync()
             for _ in range(args.warmup):
-                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=coll_dev, shard=shard)
+                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=coll_dev, shard=shard, run=standin)
             if slots > 1 or coalesce > 1:  # every slot captures its graphs before the timed region
                 warm = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
-                                                      coalesce=coalesce)
+                                                      coalesce=coalesce, run=standin)
                 for _ in range(max(args.warmup, 1) * slots * coalesce):
                     warm.step()
                 warm.close()
             dist.barrier()
-            torch.cuda.synchronize()
+            sync()
             t0 = time.perf_counter()
             # every step's records are exchanged; the exchange of step i overlaps the GPU work of later steps
             pipe = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
-                                                  coalesce=coalesce)
+                                                  coalesce=coalesce, run=standin)
             for _ in range(args.steps):
                 pipe.step()
             pipe.close()
-            torch.cuda.synchronize()
+            sync()
             dist.barrier()
             t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)  # max over ranks
@@ -487,17 +567,23 @@ def main():
     out = None
     if rank == 0:
         out = {
-            "metric": METRIC, "value": value, "unit": "layers/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC, "value": value, "unit": "layers/s", "n_gpus": n_gpus, "ranks": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el_ms, "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f32", "data": DATA[args.workload],
-            "config": {"workload": desc, "layers_per_gpu_step": L if args.scaling == "weak" else -(-L // world),
+            "config": {"workload": desc, "workload_name": args.workload,
+                       "layers_per_gpu_step": L if args.scaling == "weak" else -(-L // world),
                        "n_points": NPOINTS[args.workload], "dim": DIMS[args.workload], "maxdim": maxdim,
-                       "parallelism": f"layers sharded ({args.scaling}), {world} process(es) x 1 GPU, "
+                       "parallelism": f"layers sharded ({args.scaling}), {world} process(es) on {n_gpus} GPU(s), "
                                       f"{'RCCL' if backend == 'nccl' else backend} gather of per-layer records "
                                       f"(overlapped with the next step's GPU work)"},
             "roofline": prim["roofline"] if prim else None,
             "cpu_baseline": None,
         }
+        if standin:
+            out["rehearsal"] = {"kind": "cpu stand-in (no GPU)", "standin": os.environ["TDA_BENCH_STANDIN"],
+                                "note": "multi-rank launch + gloo collectives rehearsed on the CPU; not a GPU measurement"}
+        elif world > n_gpus:
+            out["rehearsal"] = {"kind": f"{world} ranks on {n_gpus} GPU(s) over gloo", "note": "not a multi-GPU measurement"}
         if prim:
             if prim.get("roofline_mfma"):
                 out["roofline_mfma"] = prim["roofline_mfma"]
@@ -544,6 +630,8 @@ def main():
         pool.close()
         pool.join()
     if rank == 0:
+        if world == 1:
+            out["summary"] = summary(out)  # last key: the driver keeps the tail of the line
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

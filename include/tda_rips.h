@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TDA_RIPS_ABI_VERSION 6
+#define TDA_RIPS_ABI_VERSION 7
 
 /* error codes */
 #define TDA_OK 0
@@ -62,7 +62,13 @@ typedef struct tda_rips_args {
     float thresh;       /* +inf -> enclosing radius (ripser.py default)         */
     int32_t modulus;    /* must be 2                                            */
     int32_t device;     /* HIP device ordinal                                   */
-    void *stream;       /* hipStream_t or NULL (library stream)                 */
+    void *stream;       /* device input (x_on_device) is read after the work queued
+                           on this hipStream_t so far; NULL = the null (legacy
+                           default) stream, which is torch's default stream.  ABI 7:
+                           before, NULL meant no ordering.  A handle that is not a
+                           stream of the library's HIP runtime on `device` is
+                           refused (TDA_E_HIP).  Ignored with TDA_FLAG_INPUT_READY
+                           and for host input.                                   */
     int32_t want_dist;  /* 1: also return the (L, N, N) f32 distance matrices   */
     int32_t flags;      /* TDA_FLAG_* bits (0 = none)                           */
     /* optional silhouette scores on the same distance matrices (ABI >= 2):
@@ -172,6 +178,9 @@ typedef struct tda_rips_result {
  * hardware queue, so several slots driven from their own host threads
  * (args.slot) run their batches side by side (ripser.SweepPipeline) */
 #define TDA_FLAG_ONE_STREAM 16
+/* ABI >= 7: device input is complete (the caller synchronised after producing
+ * it): no ordering after args.stream at all */
+#define TDA_FLAG_INPUT_READY 32
 
 /* Batched point clouds (or distance matrices) -> persistence diagrams. */
 int tda_rips_batch(const tda_rips_args *args, tda_rips_result **out);
@@ -202,7 +211,7 @@ typedef struct tda_ed_args {
     int32_t x_on_device;    /* 1: x is a device pointer on `device`              */
     int64_t B, N, D;
     int32_t device;
-    void *stream;           /* hipStream_t or NULL: device input is read after it */
+    void *stream;           /* device input is read after it; NULL = null stream  */
 } tda_ed_args;
 
 int tda_effective_dim(const tda_ed_args *args, float *out);

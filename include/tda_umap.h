@@ -47,8 +47,9 @@ typedef struct tda_umap_args {
     int32_t device;
     float *out;             /* host (L, N, n_components) f32: the embedding          */
     float *graph_out;       /* optional host (L, N, N) f32: the pruned fuzzy graph   */
-    void *stream;           /* hipStream_t (or NULL): device inputs are read after the
-                               work queued on it so far (e.g. torch's current stream) */
+    void *stream;           /* device inputs are read after the work queued on this
+                               hipStream_t so far (e.g. torch's current stream);
+                               NULL = the null (legacy default) stream            */
 } tda_umap_args;
 
 int tda_umap_batch(const tda_umap_args *args);

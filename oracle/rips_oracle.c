@@ -38,6 +38,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 
 #define OR_MAXDIM 3
 
@@ -421,6 +422,8 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
     /* ORACLE_STATS=1: debug statistics (apparent pairs, heap sizes); off by
        default so the CPU baseline does only the work the result needs */
     const int stats = getenv("ORACLE_STATS") != NULL;
+    /* ORACLE_COLSTATS=1: print the columns with more than 500 additions (dev aid) */
+    const int colstats = getenv("ORACLE_COLSTATS") != NULL;
     /* threshold (ripser.py rips_dm): enclosing radius when thresh is inf/max */
     if (isinf(thresh) || thresh == 3.402823466e+38f) {
         float enc = INFINITY;
@@ -566,6 +569,7 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
             }
             work.n = 0;
             vwork.n = 0;
+            int64_t adds0 = res->n_adds[dim];
             for (int64_t q = 0; q < m; ++q) {
                 splx_t e = {cbuf[q].diam, cbuf[q].idx};
                 heap_push(&work, e);
@@ -576,6 +580,10 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
                     if (work.n > res->max_heap[dim]) res->max_heap[dim] = work.n;
                     res->sum_heap_steps[dim] += work.n;
                 }
+                if ((p.idx == HM_EMPTY || hm_get(&piv, p.idx) < 0) && colstats && res->n_adds[dim] - adds0 > 500)
+                    fprintf(stderr, "[oracle-col] dim %d col %lld of %lld adds %lld birth %.6f death %.6f heap %lld\n", dim,
+                            (long long)j, (long long)ncols, (long long)(res->n_adds[dim] - adds0), sg.diam,
+                            p.idx == HM_EMPTY ? INFINITY : p.diam, (long long)work.n);
                 if (p.idx == HM_EMPTY) {
                     pairs_push(&P[dim], sg.diam, INFINITY, (int64_t)sg.idx, -1);
                     voff[j + 1] = vn;

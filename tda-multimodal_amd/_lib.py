@@ -89,6 +89,7 @@ TDA_FLAG_STAGE_SERIAL = 2
 TDA_FLAG_DIST64 = 4
 TDA_FLAG_NO_PERSISTENCE = 8
 TDA_FLAG_ONE_STREAM = 16
+TDA_FLAG_INPUT_READY = 32
 TDA_MAX_SLOTS = 8
 TDA_MAX_PARTS = 16
 

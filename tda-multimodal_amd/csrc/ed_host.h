@@ -44,10 +44,9 @@ extern "C" int tda_effective_dim(const tda_ed_args* a, float* out) {
     std::lock_guard<std::mutex> guard(w.mu);
     if (!w.stream) HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
     hipStream_t s = w.stream;
-    if (a->stream) {
+    if (a->x_on_device) {  // device inputs: read after the caller's queued work (NULL = the null stream)
         if (!w.evin) HIPC(hipEventCreateWithFlags(&w.evin, hipEventDisableTiming));
-        HIPC(hipEventRecord(w.evin, (hipStream_t)a->stream));
-        HIPC(hipStreamWaitEvent(s, w.evin, 0));
+        if (int rc = order_after_caller(s, w.evin, a->stream, a->device)) return rc;
     }
     const size_t esz = a->dtype == TDA_F64 ? 8 : 4;
     size_t o = 0;

@@ -6,6 +6,8 @@
 // debug_tda_pipeline.py:92-150) with ~8 + 3*maxdim kernel launches on one
 // stream and a single host synchronisation at the end.
 #include <hip/hip_runtime.h>
+#include <link.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <chrono>
@@ -22,7 +24,6 @@
 #include "rips_reduce_big.h"
 #include "rips_reduce_par.h"
 #include "rips_reduce_small.h"
-#include "rips_dense.h"
 
 using namespace tda;
 
@@ -105,7 +106,7 @@ struct Plan {
     size_t o_bcomp = 0, o_bcheap = 0, o_bctl = 0;  // Borůvka H0 state (N > kH0WaveMaxN)
     bool serial_tables = false;  // HBM working tables of k_reduce_all (global mode) / k_reduce_big
     uint64_t ostride = 0, rec_cap = 0, rpool_cap = 0, bpool_cap = 0, rq_cap = 0;
-    size_t o_pctl = 0, o_pitem = 0, o_pokey = 0, o_poval = 0, o_colpiv = 0, o_prec = 0, o_prpool = 0, o_pbpool = 0, o_prq = 0;
+    size_t o_pctl = 0, o_pitem = 0, o_pokey = 0, o_poval = 0, o_colpiv = 0, o_prec = 0, o_prpool = 0, o_pbpool = 0, o_prq = 0, o_pdbg = 0;
     bool dense = false;  // N <= 64: dense-bitmap H1 chain + column-parallel H2 phase 1 (rips_reduce_small.h)
     int dK = 0;          // dense H1 bitmap words per lane (a k_h1_chain instantiation)
     uint32_t inv_stride = 0;  // rank -> edge table stride (C(N,3) rounded up)
@@ -119,13 +120,10 @@ struct Plan {
     uint32_t n2p = 0;         // stride of the per-layer edge-class table (N * N rounded up)
     uint32_t bm_words = 0;    // tetrahedron membership bitmap of k_h2_phase1 (words)
     uint32_t prep_lds = 0;    // dynamic LDS of k_prep_edges
-    bool fused = false;       // N <= 48: the whole dense path in one launch (k_dense_fused, rips_dense.h)
-    uint32_t fused_lds = 0;
-    size_t o_fdone = 0, o_fout = 0, o_f1k = 0, o_f1i = 0, o_froff = 0, o_frlen = 0;
     ReduceAllCfg rcfg = {};
     // byte offsets in the device workspace
     size_t o_x = 0, o_dist = 0, o_stats = 0, o_mst = 0, o_piv[4] = {0}, o_resid[4] = {0}, o_tmp = 0, o_rmk = 0, o_rmv = 0,
-           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_epos = 0, o_cobt = 0, o_lenr = 0, o_eM = 0, o_cpos = 0, o_necnt = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
+           o_voff = 0, o_vlen = 0, o_vpool = 0, o_wk = 0, o_wt = 0, o_wp = 0, o_wl = 0, o_vk = 0, o_vt = 0, o_vp = 0, o_vl = 0, o_bref = 0, o_recs = 0, o_cls2 = 0, o_cls = 0, o_res1 = 0, o_inv32 = 0, o_rof = 0, o_inv = 0, o_epos = 0, o_cobt = 0, o_eM = 0, o_necnt = 0, o_p1next = 0, o_p1k = 0, o_p1i = 0, o_p1x = 0, o_roff2 = 0, o_rlen2 = 0, o_rpool2 = 0, o_p1used = 0,
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
@@ -177,8 +175,7 @@ ReduceAllCfg reduce_cfg(int n, int maxdim, const uint64_t* piv_words, bool lds_m
 }
 
 // no_par: 0 = k_reduce_par for H1 and H2, 1 = H1 only (an H2 launch aborted), 2 = none
-// no_fused: the fused dense kernel gave up on this shape (ERR_FUSED): the multi-kernel dense path
-int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par, bool no_fused) {
+int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par) {
     const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
     p.mst_words = (binom(N, 2) + 31) / 32 + 1;
     for (int d = 1; d <= p.maxdim; ++d) {
@@ -258,14 +255,6 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par,
         if (p.chain_lds > (uint32_t)kLdsMax || p.prep_lds > (uint32_t)kLdsMax || p.p1_lds > (uint32_t)kLdsMax || p.dK == 0)
             p.dense = false;
     }
-    if (p.dense && !no_fused && test_env_is("TDA_FUSED", "1") && p.N >= 4 && binom(N, 2) <= 2048) {
-        bool kok = false;
-        for (int k : kFusedKs) kok |= k == p.dK;
-        const FCarve ca = fused_carve_a((int)N, p.dK, p.tri_stride, p.inv_stride, (uint32_t)p.piv_words[1]);
-        const FCarve cb = fused_carve_b((int)N, (uint32_t)p.piv_words[1]);
-        p.fused_lds = std::max<uint32_t>(ca.endA, p.maxdim >= 2 ? cb.endB : 0u);
-        p.fused = kok && p.fused_lds <= (uint32_t)kLdsMax;
-    }
     uint64_t maxp = 16;
     for (int d = 1; d <= p.maxdim; ++d) maxp = std::max(maxp, p.pcap[d]);
     p.sstride = 3 * maxp;
@@ -320,10 +309,6 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par,
     if (p.dense) {
         p.o_res1 = take(L * p.piv_words[1] * 4);
         p.o_necnt = take(L * 4);
-    }
-    if (p.fused) {
-        p.o_fdone = take(L * 4);
-        p.o_fout = take(8);
     }
     p.memset_hi = o;
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
@@ -381,6 +366,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par,
             p.o_prpool = take(p.rpool_cap * 8);
             p.o_pbpool = take(p.bpool_cap * 8);
             p.o_prq = take(p.rq_cap * 8);
+#ifdef TDA_PROFILE
+            p.o_pdbg = take((size_t)kParDbgCap * 32);
+#endif
         }
         if (p.dense) {
             p.o_recs = take(L * binom(N, 2) * 16);
@@ -388,20 +376,12 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par,
             p.o_cls = take(L * binom(N, 2) * 4);
             p.o_inv = take(L * (uint64_t)p.inv_stride * 2);
             p.o_epos = take(L * binom(N, 2) * 4);
-            p.o_lenr = take(L * (binom(N, 2) + 8) * 4);
             p.o_eM = take(L * binom(N, 2) * 8);
-            p.o_cpos = take(L * (binom(N, 2) + 8) * 4);
             if (p.fast) {
                 p.o_inv32 = take(L * (uint64_t)p.inv_stride * 4);
                 p.o_rof = take(L * (uint64_t)p.tri_stride * 2);
             }
             if (p.cmode == kChainTable) p.o_cobt = take(L * (uint64_t)p.cob_stride * 2);
-            if (p.fused && p.maxdim >= 2) {
-                p.o_f1k = take(L * kF2Cap * 4);
-                p.o_f1i = take(L * kF2Cap * 4);
-                p.o_froff = take(L * kF2Cap * 4);
-                p.o_frlen = take(L * kF2Cap * 4);
-            }
             if (p.maxdim >= 2) {
                 p.o_p1k = take(L * p.rcap[2] * 8);
                 p.o_p1i = take(L * p.rcap[2] * 4);
@@ -472,7 +452,6 @@ struct Workspace {
         bool force_global, force_big;
         int no_par;
         int scale;
-        bool no_fused;
     };
     std::vector<Retry> retry;
     std::mutex mu;
@@ -526,6 +505,66 @@ struct StageTimer {
         return 0;
     }
 };
+
+// ------------------------------------------------------------------ caller streams
+// Device input is read after the work the caller queued on its stream.  A NULL
+// handle is the null (legacy default) stream -- what torch's default stream is
+// on ROCm (raw handle 0).  Before r05 NULL meant "no ordering": a tensor that a
+// torch kernel had just written on the default stream (r04's torch.cat of the
+// coalesced sweeps) could be read by the library's non-blocking stream before
+// that kernel ran, i.e. as stale / uninitialised memory.
+//
+// Distinct HIP runtimes (libamdhip64 objects, by inode) mapped in the process.
+// The torch wheel ships its own copy with the same soname, so the dynamic linker
+// normally maps ONE of the two; a second one (a dlmopen'ed namespace,
+// RTLD_DEEPBIND) would own streams this library's runtime cannot use.
+int hip_runtimes_loaded() {
+    struct Acc {
+        dev_t dev[8];
+        ino_t ino[8];
+        int n;
+    } acc{};
+    dl_iterate_phdr(
+        [](struct dl_phdr_info* info, size_t, void* data) -> int {
+            auto* a = (Acc*)data;
+            const char* nm = info->dlpi_name;
+            const char* base = nm ? strrchr(nm, '/') : nullptr;
+            base = base ? base + 1 : nm;
+            if (!base || strncmp(base, "libamdhip64", 11) != 0) return 0;
+            struct stat st;
+            if (stat(nm, &st) != 0) return 0;
+            for (int i = 0; i < a->n; ++i)
+                if (a->dev[i] == st.st_dev && a->ino[i] == st.st_ino) return 0;
+            if (a->n < 8) a->dev[a->n] = st.st_dev, a->ino[a->n] = st.st_ino, ++a->n;
+            return 0;
+        },
+        &acc);
+    return acc.n;
+}
+
+// Order `lib` after the caller's stream (NULL = the null stream) with `ev`.  A
+// non-NULL handle must be a stream of THIS library's HIP runtime on `dev`:
+// hipStreamGetDevice validates it against the runtime's own stream set, so a
+// handle from another runtime, a destroyed stream or garbage is refused with
+// TDA_E_HIP instead of being dereferenced by hipEventRecord.
+int order_after_caller(hipStream_t lib, hipEvent_t ev, void* caller, int dev) {
+    if (caller) {
+        if (hip_runtimes_loaded() > 1)
+            return fail(TDA_E_HIP, "two HIP runtimes are loaded in this process: a caller stream handle cannot be trusted "
+                                   "(pass the input ready instead, TDA_FLAG_INPUT_READY)");
+        hipDevice_t d = -1;
+        const hipError_t e = hipStreamGetDevice((hipStream_t)caller, &d);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(TDA_E_HIP, std::string("caller stream is not a stream of this library's HIP runtime: ") + hipGetErrorString(e));
+        }
+        if ((int)d != dev)
+            return fail(TDA_E_INVALID, "caller stream is on device " + std::to_string((int)d) + ", the call on " + std::to_string(dev));
+    }
+    HIPC(hipEventRecord(ev, (hipStream_t)caller));
+    HIPC(hipStreamWaitEvent(lib, ev, 0));
+    return 0;
+}
 
 std::mutex g_ws_mu;
 // Graph capture + instantiation AND every workspace (re)allocation / free, across
@@ -678,9 +717,6 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_prep_edges, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_prep_tables, hipFuncAttributeMaxDynamicSharedMemorySize, (int)prep_tables_lds(kDenseMaxN)));
     HIPC(hipFuncSetAttribute((const void*)k_reduce_h2_finish, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-#define TDA_ATTR_FUSED(K) HIPC(hipFuncSetAttribute((const void*)k_dense_fused<K>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    TDA_ATTR_FUSED(1) TDA_ATTR_FUSED(2) TDA_ATTR_FUSED(3) TDA_ATTR_FUSED(4) TDA_ATTR_FUSED(6) TDA_ATTR_FUSED(9)
-#undef TDA_ATTR_FUSED
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
     HIPC(hipFuncSetAttribute((const void*)k_apparent<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -718,7 +754,7 @@ std::string err_flags(int e) {
 // ------------------------------------------------------------------ pipeline
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
-                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0, bool no_fused = false) {
+                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0) {
     const auto h_entry = std::chrono::steady_clock::now();
     Plan p;
     p.L = a.L;
@@ -728,7 +764,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     p.dtype = a.dtype;
     p.is_dist = input_kind != 0;
     p.want64 = input_kind == 0 && a.dtype == TDA_F64 && a.want_dist && (a.flags & TDA_FLAG_DIST64);
-    make_plan(p, force_global, scale, force_big, no_par, no_fused);
+    make_plan(p, force_global, scale, force_big, no_par);
     const int dev = a.device;
     HIPC(hipSetDevice(dev));
     Workspace& w = *get_ws(dev, a.slot);
@@ -739,10 +775,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     if (int rc = set_lds_attrs(dev)) return rc;
     // all work runs on the library stream, ordered after the caller's stream
     hipStream_t s = w.stream;
-    if (a.stream) {
-        HIPC(hipEventRecord(w.evin, (hipStream_t)a.stream));
-        HIPC(hipStreamWaitEvent(s, w.evin, 0));
-    }
+    if (a.x_on_device && input_kind != 2 && !(a.flags & TDA_FLAG_INPUT_READY))
+        if (int rc = order_after_caller(s, w.evin, a.stream, dev)) return rc;
     char* B = w.dbuf;
     const int n = (int)p.N, L = (int)p.L;
     float* dist = (float*)(B + p.o_dist);
@@ -881,7 +915,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.force_big = force_big;
     gk.no_par = no_par;
     gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0) |
-                 (p.wide ? 1 << 10 : 0) | (p.want64 ? 1 << 11 : 0) | (p.fused ? 1 << 12 : 0);
+                 (p.wide ? 1 << 10 : 0) | (p.want64 ? 1 << 11 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
     gk.sil_K = sil_K;  // baked into the k_silhouette launch (argument K and its LDS size)
@@ -974,85 +1008,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(hipGetLastError());
     MARK(input_kind != 0 ? "k_square_dist" : dist_mfma ? ((p.dsplit > 1 || p.gram_layer) && p.dtype == TDA_F32 ? "k_rowmax" : "k_distance_mfma") : "k_distance");
     HIPC(hipEventRecord(w.evf, s));  // fork point of the side streams
-
-    if (p.fused) {  // N <= 48: everything after the distances in one launch (rips_dense.h)
-        if (nls || want_tn) {  // silhouettes / TwoNN read the same matrices, beside it
-            hipStream_t s4 = w.stream4;
-            HIPC(hipStreamWaitEvent(s4, w.evf, 0));
-            if (int rc = tm4.begin()) return rc;
-            if (nls) {
-                const size_t lds = (size_t)sil_K * kSilT * 8 + (size_t)n * 4;
-                hipLaunchKernelGGL(k_silhouette, dim3(L, nls), dim3(kSilT), lds, s4, dist, n, (const int32_t*)w.hsil_dev, sil_K,
-                                   (double*)(w.hsil_dev + sil_out_off));
-                HIPC(hipGetLastError());
-                if (int rc = tm4.mark("k_silhouette")) return rc;
-            }
-            if (want_tn) {
-                const int pw2 = (int)next_pow2((uint64_t)std::max(n, 64));
-                hipLaunchKernelGGL(k_twonn, dim3(L), dim3(kTnT), (size_t)pw2 * 4, s4, dist, n, a.twonn_discard, a.twonn_eps, pw2, w.htn_dev);
-                HIPC(hipGetLastError());
-                if (int rc = tm4.mark("k_twonn")) return rc;
-            }
-            HIPC(hipEventRecord(w.evsil, s4));
-        }
-        FusedBufs fb = {};
-        fb.dist = dist;
-        fb.rowmax = rowmax;
-        fb.user_thresh = a.thresh;
-        fb.stats = stats;
-        for (int d = 0; d < 3; ++d) {
-            fb.pairs[d] = ps.p[std::min(d, p.maxdim)];
-            fb.pcap[d] = ps.cap[std::min(d, p.maxdim)];
-        }
-        fb.res1 = (uint32_t*)(B + p.o_res1);
-        fb.res1_words = p.piv_words[1];
-        fb.clsg = (uint32_t*)(B + p.o_cls);
-        fb.pool1 = (uint32_t*)(B + p.o_vpool);
-        fb.pool1_words = 2ull * p.vpool_cap;
-        fb.done = (uint32_t*)(B + p.o_fdone);
-        if (p.maxdim >= 2) {
-            fb.p1_key = (uint32_t*)(B + p.o_f1k);
-            fb.p1_info = (uint32_t*)(B + p.o_f1i);
-            fb.roff2 = (uint32_t*)(B + p.o_froff);
-            fb.rlen2 = (uint32_t*)(B + p.o_frlen);
-            fb.rpool2 = (uint64_t*)(B + p.o_rpool2);
-            fb.rpool2_cap = p.vpool_cap;
-        }
-        fb.out_used = (unsigned long long*)(B + p.o_fout);
-        fb.hout = w.hout_dev;
-        fb.hout_cap = w.hout_cap;
-        fb.houtoff = w.houtoff_dev;
-        fb.hstats = w.hstats_dev;
-        fb.step_limit = std::min<uint64_t>(step_limit(), 1ull << 16);  // N <= 48: far above any real column
-        fb.tri_stride = p.tri_stride;
-        fb.inv_stride = p.inv_stride;
-        fb.piv_words1 = (uint32_t)p.piv_words[1];
-        {
-            const char* fs = test_env("TDA_FUSED_STOP");
-            fb.stop = fs ? atoi(fs) : 0;
-        }
-        // one workgroup per CU (LDS): B(l) spins on A(l), so a chunk keeps both roles resident
-        const int chunk = p.maxdim >= 2 ? 128 : 256;
-        for (int l0 = 0; l0 < L; l0 += chunk) {
-            const int Lc = std::min(chunk, L - l0), L8 = (Lc + 7) & ~7;
-            const unsigned grid = p.maxdim >= 2 ? (unsigned)(2 * L8) : (unsigned)Lc;
-            switch (p.dK) {
-#define TDA_FUSED(K)                                                                                                    \
-    case K:                                                                                                             \
-        hipLaunchKernelGGL(k_dense_fused<K>, dim3(grid), dim3(kFT), p.fused_lds, s, fb, n, p.maxdim, l0, Lc, L8); \
-        break;
-                TDA_FUSED(1) TDA_FUSED(2) TDA_FUSED(3) TDA_FUSED(4) TDA_FUSED(6) TDA_FUSED(9)
-#undef TDA_FUSED
-                default:
-                    return fail(TDA_E_INVALID, "no k_dense_fused instantiation for this N");
-            }
-            HIPC(hipGetLastError());
-        }
-        MARK("k_dense_fused");
-        if (nls || want_tn) HIPC(hipStreamWaitEvent(s, w.evsil, 0));
-        HIPC(rec_t(w.ev1));
-        return 0;
-    }
 
     DenseBufs dnb = {};
 
@@ -1159,11 +1114,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             dnb.inv_stride = p.inv_stride;
             dnb.K = p.dK;
             dnb.epos = (uint32_t*)(B + p.o_epos);
-            dnb.lenr = (uint32_t*)(B + p.o_lenr);
             dnb.cobt = (uint16_t*)(B + p.o_cobt);
             dnb.cob_stride = p.cob_stride;
             dnb.eM = (uint64_t*)(B + p.o_eM);
-            dnb.cpos = (uint32_t*)(B + p.o_cpos);
             dnb.necnt = (uint32_t*)(B + p.o_necnt);
             const dim3 pg((unsigned)L, (unsigned)((dnb.E + kPrepEdges - 1) / kPrepEdges + 1));  // + the rank-sort block
             hipLaunchKernelGGL(k_prep_edges, pg, dim3(kPrepT), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode);
@@ -1478,6 +1431,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 pb.rq = (uint64_t*)(B + p.o_prq);
                 pb.rq_cap = p.rq_cap;
                 pb.step_limit = step_limit();
+                pb.dbg = p.o_pdbg ? (uint64_t*)(B + p.o_pdbg) : nullptr;
                 HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                 hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);
                 HIPC(hipGetLastError());
@@ -1624,34 +1578,29 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         const bool capacity = code == 21 || code == 22 || code == 41 || code == 53;  // pools / requeue slots
         if (capacity && scale < 2) {  // the same parallel reduction with larger pools
             guard.unlock();
-            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par, no_fused);
+            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par);
         }
         if (test_env_is("TDA_PAR_STRICT", "1"))  // tests: the parallel path itself must succeed
             return fail(TDA_E_CAPACITY, "k_reduce_par aborted: item " + std::to_string(c.err >> 16) + " code " +
                                             std::to_string(code));
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, np_next, no_fused);
-    }
-    if (p.fused && (errs & (ERR_FUSED | ERR_LDS_SPILL | ERR_VPOOL_CAP | ERR_STEP_LIMIT))) {
-        // the fused dense kernel gave up (LDS lists, spin limit, pools): the multi-kernel dense path
-        guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, no_par, true);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, np_next);
     }
     if ((errs & ERR_LDS_SPILL) && !force_global) {
         // a working column outgrew LDS: redo the batch with global-memory tables
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par, no_fused);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par);
     }
     if ((errs & ERR_WORK_CAP) && !p.big && !test_env_is("TDA_REDUCE", "wave")) {
         // a working column outgrew the one-wave HBM tables: full scans of a
         // large column are the slow case, so switch to the radix-heap kernel
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true, no_par, no_fused);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true, no_par);
     }
     if ((errs & ~(ERR_LDS_SPILL)) == (errs & (ERR_WORK_CAP | ERR_VPOOL_CAP)) && errs && scale < 2) {
         // working column / reduced-column pool too small: retry with larger buffers
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par, no_fused);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par);
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
 #ifdef TDA_PROFILE
@@ -1695,6 +1644,27 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 (unsigned long long)h[4]);
     }
     if (p.par) {
+        {   // long-column timeline of the last k_reduce_par launch (H2's when it ran, else H1's)
+            ParCtl c;
+            HIPC(hipMemcpy(&c, B + p.o_pctl, sizeof(c), hipMemcpyDeviceToHost));
+            const uint64_t nlog = std::min<uint64_t>(c.pad[1], kParDbgCap);
+            std::vector<uint64_t> d(nlog * 4);
+            if (nlog) HIPC(hipMemcpy(d.data(), B + p.o_pdbg, nlog * 32, hipMemcpyDeviceToHost));
+            std::vector<uint64_t> order(nlog);
+            for (uint64_t i = 0; i < nlog; ++i) order[i] = i;
+            std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) { return d[x * 4 + 2] - d[x * 4 + 1] > d[y * 4 + 2] - d[y * 4 + 1]; });
+            uint64_t tend = 0;
+            for (uint64_t i = 0; i < nlog; ++i) tend = std::max(tend, d[i * 4 + 2]);
+            fprintf(stderr, "[tda-prof] k_reduce_par timeline: %llu columns of >= %llu steps; last one ends %.3f ms after the first workgroup started\n",
+                    (unsigned long long)nlog, (unsigned long long)kParDbgMinSteps, nlog ? (tend - c.pad[0]) * 1e-5 : 0.0);
+            for (uint64_t k = 0; k < std::min<uint64_t>(nlog, 12); ++k) {
+                const uint64_t i = order[k];
+                fprintf(stderr, "[tda-prof]   layer %llu column %llu: start %.3f ms, %.3f ms, %llu steps%s\n",
+                        (unsigned long long)(d[i * 4] >> 40), (unsigned long long)(d[i * 4] & ((1ull << 40) - 1)),
+                        (d[i * 4 + 1] - c.pad[0]) * 1e-5, (d[i * 4 + 2] - d[i * 4 + 1]) * 1e-5,
+                        (unsigned long long)(d[i * 4 + 3] & ~(1ull << 63)), (d[i * 4 + 3] >> 63) ? " (resumed)" : "");
+            }
+        }
         const uint64_t* q = w.hstats[0].prof[2];
         fprintf(stderr, "[tda-prof] k_reduce_par longest column: %llu steps, %llu cycles: front_min %llu, pivot+rows %llu, apparent adds %llu, refills %llu (%llu), owner path %llu; avg front log %llu, compactions %llu, spills %llu\n",
                 (unsigned long long)q[6], (unsigned long long)q[0], (unsigned long long)q[1], (unsigned long long)q[2], (unsigned long long)q[3],
@@ -1736,7 +1706,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 #endif
 
-    if (force_global || scale || force_big || no_par || no_fused) {  // remember what this shape needed
+    if (force_global || scale || force_big || no_par) {  // remember what this shape needed
         bool seen = false;
         for (auto& m : w.retry)
             if (m.N == p.N && m.maxdim == p.maxdim && m.input_kind == input_kind) {
@@ -1744,10 +1714,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 m.force_big = m.force_big || force_big;
                 m.no_par = std::max(m.no_par, no_par);
                 m.scale = std::max(m.scale, scale);
-                m.no_fused = m.no_fused || no_fused;
                 seen = true;
             }
-        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale, no_fused});
+        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale});
     }
 
     // ---- result
@@ -1787,7 +1756,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         }
     }
     // layer-major result (tda_rips.h); the device wrote each (layer, dim) segment
-    // at houtoff, in layer order (k_emit) or in completion order (k_dense_fused)
+    // at houtoff, in layer order (k_emit)
     {
         size_t e = 0;
         for (int l = 0; l < L; ++l)
@@ -1898,7 +1867,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 
 // entry: start from the configuration an earlier call of this shape ended on
 int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_result** out) {
-    bool fg = false, fb = false, nf = false;
+    bool fg = false, fb = false;
     int np = 0;
     int sc = 0;
     // not when a test forces a reducer (the memo would override what it asks for)
@@ -1912,10 +1881,9 @@ int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_
                 fb = m.force_big;
                 np = m.no_par;
                 sc = m.scale;
-                nf = m.no_fused;
             }
     }
-    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np, nf);
+    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np);
 }
 
 int validate(const tda_rips_args* a) {

@@ -1211,10 +1211,9 @@ __global__ __launch_bounds__(1024) void k_h0(const float* __restrict__ dist, int
 // owns vertex v; Prim's frontier keys live in registers, the arg-min vertex is
 // found by ballot (no index decode); the <= 63 forest edges are sorted with an
 // in-register bitonic network.  Same results as k_h0.
-// The body is shared with the fused dense kernel (rips_dense.h), which runs it
-// on one wave of its workgroup: D is the layer's matrix in LDS, thr the
-// resolved threshold; forest edges go to mst_bits (LDS when MST_LDS, else
-// HBM, per-layer pointer), H0 pairs to P, the H0 stats to st.
+// Body: D is the layer's matrix in LDS, thr the resolved threshold; forest
+// edges go to mst_bits (LDS when MST_LDS, else HBM, per-layer pointer), H0
+// pairs to P, the H0 stats to st.
 template <bool MST_LDS>
 __device__ __forceinline__ void h0_wave_body(const float* D, int n, float thr, LayerStats* st, uint32_t* mst_bits, Pair* P) {
     const int v = lane_id();

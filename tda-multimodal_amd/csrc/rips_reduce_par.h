@@ -109,7 +109,10 @@ struct ParBufs {
     uint64_t* rq;         // requeue slots (used once per launch, zero = not yet written): item << 32 | record + 1
     uint64_t rq_cap;
     uint64_t step_limit;
+    uint64_t* dbg;        // -DTDA_PROFILE: [kParDbgCap][4] long-column timeline (layer << 40 | column, start, end, steps)
 };
+constexpr uint32_t kParDbgCap = 4096;
+constexpr uint64_t kParDbgMinSteps = 256;  // columns with at least this many steps are logged
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint64_t ald(const uint64_t* p) {  // sc1 load (agent scope)
@@ -1081,6 +1084,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
     }
     __syncthreads();
     const uint64_t total = ald(&P.ctl->total);
+#ifdef TDA_PROFILE
+    if (tid == 0) atomicMin((unsigned long long*)&P.ctl->pad[0], (unsigned long long)wall_clock64());
+#endif
     bool prealloc = false;
     for (;;) {
         // ---------------- get work (lane 0): requeued columns first, then fresh ones.
@@ -1200,7 +1206,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         bool done = false;
 #ifdef TDA_PROFILE
         uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nref = 0, fsum = 0;
-        const uint64_t t_col = clock64();
+        const uint64_t t_col = clock64(), w_col = wall_clock64();
         C.ncompact = C.nspill = 0;
         for (int q = 0; q < 8; ++q) C.q[q] = C.q2[q] = C.q3[q] = 0;
 #endif
@@ -1390,6 +1396,17 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             for (int q = 0; q < 8; ++q) stats[0].prof[1][q] = C.q3[q];
         }
 #endif
+#ifdef TDA_PROFILE
+        if (tid == 0 && step >= kParDbgMinSteps && P.dbg) {  // the long columns' timeline (wall clock, 100 MHz)
+            const uint64_t q = aadd(&P.ctl->pad[1], 1ull);
+            if (q < kParDbgCap) {
+                P.dbg[q * 4 + 0] = ((uint64_t)l << 40) | j;
+                P.dbg[q * 4 + 1] = w_col;
+                P.dbg[q * 4 + 2] = wall_clock64();
+                P.dbg[q * 4 + 3] = step | (rec0 ? 1ull << 63 : 0ull);
+            }
+        }
+#endif
         if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)adds);
         if (done && my_rec >= 0 && my_seg) {  // the claimed record references this workgroup's chunks: fresh ones next
             for (uint32_t e = tid; e < (uint32_t)kParLv * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
@@ -1433,6 +1450,7 @@ __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats
         unsigned long long* c = (unsigned long long*)P.ctl;
         for (int q = 0; q < (int)(sizeof(ParCtl) / 8); ++q) c[q] = 0;
         P.ctl->total = s;
+        P.ctl->pad[0] = ~0ull;  // -DTDA_PROFILE: earliest workgroup start (atomicMin)
     }
 }
 

@@ -111,9 +111,7 @@ struct DenseBufs {
     uint32_t n2p;
     uint32_t* res1;     // [L][piv_words1] colex bitmap of residual H1 pivots (H2 clearing; zeroed per call)
     uint32_t* epos;     // [L][E] rank of the edge among edges <= thresh (kNoRank above)
-    uint32_t* lenr;     // [L][E + 8] length bits by rank
     uint64_t* eM;       // [L][E] block masks
-    uint32_t* cpos;     // [L][E + 8] block sizes by rank (k_prep_tables scans them in LDS)
     uint32_t* necnt;    // [L] edges <= thresh (zeroed per call)
     uint16_t* cobt;     // [L][cob_stride] TABLE chain: rank of {a, b, v} at e * n + v
     uint32_t cob_stride;
@@ -424,8 +422,8 @@ __global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restri
 //   kChainFast (N <= ~51): rank_of[triangle] + inv32 in LDS.
 //   kChainGeneral: edge records (youngest facet, block mask) + inv16.
 // LDS: [16][D][recs E | rank_of | cobt][inv16 | inv32][W 64K][res 64K][piv][cols][own].
-// The serial chain of k_h1_chain (wave 0 after the staging), shared with the
-// fused dense kernel (rips_dense.h): every table pointer is the layer's (LDS
+// The serial chain of k_h1_chain (wave 0 after the staging): every table
+// pointer is the layer's (LDS
 // where the MODE reads it from LDS), cols holds the nc non-cleared residual
 // columns in column order, nskip the cleared ones (stats only).
 struct ChainCtx {

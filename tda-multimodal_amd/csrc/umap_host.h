@@ -99,10 +99,9 @@ extern "C" int tda_umap_batch(const tda_umap_args* a) {
     }
     char* B = w.buf;
     hipStream_t s = w.stream;
-    if (a->stream) {  // device inputs: read after the caller's queued work (torch's current stream)
+    if (a->x_on_device) {  // device inputs: read after the caller's queued work (NULL = the null stream)
         if (!w.evin) HIPC(hipEventCreateWithFlags(&w.evin, hipEventDisableTiming));
-        HIPC(hipEventRecord(w.evin, (hipStream_t)a->stream));
-        HIPC(hipStreamWaitEvent(s, w.evin, 0));
+        if (int rc = order_after_caller(s, w.evin, a->stream, a->device)) return rc;
     }
     const void* x = a->x;
     if (!a->x_on_device) {
@@ -196,10 +195,9 @@ extern "C" int tda_umap_transform(const tda_umap_transform_args* a) {
     std::lock_guard<std::mutex> guard(w.mu);
     if (!w.stream) HIPC(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
     hipStream_t s = w.stream;
-    if (a->stream) {
+    if (a->x_on_device) {  // device inputs: read after the caller's queued work (NULL = the null stream)
         if (!w.evin) HIPC(hipEventCreateWithFlags(&w.evin, hipEventDisableTiming));
-        HIPC(hipEventRecord(w.evin, (hipStream_t)a->stream));
-        HIPC(hipStreamWaitEvent(s, w.evin, 0));
+        if (int rc = order_after_caller(s, w.evin, a->stream, a->device)) return rc;
     }
     const size_t esz = a->dtype == TDA_F64 ? 8 : 4;
     const uint64_t ecap = (uint64_t)M * k;

@@ -202,25 +202,28 @@ class PipelinedSweep:
             import torch
 
             torch.cuda.set_device(self.device)  # the current device is per thread
-        group, gids = [], []
+        held = []  # this exchange group's steps (SweepPipeline futures or results), in step order
         while True:
             res = self.q.get()
+            if res is not None and self.err is None:
+                held.append(res)
+            if res is None or len(held) == self.group:
+                # futures are waited on only once the group is complete (or at close()): a result()
+                # on a pending future would dispatch its batch early, with fewer sweeps than
+                # `coalesce`
+                if held and self.err is None:
+                    try:
+                        group, gids = [], []
+                        for r in held:
+                            r = r.result() if hasattr(r, "result") else r
+                            gids.append(self.ids + len(gids) * self.total)  # the step's place in its exchange group
+                            group.extend(r)
+                        self._exchange(group, gids)
+                    except BaseException as e:  # re-raised by the next step() or close()
+                        self.err = e
+                held = []
             if res is None:
-                if group and self.err is None:
-                    self._exchange(group, gids)
                 return
-            if self.err is not None:  # after a failure: keep draining, so step() / close() never block on a full queue
-                continue
-            try:
-                if hasattr(res, "result"):  # a SweepPipeline future: this step's own layers, in step order
-                    res = res.result()
-                gids.append(self.ids + len(gids) * self.total)  # the step's place in its exchange group
-                group.extend(res)
-                if len(gids) == self.group:
-                    self._exchange(group, gids)
-                    group, gids = [], []
-            except BaseException as e:  # re-raised by the next step() or close()
-                self.err = e
 
     def _exchange(self, group, gids):
         k = len(gids)

@@ -337,6 +337,8 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
     a.flags = (_lib.TDA_FLAG_STAGE_TIMES | (_lib.TDA_FLAG_STAGE_SERIAL if stage_serial else 0)) if stage_times else 0
     if one_stream:
         a.flags |= _lib.TDA_FLAG_ONE_STREAM
+    if input_ready:
+        a.flags |= _lib.TDA_FLAG_INPUT_READY
     if not persistence:
         if maxdim != 0:
             raise ValueError("persistence=False needs maxdim=0")
@@ -493,7 +495,8 @@ class SweepPipeline:
         self._ex = [ThreadPoolExecutor(max_workers=1) for _ in range(depth)]  # one thread per slot: calls on a slot stay ordered
         self._n = 0
         self._lock = threading.Lock()
-        self._pending = []  # (X, args, future) not yet dispatched
+        self._pending = []  # (X, args, future, producer event or None) not yet dispatched
+        self._streams = [None] * depth  # per executor: the side stream its calls order their reads after
         self._pkey = None
         self._run = run  # the batch call (default ripser_batch; CPU tests pass a stand-in)
 
@@ -505,8 +508,17 @@ class SweepPipeline:
 
     @staticmethod
     def _key(X, args):
+        """Sweeps coalesce only with the same FULL shape (the C ABI's parts are
+        equal: L % n_parts == 0), dtype, device and arguments.  Scalar
+        arguments compare by value; anything else (label arrays, lists) by
+        identity -- a repr() of a large numpy array is summarised and two
+        different arrays could compare equal."""
         dev = (X.device.type, X.device.index) if _is_torch(X) else None
-        return (type(X).__module__, dev, tuple(X.shape[1:]), str(X.dtype), tuple(sorted((k, repr(v)) for k, v in args.items())))
+
+        def val(v):
+            return ("v", v) if v is None or isinstance(v, (bool, int, float, str)) else ("id", id(v))
+
+        return (type(X).__module__, dev, tuple(X.shape), str(X.dtype), tuple(sorted((k, val(v)) for k, v in args.items())))
 
     def submit(self, X, **kw):
         self._check_kw(kw)
@@ -515,13 +527,22 @@ class SweepPipeline:
             X = np.asarray(X)
         if X.ndim != 3:
             raise ValueError("X must be (L, N, D)")
+        ev = None
+        if _is_torch(X) and X.is_cuda and not args.get("input_ready"):
+            # ordered after the SUBMITTING thread's current stream, as of now: the call may be
+            # dispatched later, from another thread (a future's result()), or after the caller
+            # left a `with torch.cuda.stream(...)` block
+            import torch
+
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(X.device))
         with self._lock:
             key = self._key(X, args)
             if self._pending and (key != self._pkey or self.coalesce == 1):
                 self._dispatch_locked()
             lo = sum(int(p[0].shape[0]) for p in self._pending)
             f = _SweepFuture(self, lo, lo + int(X.shape[0]))
-            self._pending.append((X, args, f))
+            self._pending.append((X, args, f, ev))
             self._pkey = key
             if len(self._pending) >= self.coalesce:
                 self._dispatch_locked()
@@ -546,25 +567,30 @@ class SweepPipeline:
         self._n += 1
         args = dict(batch[0][1])
         Xs = [b[0] for b in batch]
-        if _is_torch(Xs[0]) and Xs[0].is_cuda:
-            # the worker thread's current stream is its own default stream: order the
-            # read after the SUBMITTING thread's current stream (where X -- and the
-            # concatenation below -- were produced)
+        evs = [b[3] for b in batch if b[3] is not None]
+        X = Xs[0] if len(Xs) == 1 else Xs  # parts: gathered on the device by the library (ABI 6)
+        if evs:
+            # every part's producer, as recorded at its submit(): the call runs on a side stream
+            # of this executor that waits on all of them, and the library orders its reads
+            # after that stream
             import torch
 
-            caller = torch.cuda.current_stream(Xs[0].device)
-            X = Xs[0] if len(Xs) == 1 else Xs  # parts: gathered on the device by the library (ABI 6)
+            dev = Xs[0].device
+            if self._streams[e] is None:
+                self._streams[e] = torch.cuda.Stream(dev)
+            ws = self._streams[e]
 
             def call():
-                with torch.cuda.stream(caller):
+                for ev in evs:
+                    ws.wait_event(ev)
+                with torch.cuda.stream(ws):
                     return run(X, device=self.device, slot=s, **args)
 
             cf = self._ex[e].submit(call)
         else:
-            X = Xs[0] if len(Xs) == 1 else Xs
             cf = self._ex[e].submit(run, X, device=self.device, slot=s, **args)
-        for _, _, f in batch:
-            f._call, f._n = cf, len(batch)
+        for b in batch:
+            b[2]._call, b[2]._n = cf, len(batch)
 
     def close(self):
         self.flush()

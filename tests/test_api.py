@@ -232,3 +232,42 @@ def test_ripser_batch_parts_validation(pkg):
         pkg.ripser_batch([a] * 17, maxdim=1)
     with pytest.raises(ValueError):
         pkg.ripser_batch([a, np.full((2, 5, 3), np.nan, np.float32)], maxdim=1)
+
+
+def test_sweep_pipeline_uneven_layer_counts_never_share_a_call(pkg):
+    """sweeps with different layer counts (a final partial sweep)
+    must not be coalesced -- the C ABI's parts are equal (L % n_parts == 0) and
+    ripser_batch refuses unequal parts with ValueError.  With the real
+    ripser_batch (no GPU here) each sweep is its own call and fails at the
+    device check instead."""
+    with pkg.SweepPipeline(depth=1, coalesce=4, maxdim=1) as pipe:
+        f3 = pipe.submit(np.zeros((3, 5, 3), np.float32))
+        f2 = pipe.submit(np.zeros((2, 5, 3), np.float32))
+        for f in (f3, f2):
+            with pytest.raises(RuntimeError):  # NODEVICE, never "parts must share shape"
+                f.result()
+
+
+def test_sweep_pipeline_array_kwargs_compare_by_identity(pkg, monkeypatch):
+    """two different large per-submit arrays (whose numpy reprs are
+    summarised to the same text) are different arguments: no coalescing."""
+    rip = importlib.import_module("tda-multimodal_amd.ripser")
+    calls = []
+
+    def fake(X, device=0, slot=0, labels=None, **kw):
+        n = len(X) if isinstance(X, list) else 1
+        calls.append((n, labels))
+        L = sum(x.shape[0] for x in X) if isinstance(X, list) else X.shape[0]
+        return [0.0] * L
+
+    monkeypatch.setattr(rip, "ripser_batch", fake)
+    a = [np.zeros(5000, np.int32)]
+    b = [np.zeros(5000, np.int32)]
+    b[0][2500] = 1  # same summarised repr, different content
+    assert repr(a[0]) == repr(b[0])
+    with pkg.SweepPipeline(depth=1, coalesce=4, maxdim=1) as pipe:
+        fs = [pipe.submit(np.zeros((2, 5, 3), np.float32), labels=lab) for lab in (a, a, b)]
+        for f in fs:
+            f.result()
+    assert [c[0] for c in calls] == [2, 1]
+    assert calls[0][1] is a and calls[1][1] is b

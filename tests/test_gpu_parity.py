@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, ROOT
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5  # north_star tolerance on filtration values
@@ -795,3 +795,61 @@ def test_dist64_flag_with_want_dist_toggled_at_the_c_abi(gpu):
         assert (o[0].dist64 is not None) == bool(w)
     d = X[0][:, None, :] - X[0][None, :, :]
     np.testing.assert_allclose(outs[2][0].dist64, np.sqrt((d * d).sum(-1)), rtol=1e-9, atol=1e-9)
+
+
+def test_device_input_ordered_after_torch_default_stream(gpu):
+    """VERDICT r04 #6 / DESIGN §6.6: torch's default stream is the null stream
+    (raw handle 0).  Before ABI 7 a NULL caller stream meant "no ordering", so
+    a tensor a torch kernel had just written on the default stream could be
+    read by the library's non-blocking stream before that kernel ran (r04's
+    torch.cat of coalesced sweeps: stale input -- the likely source of r04's
+    illegal-address fault).  Here the input is written by a copy queued
+    behind ~tens of ms of matmuls on the default stream, and the library is
+    called with no synchronisation: the result must equal the synchronised
+    call.  Run once."""
+    import torch
+
+    X0 = gpu.synthetic.sweep48(32)
+    ref = gpu.ripser_batch(X0, maxdim=2)
+    src = torch.from_numpy(X0).cuda()
+    torch.cuda.synchronize()
+    assert torch.cuda.current_stream().cuda_stream == 0  # the null stream (what this test is about)
+    X = torch.full_like(src, float("nan"))
+    torch.cuda.synchronize()
+    big = torch.randn(4096, 4096, device="cuda")
+    for _ in range(12):  # queue work ahead of the copy on the default stream
+        big = (big @ big) * 1e-3
+    X.copy_(src)  # runs after the matmuls
+    got = gpu.ripser_batch(X, maxdim=2)  # no synchronisation: the library must order after the null stream
+    for l in range(32):
+        assert got[l].checksum == ref[l].checksum
+        assert all(np.array_equal(a, b) for a, b in zip(got[l].dgms, ref[l].dgms))
+
+
+def test_foreign_caller_stream_is_refused(gpu):
+    """A caller stream handle that is not a stream of the library's HIP
+    runtime (another runtime's handle, a destroyed stream, garbage) is
+    refused with TDA_E_HIP before any use (rips.hip order_after_caller).  In a
+    child process, so a runtime that did dereference it could not take the
+    test session down."""
+    import subprocess
+    import sys
+
+    code = (
+        "import ctypes, importlib, sys, numpy as np, torch\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "torch.cuda.init()\n"
+        "pkg = importlib.import_module('tda-multimodal_amd')\n"
+        "X = torch.from_numpy(pkg.synthetic.sweep48(2)).cuda(); torch.cuda.synchronize()\n"
+        "junk = ctypes.create_string_buffer(4096)\n"
+        "a = pkg._lib.RipsArgs(); a.x = X.data_ptr(); a.x_on_device = 1; a.dtype = 0; a.L, a.N, a.D = 2, 48, 3\n"
+        "a.maxdim = 1; a.thresh = float('inf'); a.modulus = 2; a.device = 0; a.stream = ctypes.addressof(junk)\n"
+        "res = ctypes.POINTER(pkg._lib.RipsResult)()\n"
+        "rc = pkg.lib().tda_rips_batch(ctypes.byref(a), ctypes.byref(res))\n"
+        "print('RC', rc, pkg.lib().tda_last_error().decode())\n"
+    )
+    env = dict(os.environ, TDA_TEST_OVERRIDES="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RC")][0]
+    assert line.startswith("RC -3") and "caller stream" in line, line
