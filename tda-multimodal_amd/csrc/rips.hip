@@ -366,8 +366,8 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
             p.o_prpool = take(p.rpool_cap * 8);
             p.o_pbpool = take(p.bpool_cap * 8);
             p.o_prq = take(p.rq_cap * 8);
-#ifdef TDA_PROFILE
-            p.o_pdbg = take((size_t)kParDbgCap * 32);
+#if defined(TDA_PROFILE) || defined(TDA_PROF2)
+            p.o_pdbg = take((size_t)kParDbgCap * 32 + (size_t)kParDbgCap * kParP2Words * 8);
 #endif
         }
         if (p.dense) {
@@ -1431,7 +1431,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 pb.rq = (uint64_t*)(B + p.o_prq);
                 pb.rq_cap = p.rq_cap;
                 pb.step_limit = step_limit();
-                pb.dbg = p.o_pdbg ? (uint64_t*)(B + p.o_pdbg) : nullptr;
+                pb.dbg = p.o_pdbg ? (uint64_t*)(B + p.o_pdbg) : nullptr;  // profile builds only
                 HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                 hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);
                 HIPC(hipGetLastError());
@@ -1603,6 +1603,29 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par);
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
+#ifdef TDA_PROF2
+    if (p.par) {  // per-wave phase cycles of the long columns (k_reduce_par, the last launch)
+        ParCtl c;
+        HIPC(hipMemcpy(&c, B + p.o_pctl, sizeof(c), hipMemcpyDeviceToHost));
+        const uint64_t nrec = std::min<uint64_t>(c.pad[2], kParDbgCap);
+        std::vector<uint64_t> d(nrec * kParP2Words);
+        if (nrec) HIPC(hipMemcpy(d.data(), B + p.o_pdbg + (size_t)kParDbgCap * 32, nrec * kParP2Words * 8, hipMemcpyDeviceToHost));
+        static const char* nm[8] = {"room+barrier", "min", "pivot+loads", "keys", "appends", "toggles", "refills", "owner"};
+        uint64_t best = ~0ull, bsteps = 0;
+        for (uint64_t i = 0; i < nrec; ++i)
+            if (d[i * kParP2Words + 2] > bsteps) bsteps = d[i * kParP2Words + 2], best = d[i * kParP2Words];
+        for (uint64_t i = 0; i < nrec; ++i) {
+            const uint64_t* r = &d[i * kParP2Words];
+            if (r[0] != best) continue;
+            uint64_t tot = 0;
+            for (int u = 0; u < 8; ++u) tot += r[3 + u];
+            fprintf(stderr, "[tda-prof2] layer %llu column %llu wave %llu: %llu steps, %.0f cycles/step:", (unsigned long long)(r[0] >> 40),
+                    (unsigned long long)(r[0] & ((1ull << 40) - 1)), (unsigned long long)r[1], (unsigned long long)r[2], (double)tot / (double)r[2]);
+            for (int u = 0; u < 8; ++u) fprintf(stderr, " %s %.0f", nm[u], (double)r[3 + u] / (double)r[2]);
+            fprintf(stderr, "\n");
+        }
+    }
+#endif
 #ifdef TDA_PROFILE
     if (p.dense && !p.par) {
         int arg = 0;

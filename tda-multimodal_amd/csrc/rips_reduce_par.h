@@ -112,6 +112,8 @@ struct ParBufs {
     uint64_t* dbg;        // -DTDA_PROFILE: [kParDbgCap][4] long-column timeline (layer << 40 | column, start, end, steps)
 };
 constexpr uint32_t kParDbgCap = 4096;
+constexpr uint32_t kParP2Words = 12;       // -DTDA_PROF2 record: layer << 40 | column, wave, steps, 8 phase cycle sums, spare
+constexpr uint64_t kParP2MinSteps = 1000;
 constexpr uint64_t kParDbgMinSteps = 256;  // columns with at least this many steps are logged
 
 // ------------------------------------------------------------------ helpers
@@ -423,11 +425,60 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
 // allocates chunk c + 2, so a pass of up to 3072 keys per bucket never needs a
 // chunk that is not there yet (chunks c and c + 1 hold >= 3072 keys from c = 2
 // on).  Callers put a barrier between passes that may open new chunks.
+#ifndef TDA_PAR_WAGG  // build-time A/B knob (tools/): bit 0 = refill histogram, bit 1 = bucket slots, wave-aggregated
+#define TDA_PAR_WAGG 0
+#endif
+
+// Wave-aggregated LDS counters: the keys of one wave that hit the same counter
+// (a radix level) take their slots with ONE atomic by a leader lane instead
+// of one per key (a step's ~600 back keys and a refill's ~3 K keys fall into a
+// handful of levels: same-address LDS atomics serialise lane by lane).
+// Returns each valid lane's old value + its rank among the wave's lanes on the
+// same counter.  Wave-uniform control flow: every lane of the wave calls it.
+__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr, uint32_t b, bool valid) {
+    const int ln = threadIdx.x & 63;
+    uint64_t todo = __ballot(valid);
+    int lead = 0;
+    uint32_t rank = 0, cnt = 0;
+    while (todo) {  // one iteration per distinct counter among the valid lanes
+        const int l0 = __builtin_ctzll(todo);
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)b, l0);
+        const uint64_t m = __ballot(valid && b == b0);
+        if ((m >> ln) & 1ull) {
+            lead = l0;
+            rank = lanes_below(m);
+        }
+        if (ln == l0) cnt = (uint32_t)__popcll(m);
+        todo &= ~m;
+    }
+    uint32_t base = 0;
+    if (valid && lead == ln) base = atomicAdd(&ctr[b], cnt);  // one ds_add_rtn for all groups' leaders
+    base = (uint32_t)__shfl((int)base, lead, 64);
+    return base + rank;
+}
+// the same without slots: hist[b] += (valid lanes on b)
+__device__ __forceinline__ void wave_count(uint32_t* hist, uint32_t b, bool valid) {
+    const int ln = threadIdx.x & 63;
+    uint64_t todo = __ballot(valid);
+    while (todo) {
+        const int l0 = __builtin_ctzll(todo);
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)b, l0);
+        const uint64_t m = __ballot(valid && b == b0);
+        if (ln == l0) atomicAdd(&hist[b0], (uint32_t)__popcll(m));
+        todo &= ~m;
+    }
+}
+
 template <int R>
 __device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint32_t (&bb)[R], uint32_t vmask, const ParBufs& P) {
     uint32_t slot[R];
+#if TDA_PAR_WAGG & 2
+#pragma unroll
+    for (int r = 0; r < R; ++r) slot[r] = wave_slot(PS.bcnt, bb[r], (vmask >> r) & 1u);
+#else
 #pragma unroll
     for (int r = 0; r < R; ++r) slot[r] = ((vmask >> r) & 1u) ? atomicAdd(&PS.bcnt[bb[r]], 1u) : 0u;
+#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (!((vmask >> r) & 1u)) continue;
@@ -456,6 +507,11 @@ __device__ __forceinline__ uint64_t bucket_at(const ParBufs& P, uint32_t b, uint
 struct ParCol {
     ParRed rd;
     uint64_t steps = 0, adds = 0;
+#ifdef TDA_PROF2
+    // per-wave phase cycles of the current column (SHADER_CYCLES deltas: no memory op, no wait):
+    // room + step barrier, front min, pivot + row loads, keys, bucket appends, front toggles, refills, owner path / records
+    uint32_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 #ifdef TDA_PROFILE
     uint64_t ncompact = 0, nspill = 0;
     uint64_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // keys, front toggle, bucket append, capacity, R adds, R entries, refill keys, load wait
@@ -463,6 +519,20 @@ struct ParCol {
     uint64_t q3[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // refill: search, pass 1 (loads + min), pass 2 (histogram), level choice, toggles, appends, compactions, keys kept in front
 #endif
 };
+#ifdef TDA_PROF2
+__device__ __forceinline__ uint32_t p2_now() {
+    uint32_t c;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_SHADER_CYCLES, 0, 20)" : "=s"(c) : : "memory");
+    return c;
+}
+#define P2_T(v) const uint32_t v = p2_now()
+#define P2_ACC(i, v) C.tp[i] += (p2_now() - (v)) & 0xFFFFFu
+#define P2_DEP(x) asm volatile("" : : "v"(x))
+#else
+#define P2_T(v)
+#define P2_ACC(i, v)
+#define P2_DEP(x)
+#endif
 #ifdef TDA_PROFILE
 #define PAR_T0(v) const uint64_t v = clock64()
 #define PAR_ACC(i, v) C.q[i] += clock64() - (v)
@@ -518,6 +588,9 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
 // Back keys of one coboundary round kept in registers: appended to their HBM
 // buckets during the NEXT step, while that step's row loads are in flight
 // (they never affect the next pivot: every back key is above every front key).
+#ifndef TDA_PAR_STASH  // build-time A/B knob (tools/): 1 = r04's deferred back-key appends (stash)
+#define TDA_PAR_STASH 0
+#endif
 struct ParStash {
     uint64_t k[kParRV];
     uint32_t b[kParRV];
@@ -541,6 +614,7 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
 #ifdef TDA_PROFILE
     C.q[7] += (wave_sum_u64((uint64_t)__builtin_popcount(fm)) << 32) | wave_sum_u64((uint64_t)__builtin_popcount(bm));  // wave 0's front / back keys
 #endif
+#if TDA_PAR_STASH
     PAR_T0(tf0);
     front_toggle<R>(k, fm);
     PAR_ACC(1, tf0);
@@ -555,6 +629,24 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
     PAR_T0(tb0);
     bucket_append<R>(k, bb, bm, P);
     PAR_ACC(2, tb0);
+#else
+    // back keys first: their stores are issued as early as possible, so they are
+    // acknowledged before the next step waits for its row loads (gfx950 has no
+    // separate store counter: a load's s_waitcnt vmcnt also waits for every
+    // store issued before it -- with the r04 stash, the previous step's ~600
+    // bucket stores went out right after the row loads and sat in their wait)
+    (void)stash;
+    PAR_T0(tb0);
+    P2_T(pb0);
+    bucket_append<R>(k, bb, bm, P);
+    P2_ACC(4, pb0);
+    PAR_ACC(2, tb0);
+    PAR_T0(tf0);
+    P2_T(pf0);
+    front_toggle<R>(k, fm);
+    P2_ACC(5, pf0);
+    PAR_ACC(1, tf0);
+#endif
 }
 
 __device__ __forceinline__ void stash_flush(ParCol& C, const ParBufs& P, ParStash& st) {
@@ -627,21 +719,25 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     // levels that hold at most kFrontFill keys.  (A binary search on the level
     // with block counts instead of the atomics measured slower: 7.1 vs 4.3 M
     // cycles over torus1024's refills.)
+#if TDA_PAR_WAGG & 1
+#define PAR_HIST_ADD(key, valid) wave_count(PS.hist, par_bucket((key), nl), (valid))
+#else
+#define PAR_HIST_ADD(key, valid) do { if (valid) atomicAdd(&PS.hist[par_bucket((key), nl)], 1u); } while (0)
+#endif
     if (inreg) {
 #pragma unroll
         for (int h = 0; h < kParRefill; ++h)
 #pragma unroll
-            for (int r = 0; r < kParRegs; ++r)
-                if ((vm[h] >> r) & 1u) atomicAdd(&PS.hist[par_bucket(x[h][r], nl)], 1u);
+            for (int r = 0; r < kParRegs; ++r) PAR_HIST_ADD(x[h][r], (vm[h] >> r) & 1u);
     } else {
         for (uint32_t e0 = 0; e0 < c; e0 += kPass) {
             uint64_t y[kParRegs];
             const uint32_t ym = bucket_batch(P, (uint32_t)b, e0, c, y);
 #pragma unroll
-            for (int r = 0; r < kParRegs; ++r)
-                if ((ym >> r) & 1u) atomicAdd(&PS.hist[par_bucket(y[r], nl)], 1u);
+            for (int r = 0; r < kParRegs; ++r) PAR_HIST_ADD(y[r], (ym >> r) & 1u);
         }
     }
+#undef PAR_HIST_ADD
     __syncthreads();
     int keep = par_keep_level(PS.hist, b, kFrontFill);
     const uint32_t cnt0 = PS.hist[0];  // keys equal to nl (level 0)
@@ -730,6 +826,7 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
             }
         }
         PAR_T0(tk0);
+        P2_T(pk0);
         uint64_t key[kParRV];
         uint32_t vm = 0;
 #pragma unroll
@@ -760,6 +857,8 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
             key[q] = ((uint64_t)__float_as_uint(cd + 0.0f) << 32) | tri_lo<PACKED>(x, y, z, f);
             vm |= 1u << q;
         }
+        P2_DEP(vm);
+        P2_ACC(3, pk0);
         PAR_ACC(0, tk0);
         col_add<kParRV>(C, P, key, vm, v0 == 0 ? stash : nullptr);  // no barrier: the caller made room for all n keys
     }
@@ -1213,8 +1312,13 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         uint64_t step = 0;
         const uint32_t need = par_need(n);
         ParStash stash;
+#ifdef TDA_PROF2
+        for (int q = 0; q < 8; ++q) C.tp[q] = 0;
+#endif
         for (; !done; ++step) {
+            P2_T(ps0);
             front_room(C, P, need);  // barrier: the previous step's toggles and appends are done
+            P2_ACC(0, ps0);
             if (PS.err) break;
             if (step > P.step_limit) {
                 if (tid == 0) PS.err = 61;
@@ -1224,7 +1328,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             fsum += PS.fcnt;
             uint64_t t0 = clock64();
 #endif
+            P2_T(ps1);
             uint64_t pk = front_min(C.rd);
+            P2_ACC(1, ps1);
 #ifdef TDA_PROFILE
             pf[1] += clock64() - t0;
             t0 = clock64();
@@ -1233,8 +1339,10 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #ifdef TDA_PROFILE
                 ++nref;
 #endif
+                P2_T(ps6);
                 stash_flush(C, P, stash);  // the refill reads every bucket count
                 const bool more = col_refill(C, P);
+                P2_ACC(6, ps6);
 #ifdef TDA_PROFILE
                 pf[4] += clock64() - t0;
 #endif
@@ -1246,6 +1354,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 continue;
             }
             // pivot: vertices, index, apparent facet fv
+            P2_T(ps2);
             int fv[DIM + 1];
             uint64_t pidx;
             const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
@@ -1297,6 +1406,8 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             const uint32_t pw = ld_glb(pivg, pidx >> 5);
             stash_flush(C, P, stash);  // the previous step's back keys, under this step's load latency
             const bool app = (pw >> (pidx & 31)) & 1u;
+            P2_DEP(pw);
+            P2_ACC(2, ps2);
 #ifdef TDA_PROFILE
             pf[2] += clock64() - t0;
             t0 = clock64();
@@ -1313,6 +1424,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 continue;
             }
             // ---------------- residual pivot: owner map
+            P2_T(ps7);
             const uint64_t fkey = WIDE ? pk : filt_key(pd, pidx);  // colpiv: k_par_emit decodes it
             for (uint32_t round = 0;; ++round) {
                 if (tid == 0) {
@@ -1380,6 +1492,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             }
             // a record added above changes the column: any saved record is stale
             if (!done) my_rec = -1;
+            P2_ACC(7, ps7);
 #ifdef TDA_PROFILE
             pf[5] += clock64() - t0;
 #endif
@@ -1394,6 +1507,18 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             for (int q = 0; q < 8; ++q) stats[0].prof[3][q] = C.q[q];
             for (int q = 0; q < 8; ++q) stats[0].prof[4][q] = C.q2[q];
             for (int q = 0; q < 8; ++q) stats[0].prof[1][q] = C.q3[q];
+        }
+#endif
+#ifdef TDA_PROF2
+        if ((tid & 63) == 0 && step >= kParP2MinSteps && P.dbg) {  // every wave's phase cycles of a long column
+            const uint64_t q = aadd(&P.ctl->pad[2], 1ull);
+            if (q < kParDbgCap) {
+                uint64_t* o = P.dbg + (uint64_t)kParDbgCap * 4 + q * kParP2Words;
+                o[0] = ((uint64_t)l << 40) | j;
+                o[1] = (uint64_t)(tid >> 6);
+                o[2] = step;
+                for (int u = 0; u < 8; ++u) o[3 + u] = C.tp[u];
+            }
         }
 #endif
 #ifdef TDA_PROFILE

@@ -11,7 +11,10 @@ import importlib, statistics, sys
 sys.path.insert(0, sys.argv[1])
 import bench, torch
 pkg = importlib.import_module("tda-multimodal_amd")
-for wl, md, calls in (("torus1024", 1, 4), ("grid144", 2, 6)):
+import os
+WLS = {"torus1024": 4, "grid144": 6, "torus1024x32": 3, "torus2048": 3}
+for wl in os.environ.get("AB_WL", "torus1024,grid144").split(","):
+    md, calls = bench.WORKLOADS[wl][1], WLS.get(wl, 3)
     X = torch.from_numpy(bench.make_workload(wl)).to("cuda:0")
     ms = []
     for i in range(calls):
