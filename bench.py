@@ -310,11 +310,17 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     dev_index = dev.index if dev.index is not None else 0
     seq = None
     piped = depth > 1 or coalesce > 1
-    if piped and os.environ.get("TDA_BENCH_NO_SEQ") != "1":  # the one-call-at-a-time figure next to the pipelined one
+    # TDA_BENCH_STAGE_ONLY=1 (profiling): only the stage pass below runs, so a rocprof trace of the
+    # command holds exactly the launches the roofline's kernel_avg_ms is taken from (profiles/*_stage.csv)
+    stage_only = os.environ.get("TDA_BENCH_STAGE_ONLY") == "1"
+    if piped and os.environ.get("TDA_BENCH_NO_SEQ") != "1" and not stage_only:  # the one-call-at-a-time figure next to the pipelined one
         # (TDA_BENCH_NO_SEQ=1: profiling runs, so every launch in the trace is the pipeline's batch)
         el_s, dm_s = _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, 1, host_in, dev_index)
         seq = {"value": L * steps / el_s, "ms_per_step": el_s / steps * 1e3, "device_ms_per_step": sum(dm_s) / len(dm_s)}
-    el, dev_ms = _timed_steps(pkg, torch, X, maxdim, kw_pipe if piped else kw, steps, warmup, depth, host_in, dev_index, coalesce)
+    if stage_only:
+        el, dev_ms = float("nan"), [float("nan")]
+    else:
+        el, dev_ms = _timed_steps(pkg, torch, X, maxdim, kw_pipe if piped else kw, steps, warmup, depth, host_in, dev_index, coalesce)
     # per-kernel durations: HIP events around every kernel with all stages on
     # ONE stream (each interval brackets exactly one kernel), same batch,
     # after the timed region; the dominant kernel has the largest mean
@@ -329,6 +335,7 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
     stages = {k: float(np.median(v)) for k, v in acc.items()}  # median: one slow outlier (a profiler hiccup) no longer sets it
     kern = {k: v for k, v in stages.items() if k.startswith("k_")}
     dom = max(kern, key=kern.get)
+    dom_mean = float(np.mean(acc[dom]))  # rocprof's --stats average is a mean over the same launches
     bpl = algo_bytes_per_layer(n, d, maxdim)
     achieved = bpl * Lk / (kern[dom] * 1e-3) / 1e9
     bound, peak, unit, per_layer = "hbm", HBM_PEAK_GBS, "GB/s", {"algo_bytes_per_layer": bpl}
@@ -366,9 +373,11 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
         "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim},
         "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
                      "frac": achieved / peak, "traffic": traffic, **per_layer,
-                     "layers_per_launch": Lk, "kernel_avg_ms": kern[dom],
+                     "layers_per_launch": Lk, "kernel_avg_ms": kern[dom], "kernel_mean_ms": dom_mean,
                      "kernel_timing": "HIP events around each kernel on its stream, all stages serialised on one "
-                                      "stream, after the timed region (same batch)"},
+                                      "stream, after the timed region (same batch); median (kernel_avg_ms) and mean "
+                                      "(kernel_mean_ms) of the stage pass's calls.  The same launches alone under "
+                                      "rocprofv3: profiles/<round>_kernel_stats_<workload>_stage.csv"},
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},
         "roofline_mfma": mfma_roof,
         "pipeline": {"depth": depth, "coalesce": coalesce, "one_stream": kw_pipe.get("one_stream", depth > 1), "sequential": seq,

@@ -58,7 +58,17 @@ constexpr int kParW = kParT / 64;
 #ifndef TDA_PAR_FILL
 #define TDA_PAR_FILL 768
 #endif
-constexpr uint32_t kFrontLog = TDA_PAR_LOG;          // front log entries (live + cancelled)
+#ifndef TDA_PAR_FRONT  // build-time A/B knob (tools/): 1 = key log + hashed index (r02-r04), 2 = one open-addressing toggle table
+#define TDA_PAR_FRONT 2
+#endif
+#if TDA_PAR_FRONT == 2
+#ifndef TDA_PAR_TAB  // build-time A/B knob (tools/): toggle-table slots
+#define TDA_PAR_TAB 4096
+#endif
+#undef TDA_PAR_LOG
+#define TDA_PAR_LOG TDA_PAR_TAB
+#endif
+constexpr uint32_t kFrontLog = TDA_PAR_LOG;          // front log entries (live + cancelled) / toggle-table slots
 #ifndef TDA_PAR_IDX  // build-time A/B knob (tools/): front index slots per log entry
 #define TDA_PAR_IDX 2
 #endif
@@ -163,9 +173,33 @@ __device__ __forceinline__ uint32_t tri_lo(int x, int y, int z, int f) {
 }
 
 // ------------------------------------------------------------------ LDS
+#if TDA_PAR_FRONT == 2
+// FRONT 2: `log` is an open-addressing table of kFrontLog slots holding the
+// live front keys; kTabEmpty / kTabTomb (a removed key) are above every key
+// (keys < kDead), so the front minimum is the plain minimum of all slots.
+// fcnt counts the slots ever filled since the last rebuild (live + tombstones).
+constexpr uint64_t kTabEmpty = kEmpty64;
+constexpr uint64_t kTabTomb = kEmpty64 - 1;
+constexpr uint32_t kTabMax = kFrontLog * 3 / 4;  // filled slots allowed before a rebuild
+constexpr uint32_t kTabPer = kFrontLog / kParT;  // slots per thread in scans
+constexpr uint32_t kStageW = 64 * 4;            // per-wave staging of the keys one toggle pass hands to the table
+// group minima: slots [64 g, 64 g + 64) form group g.  An insert lowers gmin[g]
+// (ds_min, no return); a removal marks g dirty (ds_or, no return); the front
+// minimum rescans only the dirty groups -- one 64-lane read each -- and takes
+// the minimum of the group minima, instead of reading every slot.
+constexpr uint32_t kGroups = kFrontLog / 64;
+constexpr uint32_t kGroupsPerWave = kGroups / kParW;
+static_assert(kGroupsPerWave >= 1 && kGroupsPerWave <= 64 && kGroups % kParW == 0, "group split");
+#endif
 struct ParLds {
     uint64_t log[kFrontLog];
+#if TDA_PAR_FRONT == 2
+    uint64_t stage[kParW][kStageW];
+    uint64_t gmin[kGroups];
+    uint32_t gdirty[(kGroups + 31) / 32];
+#else
     uint64_t idx[kFrontIdx];
+#endif
     uint32_t bcnt[kParLv];
     uint32_t cptr[kParLv][kParChunks];
     uint32_t hist[kParLv];
@@ -281,6 +315,7 @@ struct ParRed {  // double-buffered block reductions: one barrier each
 };
 
 // ------------------------------------------------------------------ front
+#if TDA_PAR_FRONT == 1
 // Index: 8-slot buckets of u64 entries fp << 32 | (log pos + 1), claimed by
 // CAS on the first empty slot (slots of a bucket fill in order and are only
 // cleared by a full reset), so a probe stops at the first empty slot.
@@ -416,6 +451,163 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
     return w;
 }
 
+#else  // TDA_PAR_FRONT == 2: one open-addressing Z/2 toggle table
+// A toggle flips the presence of its key with ONE successful CAS on the key's
+// probe chain: EMPTY -> key (insert) or key -> TOMB (remove); a failed CAS
+// re-reads the same slot.  Slots never return to EMPTY between rebuilds, so a
+// present key is always reached before any EMPTY slot of its chain, and
+// concurrent toggles of one key (raw multisets from refills and records) net
+// out to the right parity in every interleaving.  Against the r04 log + index:
+// no per-wave log allocation (an LDS atomic whose result the wave waited on),
+// no index entry to publish, no fingerprint to verify.
+__device__ __forceinline__ uint32_t tab_hash(uint64_t k) { return (uint32_t)mix64(k) & (kFrontLog - 1); }
+
+__device__ __forceinline__ void front_clear() {  // no barrier
+    for (uint32_t e = threadIdx.x; e < kFrontLog; e += kParT) PS.log[e] = kTabEmpty;
+    for (uint32_t g = threadIdx.x; g < kGroups; g += kParT) PS.gmin[g] = kTabEmpty;
+    for (uint32_t g = threadIdx.x; g < (kGroups + 31) / 32; g += kParT) PS.gdirty[g] = 0;
+    if (threadIdx.x == 0) PS.fcnt = 0;
+}
+__device__ __forceinline__ void front_reset() {
+    front_clear();
+    __syncthreads();
+}
+
+// toggle one key (the lane's own); returns 1 if it filled an EMPTY slot
+__device__ __forceinline__ uint32_t tab_toggle(uint64_t key) {
+    uint32_t h = tab_hash(key);
+    for (uint32_t it = 0; it < 4 * kFrontLog; ++it) {
+        const uint64_t v = PS.log[h];
+        if (v == key) {
+            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)key, (unsigned long long)kTabTomb) == key) {
+                atomicOr(&PS.gdirty[h >> 11], 1u << ((h >> 6) & 31));  // its group's minimum may be gone
+                return 0;
+            }
+            continue;  // another toggle of this key won: read the slot again
+        }
+        if (v == kTabEmpty) {
+            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)key) == kTabEmpty) {
+                atomicMin((unsigned long long*)&PS.gmin[h >> 6], (unsigned long long)key);
+                return 1;
+            }
+            continue;
+        }
+        h = (h + 1) & (kFrontLog - 1);
+    }
+    PS.err = 13;  // table full (front_room keeps it below kTabMax)
+    return 0;
+}
+
+// Toggle up to R keys per thread (bit r of vmask) with NO workgroup barrier:
+// the wave's keys are packed into its lanes through a wave-private LDS stage
+// (no atomics), then each lane toggles ceil(n / 64) of them.  Callers put a
+// barrier between this and the next read of the front; the caller made room
+// (fcnt + R * kParT <= kTabMax).
+template <int R>
+__device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vmask) {
+    static_assert(R * 64 <= (int)kStageW, "stage");
+    const int ln = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t m[R];
+    uint32_t wtot = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        m[r] = __ballot((vmask >> r) & 1u);
+        wtot += (uint32_t)__popcll(m[r]);
+    }
+    if (!wtot) return;
+    uint32_t ins = 0;
+    if (wtot <= 64 && R == 1) {  // one key per lane already
+        if (vmask & 1u) ins = tab_toggle(k[0]);
+    } else {
+        uint32_t off = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if ((vmask >> r) & 1u) PS.stage[w][off + lanes_below(m[r])] = k[r];
+            off += (uint32_t)__popcll(m[r]);
+        }
+        // a wave's LDS operations complete in order: the stage is visible to every lane
+        for (uint32_t pos = (uint32_t)ln; pos < wtot; pos += 64) ins += tab_toggle(PS.stage[w][pos]);
+    }
+    const uint64_t mi = __ballot(ins != 0);
+    uint32_t n = ins;
+    if (__popcll(mi) > 0) {
+        n = (uint32_t)wave_sum_u64(ins);
+        if (ln == 0) atomicAdd(&PS.fcnt, n);  // no return: nobody waits on it
+    }
+}
+
+// min live front key (block-uniform; kEmpty64 if none): wave w owns groups
+// [w G, w G + G); it recomputes its dirty groups (one slot per lane, a wave
+// minimum each), then the minimum of its group minima; one block reduction.
+// Nothing toggles between the caller's barrier and the reduction's.
+__device__ __forceinline__ uint64_t front_min(ParRed& rd) {
+    const int ln = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t g0 = (uint32_t)w * kGroupsPerWave;
+    uint64_t dm;  // my groups' dirty bits (wave-uniform)
+    if constexpr (kGroupsPerWave == 64) {
+        dm = ((uint64_t)PS.gdirty[(g0 >> 5) + 1] << 32) | PS.gdirty[g0 >> 5];
+    } else {
+        dm = (PS.gdirty[g0 >> 5] >> (g0 & 31)) & ((1ull << kGroupsPerWave) - 1);
+    }
+    while (dm) {
+        const uint32_t g = g0 + (uint32_t)__builtin_ctzll(dm);
+        dm &= dm - 1;
+        const uint64_t x = PS.log[g * 64 + ln];
+        const uint64_t m = wave_min_u64(x < kDead ? x : kTabEmpty);
+        if (ln == 0) PS.gmin[g] = m;
+    }
+    if (ln == 0) {  // my groups are clean again (other waves clear their own bits of a shared word)
+        if constexpr (kGroupsPerWave == 64) {
+            PS.gdirty[g0 >> 5] = 0;
+            PS.gdirty[(g0 >> 5) + 1] = 0;
+        } else {
+            atomicAnd(&PS.gdirty[g0 >> 5], ~(uint32_t)(((1ull << kGroupsPerWave) - 1) << (g0 & 31)));
+        }
+    }
+    uint64_t b = ln < (int)kGroupsPerWave ? PS.gmin[g0 + ln] : kTabEmpty;  // after this wave's own writes (in order)
+    b = b < kDead ? b : kEmpty64;
+    return rd.min(b);
+}
+
+// Rebuild the table with the live keys of level <= keep (relative to
+// PS.last): read every slot, clear, re-insert.  Returns the live count kept
+// (block-uniform).
+__device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
+    __syncthreads();
+    const uint64_t last = PS.last;
+    uint64_t mine[kTabPer];
+    uint32_t nl = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kTabPer; ++q) {
+        const uint64_t x = PS.log[q * kParT + threadIdx.x];
+        const bool lv = x < kDead && par_bucket(x, last) <= keep;
+        mine[q] = lv ? x : kTabEmpty;
+        nl += lv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kTabPer; ++q) PS.log[q * kParT + threadIdx.x] = kTabEmpty;
+    for (uint32_t g = threadIdx.x; g < kGroups; g += kParT) PS.gmin[g] = kTabEmpty;
+    for (uint32_t g = threadIdx.x; g < (kGroups + 31) / 32; g += kParT) PS.gdirty[g] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kTabPer; ++q) {
+        if (mine[q] == kTabEmpty) continue;
+        uint32_t h = tab_hash(mine[q]);  // distinct keys: the first EMPTY slot of the chain
+        for (uint32_t it = 0; it < kFrontLog; ++it, h = (h + 1) & (kFrontLog - 1))
+            if (PS.log[h] == kTabEmpty &&
+                atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)mine[q]) == kTabEmpty) {
+                atomicMin((unsigned long long*)&PS.gmin[h >> 6], (unsigned long long)mine[q]);
+                break;
+            }
+    }
+    const uint32_t w = (uint32_t)rd.sum(nl);  // barrier: the inserts are done
+    if (threadIdx.x == 0) PS.fcnt = w;
+    __syncthreads();
+    return w;
+}
+#endif  // TDA_PAR_FRONT
+
 // ------------------------------------------------------------------ HBM buckets
 // Append key k[r] to bucket bb[r] (bit r of vmask); chunks that start in this
 // pass and were never allocated by this workgroup are taken from the pool.
@@ -425,60 +617,15 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
 // allocates chunk c + 2, so a pass of up to 3072 keys per bucket never needs a
 // chunk that is not there yet (chunks c and c + 1 hold >= 3072 keys from c = 2
 // on).  Callers put a barrier between passes that may open new chunks.
-#ifndef TDA_PAR_WAGG  // build-time A/B knob (tools/): bit 0 = refill histogram, bit 1 = bucket slots, wave-aggregated
-#define TDA_PAR_WAGG 0
-#endif
-
-// Wave-aggregated LDS counters: the keys of one wave that hit the same counter
-// (a radix level) take their slots with ONE atomic by a leader lane instead
-// of one per key (a step's ~600 back keys and a refill's ~3 K keys fall into a
-// handful of levels: same-address LDS atomics serialise lane by lane).
-// Returns each valid lane's old value + its rank among the wave's lanes on the
-// same counter.  Wave-uniform control flow: every lane of the wave calls it.
-__device__ __forceinline__ uint32_t wave_slot(uint32_t* ctr, uint32_t b, bool valid) {
-    const int ln = threadIdx.x & 63;
-    uint64_t todo = __ballot(valid);
-    int lead = 0;
-    uint32_t rank = 0, cnt = 0;
-    while (todo) {  // one iteration per distinct counter among the valid lanes
-        const int l0 = __builtin_ctzll(todo);
-        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)b, l0);
-        const uint64_t m = __ballot(valid && b == b0);
-        if ((m >> ln) & 1ull) {
-            lead = l0;
-            rank = lanes_below(m);
-        }
-        if (ln == l0) cnt = (uint32_t)__popcll(m);
-        todo &= ~m;
-    }
-    uint32_t base = 0;
-    if (valid && lead == ln) base = atomicAdd(&ctr[b], cnt);  // one ds_add_rtn for all groups' leaders
-    base = (uint32_t)__shfl((int)base, lead, 64);
-    return base + rank;
-}
-// the same without slots: hist[b] += (valid lanes on b)
-__device__ __forceinline__ void wave_count(uint32_t* hist, uint32_t b, bool valid) {
-    const int ln = threadIdx.x & 63;
-    uint64_t todo = __ballot(valid);
-    while (todo) {
-        const int l0 = __builtin_ctzll(todo);
-        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)b, l0);
-        const uint64_t m = __ballot(valid && b == b0);
-        if (ln == l0) atomicAdd(&hist[b0], (uint32_t)__popcll(m));
-        todo &= ~m;
-    }
-}
-
+// (r05: slot allocation and the refill histogram aggregated per (wave, level) by
+// ballots -- one LDS atomic per distinct level instead of per key -- measured
+// slower: torus1024 45.2 -> 50.1 ms, torus1024x32 108 -> 114 ms; the native
+// same-address LDS atomics stay)
 template <int R>
 __device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint32_t (&bb)[R], uint32_t vmask, const ParBufs& P) {
     uint32_t slot[R];
-#if TDA_PAR_WAGG & 2
-#pragma unroll
-    for (int r = 0; r < R; ++r) slot[r] = wave_slot(PS.bcnt, bb[r], (vmask >> r) & 1u);
-#else
 #pragma unroll
     for (int r = 0; r < R; ++r) slot[r] = ((vmask >> r) & 1u) ? atomicAdd(&PS.bcnt[bb[r]], 1u) : 0u;
-#endif
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (!((vmask >> r) & 1u)) continue;
@@ -508,7 +655,7 @@ struct ParCol {
     ParRed rd;
     uint64_t steps = 0, adds = 0;
 #ifdef TDA_PROF2
-    // per-wave phase cycles of the current column (SHADER_CYCLES deltas: no memory op, no wait):
+    // per-wave phase cycles of the current column (s_memtime deltas):
     // room + step barrier, front min, pivot + row loads, keys, bucket appends, front toggles, refills, owner path / records
     uint32_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -520,13 +667,17 @@ struct ParCol {
 #endif
 };
 #ifdef TDA_PROF2
+// gfx950 has no HW_REG_SHADER_CYCLES: s_memtime (an SMEM read of the shader
+// clock; its use waits lgkmcnt, so a phase is charged with the LDS work it
+// issued)
 __device__ __forceinline__ uint32_t p2_now() {
-    uint32_t c;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_SHADER_CYCLES, 0, 20)" : "=s"(c) : : "memory");
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_s_memtime();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     return c;
 }
 #define P2_T(v) const uint32_t v = p2_now()
-#define P2_ACC(i, v) C.tp[i] += (p2_now() - (v)) & 0xFFFFFu
+#define P2_ACC(i, v) C.tp[i] += p2_now() - (v)
 #define P2_DEP(x) asm volatile("" : : "v"(x))
 #else
 #define P2_T(v)
@@ -543,15 +694,20 @@ __device__ __forceinline__ uint32_t p2_now() {
 
 // Barrier, then room in the front for `need` more log entries: compact, and
 // spill the highest front levels to HBM if too many keys are live.
+#if TDA_PAR_FRONT == 2
+constexpr uint32_t kFrontRoom = kTabMax;
+#else
+constexpr uint32_t kFrontRoom = kFrontLog;
+#endif
 __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t need) {
     lds_sync();
-    if (PS.fcnt + need <= kFrontLog) return;
+    if (PS.fcnt + need <= kFrontRoom) return;
     PAR_T0(tc0);
     uint32_t w = front_compact(C.rd, kParLv);
 #ifdef TDA_PROFILE
     ++C.ncompact;
 #endif
-    if (w > kFrontLive || w + need > kFrontLog) {
+    if (w > kFrontLive || w + need > kFrontRoom) {
 #ifdef TDA_PROFILE
         ++C.nspill;
 #endif
@@ -559,21 +715,31 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
         for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
         __syncthreads();
         const uint64_t last = PS.last;
+#if TDA_PAR_FRONT == 2
+        for (uint32_t e = threadIdx.x; e < kFrontLog; e += kParT)
+            if (PS.log[e] < kDead) atomicAdd(&PS.hist[par_bucket(PS.log[e], last)], 1u);
+#else
         for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket(PS.log[e], last)], 1u);
+#endif
         __syncthreads();
         int keep = par_keep_level(PS.hist, (int)min(PS.kf + 1u, 64u), kFrontFill);
         if (keep < 0) {  // the exact-diameter level alone is too large for the front
-            if (PS.hist[0] + need <= kFrontLog) keep = 0;
+            if (PS.hist[0] + need <= kFrontRoom) keep = 0;
             else if (threadIdx.x == 0) PS.err = 31;
         }
         __syncthreads();
         if (PS.err) return;
         // move the levels above `keep` out to their HBM buckets, then drop them from the front
-        for (uint32_t e0 = 0; e0 < w; e0 += kParT) {
+#if TDA_PAR_FRONT == 2
+        const uint32_t ns = kFrontLog;  // every slot (tombstones and EMPTY are skipped)
+#else
+        const uint32_t ns = w;
+#endif
+        for (uint32_t e0 = 0; e0 < ns; e0 += kParT) {
             const uint32_t e = e0 + threadIdx.x;
-            uint64_t x[1] = {e < w ? PS.log[e] : 0};
-            uint32_t b[1] = {e < w ? par_bucket(x[0], last) : 0};
-            bucket_append<1>(x, b, (e < w && b[0] > (uint32_t)keep) ? 1u : 0u, P);
+            uint64_t x[1] = {e < ns ? PS.log[e] : kEmpty64};
+            uint32_t b[1] = {x[0] < kDead ? par_bucket(x[0], last) : 0};
+            bucket_append<1>(x, b, (x[0] < kDead && b[0] > (uint32_t)keep) ? 1u : 0u, P);
             __syncthreads();  // chunk pointers opened by this pass
         }
         if (threadIdx.x == 0) PS.kf = (uint32_t)keep;
@@ -690,9 +856,13 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
 #ifdef TDA_PROFILE
     C.q[6] += c;
 #endif
+#if TDA_PAR_FRONT == 2
+    front_clear();
+#else
     for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
-    for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
     if (threadIdx.x == 0) PS.fcnt = 0;
+#endif
+    for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
     uint64_t x[kParRefill][kParRegs];
     uint32_t vm[kParRefill] = {};
     // pass 1: minimum (raw; a cancelled duplicate is still a lower bound of every live key)
@@ -719,11 +889,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     // levels that hold at most kFrontFill keys.  (A binary search on the level
     // with block counts instead of the atomics measured slower: 7.1 vs 4.3 M
     // cycles over torus1024's refills.)
-#if TDA_PAR_WAGG & 1
-#define PAR_HIST_ADD(key, valid) wave_count(PS.hist, par_bucket((key), nl), (valid))
-#else
 #define PAR_HIST_ADD(key, valid) do { if (valid) atomicAdd(&PS.hist[par_bucket((key), nl)], 1u); } while (0)
-#endif
     if (inreg) {
 #pragma unroll
         for (int h = 0; h < kParRefill; ++h)
@@ -765,7 +931,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     auto distribute = [&](const uint64_t (&y)[kParRegs], uint32_t ym) {
         // the front takes at most kFrontLive keys in all: compaction keeps room
         __syncthreads();  // chunk pointers opened by the previous pass
-        if (PS.fcnt + kParRegs * kParT > kFrontLog) front_compact(C.rd, kParLv);
+        if (PS.fcnt + kParRegs * kParT > kFrontRoom) front_compact(C.rd, kParLv);
         PAR_Q3(6);
         uint32_t fm = 0, bm = 0, bb[kParRegs];
 #pragma unroll
@@ -964,7 +1130,11 @@ __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_
 #ifdef TDA_PROFILE
     const uint64_t tsv = clock64();
 #endif
+#if TDA_PAR_FRONT == 2
+    const uint32_t c = kFrontLog;  // every slot (only live keys are < kDead)
+#else
     const uint32_t c = PS.fcnt;
+#endif
     uint32_t lv = 0;
     for (uint32_t e = threadIdx.x; e < c; e += kParT) lv += PS.log[e] < kDead;
     const uint64_t nfront = C.rd.sum(lv);
