@@ -22,6 +22,7 @@ on bounded samples.  Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import glob
 import importlib
 import json
 import math
@@ -357,6 +358,20 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
         pmc_scale = Lk / pj["layers_per_launch"] if pj.get("layers_per_launch") else 1.0
         traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
         traffic = traffic * pmc_scale if traffic is not None else None
+    # what actually bounds the latency-bound small-N kernels: resident waves per CU and the LDS-array
+    # busy fraction of the same launch shape (tools/pmc_lds.py, the newest profiles/*_pmc_lds_<wl>.json)
+    lds_occ = None
+    lds_files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_lds_{name}.json")))
+    if lds_files:
+        with open(lds_files[-1]) as f:
+            lj = json.load(f)
+        kk = lj.get("kernels", {}).get(dom)
+        if kk:
+            lds_occ = {k: kk[k] for k in ("resident_waves_per_cu", "lds_busy_frac", "lds_bank_conflict_share",
+                                          "lds_insts_per_wave")}
+            lds_occ.update(source=os.path.relpath(lds_files[-1], ROOT), layers_per_launch=lj.get("layers_per_launch"),
+                           note="the kernel's bound: one- or two-wave workgroups with ~46 KB of LDS each (occupancy) "
+                                "and dependent LDS chains; the HBM fraction above is small by construction")
     gram = next((k for k in ("k_gram_layer", "k_distance_mfma") if k in kern), None)
     mfma_roof = None
     if gram and gram != dom:  # the FP64 Gram kernel when another kernel dominates (e.g. raw4096: H0)
@@ -372,7 +387,7 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
         "device_ms_per_step": sum(dev_ms) / len(dev_ms), "X_host": X_host, "maxdim": maxdim,
         "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim},
         "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
-                     "frac": achieved / peak, "traffic": traffic, **per_layer,
+                     "frac": achieved / peak, "traffic": traffic, **per_layer, "lds_occupancy": lds_occ,
                      "layers_per_launch": Lk, "kernel_avg_ms": kern[dom], "kernel_mean_ms": dom_mean,
                      "kernel_timing": "HIP events around each kernel on its stream, all stages serialised on one "
                                       "stream, after the timed region (same batch); median (kernel_avg_ms) and mean "

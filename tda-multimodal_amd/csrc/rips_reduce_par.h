@@ -183,20 +183,11 @@ constexpr uint64_t kTabTomb = kEmpty64 - 1;
 constexpr uint32_t kTabMax = kFrontLog * 3 / 4;  // filled slots allowed before a rebuild
 constexpr uint32_t kTabPer = kFrontLog / kParT;  // slots per thread in scans
 constexpr uint32_t kStageW = 64 * 4;            // per-wave staging of the keys one toggle pass hands to the table
-// group minima: slots [64 g, 64 g + 64) form group g.  An insert lowers gmin[g]
-// (ds_min, no return); a removal marks g dirty (ds_or, no return); the front
-// minimum rescans only the dirty groups -- one 64-lane read each -- and takes
-// the minimum of the group minima, instead of reading every slot.
-constexpr uint32_t kGroups = kFrontLog / 64;
-constexpr uint32_t kGroupsPerWave = kGroups / kParW;
-static_assert(kGroupsPerWave >= 1 && kGroupsPerWave <= 64 && kGroups % kParW == 0, "group split");
 #endif
 struct ParLds {
     uint64_t log[kFrontLog];
 #if TDA_PAR_FRONT == 2
     uint64_t stage[kParW][kStageW];
-    uint64_t gmin[kGroups];
-    uint32_t gdirty[(kGroups + 31) / 32];
 #else
     uint64_t idx[kFrontIdx];
 #endif
@@ -464,8 +455,6 @@ __device__ __forceinline__ uint32_t tab_hash(uint64_t k) { return (uint32_t)mix6
 
 __device__ __forceinline__ void front_clear() {  // no barrier
     for (uint32_t e = threadIdx.x; e < kFrontLog; e += kParT) PS.log[e] = kTabEmpty;
-    for (uint32_t g = threadIdx.x; g < kGroups; g += kParT) PS.gmin[g] = kTabEmpty;
-    for (uint32_t g = threadIdx.x; g < (kGroups + 31) / 32; g += kParT) PS.gdirty[g] = 0;
     if (threadIdx.x == 0) PS.fcnt = 0;
 }
 __device__ __forceinline__ void front_reset() {
@@ -479,17 +468,11 @@ __device__ __forceinline__ uint32_t tab_toggle(uint64_t key) {
     for (uint32_t it = 0; it < 4 * kFrontLog; ++it) {
         const uint64_t v = PS.log[h];
         if (v == key) {
-            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)key, (unsigned long long)kTabTomb) == key) {
-                atomicOr(&PS.gdirty[h >> 11], 1u << ((h >> 6) & 31));  // its group's minimum may be gone
-                return 0;
-            }
+            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)key, (unsigned long long)kTabTomb) == key) return 0;
             continue;  // another toggle of this key won: read the slot again
         }
         if (v == kTabEmpty) {
-            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)key) == kTabEmpty) {
-                atomicMin((unsigned long long*)&PS.gmin[h >> 6], (unsigned long long)key);
-                return 1;
-            }
+            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)key) == kTabEmpty) return 1;
             continue;
         }
         h = (h + 1) & (kFrontLog - 1);
@@ -536,35 +519,18 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
     }
 }
 
-// min live front key (block-uniform; kEmpty64 if none): wave w owns groups
-// [w G, w G + G); it recomputes its dirty groups (one slot per lane, a wave
-// minimum each), then the minimum of its group minima; one block reduction.
-// Nothing toggles between the caller's barrier and the reduction's.
+// min live front key (block-uniform; kEmpty64 if none): every slot, 16-B
+// reads.  (r05: group minima kept by the toggles -- ds_min on insert, a dirty
+// bit on removal, only dirty groups rescanned -- measured slower: the front
+// minimum 1.9 K -> 4.2 K cycles a step, torus1024 41.9 -> 49.2 ms.)
 __device__ __forceinline__ uint64_t front_min(ParRed& rd) {
-    const int ln = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t g0 = (uint32_t)w * kGroupsPerWave;
-    uint64_t dm;  // my groups' dirty bits (wave-uniform)
-    if constexpr (kGroupsPerWave == 64) {
-        dm = ((uint64_t)PS.gdirty[(g0 >> 5) + 1] << 32) | PS.gdirty[g0 >> 5];
-    } else {
-        dm = (PS.gdirty[g0 >> 5] >> (g0 & 31)) & ((1ull << kGroupsPerWave) - 1);
+    uint64_t b = kEmpty64;
+#pragma unroll
+    for (uint32_t q = 0; q < kTabPer; q += 2) {  // slots 2 t, 2 t + 1 of each 2 kParT block
+        const u64x2 v = *(const TDA_LDS u64x2*)&PS.log[q * kParT + 2 * threadIdx.x];
+        b = v.x < b ? v.x : b;
+        b = v.y < b ? v.y : b;
     }
-    while (dm) {
-        const uint32_t g = g0 + (uint32_t)__builtin_ctzll(dm);
-        dm &= dm - 1;
-        const uint64_t x = PS.log[g * 64 + ln];
-        const uint64_t m = wave_min_u64(x < kDead ? x : kTabEmpty);
-        if (ln == 0) PS.gmin[g] = m;
-    }
-    if (ln == 0) {  // my groups are clean again (other waves clear their own bits of a shared word)
-        if constexpr (kGroupsPerWave == 64) {
-            PS.gdirty[g0 >> 5] = 0;
-            PS.gdirty[(g0 >> 5) + 1] = 0;
-        } else {
-            atomicAnd(&PS.gdirty[g0 >> 5], ~(uint32_t)(((1ull << kGroupsPerWave) - 1) << (g0 & 31)));
-        }
-    }
-    uint64_t b = ln < (int)kGroupsPerWave ? PS.gmin[g0 + ln] : kTabEmpty;  // after this wave's own writes (in order)
     b = b < kDead ? b : kEmpty64;
     return rd.min(b);
 }
@@ -587,8 +553,6 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < kTabPer; ++q) PS.log[q * kParT + threadIdx.x] = kTabEmpty;
-    for (uint32_t g = threadIdx.x; g < kGroups; g += kParT) PS.gmin[g] = kTabEmpty;
-    for (uint32_t g = threadIdx.x; g < (kGroups + 31) / 32; g += kParT) PS.gdirty[g] = 0;
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < kTabPer; ++q) {
@@ -596,10 +560,8 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
         uint32_t h = tab_hash(mine[q]);  // distinct keys: the first EMPTY slot of the chain
         for (uint32_t it = 0; it < kFrontLog; ++it, h = (h + 1) & (kFrontLog - 1))
             if (PS.log[h] == kTabEmpty &&
-                atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)mine[q]) == kTabEmpty) {
-                atomicMin((unsigned long long*)&PS.gmin[h >> 6], (unsigned long long)mine[q]);
+                atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)mine[q]) == kTabEmpty)
                 break;
-            }
     }
     const uint32_t w = (uint32_t)rd.sum(nl);  // barrier: the inserts are done
     if (threadIdx.x == 0) PS.fcnt = w;
@@ -609,6 +571,12 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
 #endif  // TDA_PAR_FRONT
 
 // ------------------------------------------------------------------ HBM buckets
+#ifndef TDA_PAR_STORE_SC1  // build-time A/B knob (tools/): bucket appends as sc1 (L2-dropping) stores
+#define TDA_PAR_STORE_SC1 0
+#endif
+// (r05: the slot's chunk pointer read from a per-bucket "current chunk" cache
+// beside the slot atomic -- one LDS round trip instead of two -- measured no
+// faster: torus1024 49.2 vs 49.4 ms; dropped)
 // Append key k[r] to bucket bb[r] (bit r of vmask); chunks that start in this
 // pass and were never allocated by this workgroup are taken from the pool.
 // Append key k[r] to HBM bucket bb[r] (bit r of vmask), with NO workgroup
@@ -641,7 +609,14 @@ __device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint
             PS.err = 21;
             continue;
         }
+#if TDA_PAR_STORE_SC1
+        // write-through store: the bucket line leaves this XCD's L2 (MI355X_MICROARCH.md: sc1 stores
+        // DROP the line, plain ones keep it), so ~600 keys a step do not evict the distance rows the
+        // next steps load
+        ast(P.bpool + (uint64_t)cp * 256 + (slot[r] - chunk_start(kc)), k[r]);
+#else
         st_glb(P.bpool, (uint64_t)cp * 256 + (slot[r] - chunk_start(kc)), k[r]);
+#endif
     }
 }
 
@@ -1442,7 +1417,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             prealloc = true;
         }
         for (uint32_t q = tid; q < kParLv; q += kParT) PS.bcnt[q] = 0;
-        uint32_t sc = 0;  // WIDE: the column's edge code
+            uint32_t sc = 0;  // WIDE: the column's edge code
         if constexpr (WIDE) {
             const uint32_t* Dc = (const uint32_t*)Dr;
             sc = max(ld_glb(Dc, (size_t)sv[0] * n + sv[1]), max(ld_glb(Dc, (size_t)sv[0] * n + sv[2]), ld_glb(Dc, (size_t)sv[1] * n + sv[2])));
@@ -1705,7 +1680,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)adds);
         if (done && my_rec >= 0 && my_seg) {  // the claimed record references this workgroup's chunks: fresh ones next
             for (uint32_t e = tid; e < (uint32_t)kParLv * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
-            prealloc = false;
+                    prealloc = false;
             __syncthreads();
         }
         if (PS.err) {

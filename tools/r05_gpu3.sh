@@ -12,7 +12,7 @@ TDA_RIPS_LIB=$PWD/$V/lib_g4.so timeout -k 10 400 python -u -m pytest tests/test_
     -k "grid144 or torus or full_workload or parallel_h2 or h2_above or n2048 or wide_keys or random_clouds or adversarial_sizes or invariants" \
     > gpurun_out/parity_g4.txt 2>&1 || { echo "parity g4 rc $?"; tail -30 gpurun_out/parity_g4.txt; exit 1; }
 tail -1 gpurun_out/parity_g4.txt
-AB_WL=torus1024,torus1024x32,grid144 timeout -k 10 600 python -u tools/ab_libs.py $V/lib_f1.so $V/lib_g4.so $V/lib_g8.so $V/lib_g8f.so $V/lib_g16f.so \
+AB_WL=torus1024,torus1024x32,grid144 timeout -k 10 800 python -u tools/ab_libs.py $V/lib_f1.so $V/lib_g4.so $V/lib_g8.so $V/lib_g8f.so $V/lib_g16f.so $V/lib_s1.so $V/lib_cc.so $V/lib_s1cc.so \
     > gpurun_out/ab_front.txt 2>&1 || { echo "ab rc $?"; tail -20 gpurun_out/ab_front.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/ab_front.txt
 for p in pg4 pg8f; do
