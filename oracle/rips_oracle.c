@@ -424,6 +424,12 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
     const int stats = getenv("ORACLE_STATS") != NULL;
     /* ORACLE_COLSTATS=1: print the columns with more than 500 additions (dev aid) */
     const int colstats = getenv("ORACLE_COLSTATS") != NULL;
+    /* ORACLE_TRACE=<file> ORACLE_TRACE_COL=<j> (dim 1): every key the column's reduction pushes and
+       every pivot it pops, as u64 filtration keys diam_bits << 32 | ~idx (a pivot follows a ~0 marker);
+       dev aid for modelling the GPU reducer's working-column structure (tools/front_sim.py) */
+    FILE *trace = NULL;
+    int64_t trace_col = getenv("ORACLE_TRACE_COL") ? atoll(getenv("ORACLE_TRACE_COL")) : -1;
+    if (getenv("ORACLE_TRACE") && trace_col >= 0) trace = fopen(getenv("ORACLE_TRACE"), "wb");
     /* threshold (ripser.py rips_dm): enclosing radius when thresh is inf/max */
     if (isinf(thresh) || thresh == 3.402823466e+38f) {
         float enc = INFINITY;
@@ -570,9 +576,16 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
             work.n = 0;
             vwork.n = 0;
             int64_t adds0 = res->n_adds[dim];
+            const int tr = trace && dim == 1 && j == trace_col;
             for (int64_t q = 0; q < m; ++q) {
                 splx_t e = {cbuf[q].diam, cbuf[q].idx};
                 heap_push(&work, e);
+                if (tr) {
+                    uint32_t db;
+                    memcpy(&db, &cbuf[q].diam, 4);
+                    const uint64_t key = ((uint64_t)db << 32) | (0xFFFFFFFFull - (cbuf[q].idx & 0xFFFFFFFFull));
+                    fwrite(&key, 8, 1, trace);
+                }
             }
             for (;;) {
                 splx_t p = heap_get_pivot(&work);
@@ -590,6 +603,13 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
                     break;
                 }
                 int64_t o = hm_get(&piv, p.idx);
+                if (tr && p.idx != HM_EMPTY) {
+                    uint32_t db;
+                    memcpy(&db, &p.diam, 4);
+                    const uint64_t mk = ~0ull, key = ((uint64_t)db << 32) | (0xFFFFFFFFull - (p.idx & 0xFFFFFFFFull));
+                    fwrite(&mk, 8, 1, trace);
+                    fwrite(&key, 8, 1, trace);
+                }
                 if (o >= 0) {
                     res->n_adds[dim]++;
                     /* add column o: its simplex plus its V entries */
@@ -602,6 +622,12 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
                         for (int64_t q = 0; q < mm; ++q) {
                             splx_t e = {cbuf[q].diam, cbuf[q].idx};
                             heap_push(&work, e);
+                            if (tr) {
+                                uint32_t db;
+                                memcpy(&db, &cbuf[q].diam, 4);
+                                const uint64_t key = ((uint64_t)db << 32) | (0xFFFFFFFFull - (cbuf[q].idx & 0xFFFFFFFFull));
+                                fwrite(&key, 8, 1, trace);
+                            }
                         }
                         splx_t ve = {0.0f, s};
                         heap_push(&vwork, ve);
@@ -645,6 +671,10 @@ int oracle_rips_dm(const float *dist, int64_t n, int maxdim, float thresh, oracl
         }
         free(voff);
         free(vdat);
+        if (trace && dim == 1) {
+            fclose(trace);
+            trace = NULL;
+        }
 
         if (dim < maxdim) {
             /* assemble (dim+1)-simplices: add a vertex above the max vertex of

@@ -79,6 +79,15 @@ constexpr unsigned kParGrid = 512;           // k_reduce_par workgroups at most 
 // faster without a second workgroup on its CU (r02, tools/ab_pargrid.sh:
 // grid144 10.5 -> 8.5 ms, torus1024 61 -> 58.5 ms at 256 vs 512)
 constexpr unsigned kParGridDefault = 256;
+// column cap of k_reduce_par: keys above birth + f * thresh are never stored.  f = 0.5 keeps
+// 35 % of the keys of torus1024's longest column (whose pivot is at birth + 0.35 thresh; the
+// largest H1 persistence of the torus seeds, grid144 and the sweep clouds is <= 0.38 thresh); a
+// cap that is too small costs one uncapped re-run of the call, remembered for the shape.
+// TDA_PAR_CAPF (tests) overrides it (0 = off).
+float par_capf() {
+    const char* e = test_env("TDA_PAR_CAPF");
+    return e ? (float)atof(e) : 0.5f;
+}
 unsigned par_grid_size() {
     const char* g = test_env("TDA_PAR_GRID");
     const unsigned v = g ? (unsigned)atoi(g) : kParGridDefault;
@@ -452,6 +461,7 @@ struct Workspace {
         bool force_global, force_big;
         int no_par;
         int scale;
+        bool no_cap;
     };
     std::vector<Retry> retry;
     std::mutex mu;
@@ -461,8 +471,8 @@ struct Workspace {
 // a single hipGraphLaunch when the same plan, input address and flags recur
 struct GraphKey {
     int64_t L, N, D;
-    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets, sil_K, no_par, twonn;
-    float thresh, tn_eps;
+    int maxdim, dtype, input_kind, x_on_device, flags, force_global, scale, force_big, variant, n_label_sets, sil_K, no_par, twonn, no_cap;
+    float thresh, tn_eps, capf;
     double tn_discard;
     const void* x;
     uint64_t gen;
@@ -753,8 +763,9 @@ std::string err_flags(int e) {
 
 // ------------------------------------------------------------------ pipeline
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
+// no_cap: k_reduce_par without column caps (a capped column ran empty below its cap: code 81)
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
-                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0) {
+                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0, bool no_cap = false) {
     const auto h_entry = std::chrono::steady_clock::now();
     Plan p;
     p.L = a.L;
@@ -914,6 +925,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.scale = scale;
     gk.force_big = force_big;
     gk.no_par = no_par;
+    gk.no_cap = no_cap;
+    // column caps only with ripser's default threshold (the enclosing radius: no essential
+    // H1 / H2 class); a finite user threshold can leave classes essential (k_reduce_par)
+    const float capf = (no_cap || !(std::isinf(a.thresh) || a.thresh == 3.402823466e+38f)) ? 0.0f : par_capf();
+    gk.capf = capf;
     gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0) |
                  (p.wide ? 1 << 10 : 0) | (p.want64 ? 1 << 11 : 0);
     gk.thresh = a.thresh;
@@ -1431,6 +1447,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 pb.rq = (uint64_t*)(B + p.o_prq);
                 pb.rq_cap = p.rq_cap;
                 pb.step_limit = step_limit();
+                pb.capf = capf;
                 pb.dbg = p.o_pdbg ? (uint64_t*)(B + p.o_pdbg) : nullptr;  // profile builds only
                 HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                 hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);
@@ -1575,32 +1592,36 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             fprintf(stderr, "[tda] k_reduce_par aborted: code %llu, evictions %llu, records %llu, pools %llu / %llu keys\n", c.err,
                     c.evictions, c.rec_used, c.rpool_used, c.bpool_used);
         const unsigned code = (unsigned)(c.err & 0xFFFF);
+        if (code == 81 && !no_cap) {  // a capped column ran empty below its cap: the same call without caps
+            guard.unlock();
+            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, no_par, true);
+        }
         const bool capacity = code == 21 || code == 22 || code == 41 || code == 53;  // pools / requeue slots
         if (capacity && scale < 2) {  // the same parallel reduction with larger pools
             guard.unlock();
-            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par);
+            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par, no_cap);
         }
         if (test_env_is("TDA_PAR_STRICT", "1"))  // tests: the parallel path itself must succeed
             return fail(TDA_E_CAPACITY, "k_reduce_par aborted: item " + std::to_string(c.err >> 16) + " code " +
                                             std::to_string(code));
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, np_next);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, np_next, no_cap);
     }
     if ((errs & ERR_LDS_SPILL) && !force_global) {
         // a working column outgrew LDS: redo the batch with global-memory tables
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, scale, false, no_par, no_cap);
     }
     if ((errs & ERR_WORK_CAP) && !p.big && !test_env_is("TDA_REDUCE", "wave")) {
         // a working column outgrew the one-wave HBM tables: full scans of a
         // large column are the slow case, so switch to the radix-heap kernel
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true, no_par);
+        return run_pipeline(a, input_kind, host_or_dev, out, true, 0, true, no_par, no_cap);
     }
     if ((errs & ~(ERR_LDS_SPILL)) == (errs & (ERR_WORK_CAP | ERR_VPOOL_CAP)) && errs && scale < 2) {
         // working column / reduced-column pool too small: retry with larger buffers
         guard.unlock();
-        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par);
+        return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, p.big, no_par, no_cap);
     }
     if (errs) return fail(TDA_E_CAPACITY, "device work buffer overflow:" + err_flags(errs));
 #ifdef TDA_PROF2
@@ -1729,7 +1750,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 #endif
 
-    if (force_global || scale || force_big || no_par) {  // remember what this shape needed
+    if (force_global || scale || force_big || no_par || no_cap) {  // remember what this shape needed
         bool seen = false;
         for (auto& m : w.retry)
             if (m.N == p.N && m.maxdim == p.maxdim && m.input_kind == input_kind) {
@@ -1737,9 +1758,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 m.force_big = m.force_big || force_big;
                 m.no_par = std::max(m.no_par, no_par);
                 m.scale = std::max(m.scale, scale);
+                m.no_cap = m.no_cap || no_cap;
                 seen = true;
             }
-        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale});
+        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale, no_cap});
     }
 
     // ---- result
@@ -1890,7 +1912,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 
 // entry: start from the configuration an earlier call of this shape ended on
 int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_result** out) {
-    bool fg = false, fb = false;
+    bool fg = false, fb = false, nc = false;
     int np = 0;
     int sc = 0;
     // not when a test forces a reducer (the memo would override what it asks for)
@@ -1904,9 +1926,10 @@ int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_
                 fb = m.force_big;
                 np = m.no_par;
                 sc = m.scale;
+                nc = m.no_cap;
             }
     }
-    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np);
+    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np, nc);
 }
 
 int validate(const tda_rips_args* a) {

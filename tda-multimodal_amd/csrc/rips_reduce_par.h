@@ -119,6 +119,7 @@ struct ParBufs {
     uint64_t* rq;         // requeue slots (used once per launch, zero = not yet written): item << 32 | record + 1
     uint64_t rq_cap;
     uint64_t step_limit;
+    float capf;           // column caps: keys above birth + capf * thresh are dropped (0 = off); see k_reduce_par
     uint64_t* dbg;        // -DTDA_PROFILE: [kParDbgCap][4] long-column timeline (layer << 40 | column, start, end, steps)
 };
 constexpr uint32_t kParDbgCap = 4096;
@@ -629,6 +630,7 @@ __device__ __forceinline__ uint64_t bucket_at(const ParBufs& P, uint32_t b, uint
 struct ParCol {
     ParRed rd;
     uint64_t steps = 0, adds = 0;
+    uint32_t capbits = 0xFFFFFFFFu;  // the column's cap (f32 bits of the largest kept diameter); record keys above it are dropped
 #ifdef TDA_PROF2
     // per-wave phase cycles of the current column (s_memtime deltas):
     // room + step barrier, front min, pivot + row loads, keys, bucket appends, front toggles, refills, owner path / records
@@ -1210,7 +1212,7 @@ __device__ __forceinline__ void col_add_keys(ParCol& C, const ParBufs& P, const 
         for (int q = 0; q < kParRegs; ++q) {
             const uint64_t e = e0 + threadIdx.x + (uint64_t)q * kParT;
             x[q] = e < len ? ld_glb(src, e) : 0;
-            if (e < len) vm |= 1u << q;
+            if (e < len && (uint32_t)(x[q] >> 32) <= C.capbits) vm |= 1u << q;  // keys above the column's cap: dropped
         }
         PAR_T0(tr0);
         front_room(C, P, kParT * kParRegs);
@@ -1389,6 +1391,26 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         const uint64_t ckey = ld_glb(resid, j);
         const uint64_t sidx = key_idx(ckey);
         const float sdm = key_diam(ckey);
+        // Column cap (r05).  With ripser's default threshold (the enclosing radius) the complex at r
+        // is a cone, so no H1 / H2 class is essential: every residual column has a finite pivot
+        // <= r.  Column j keeps only the keys <= rc = birth_j + capf * r (the rest are never stored):
+        // the reduction restricted to rows <= rc is exact for every column whose pivot is <= rc,
+        // because pivots only grow along a column's reduction.  The records j adds come from
+        // EARLIER columns (larger births, so larger caps: they hold every key j keeps), and an
+        // evicted column re-adds the record of an earlier one (the same order).  A column that
+        // runs empty below its cap has its pivot above it: the launch aborts (code 81) and the
+        // host re-runs the call without caps (remembered for the shape).  90 % of the keys the
+        // longest torus1024 column generates lie above its final pivot (tools/front_sim.py).
+        float rc = r;
+        bool capped = false;
+        if (!WIDE && P.capf > 0.0f) {
+            const float capd = sdm + P.capf * r;
+            if (capd < r) {
+                rc = capd;
+                capped = true;
+            }
+        }
+        C.capbits = capped ? __float_as_uint(rc) : 0xFFFFFFFFu;
         int sv[DIM + 1];
         decode<DIM>(sidx, n, sv);
         const uint32_t* cbits = DIM == 1 ? mst : clr + (size_t)l * clr_words;
@@ -1436,9 +1458,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(Dr, (size_t)sv[i] * n + v) : 0.0f;
             }
             if constexpr (DIM == 1)
-                col_cob<PACKED>(C, P, D, n, r, sv[0], sv[1], sdm, z[0], z[1]);
+                col_cob<PACKED>(C, P, D, n, rc, sv[0], sv[1], sdm, z[0], z[1]);
             else
-                col_cob2<PACKED, WIDE>(C, P, Dr, n, r, sv[0], sv[1], sv[2], WIDE ? __uint_as_float(sc) : sdm, z);
+                col_cob2<PACKED, WIDE>(C, P, Dr, n, rc, sv[0], sv[1], sv[2], WIDE ? __uint_as_float(sc) : sdm, z);
         } else {
             if (tid == 0) PS.last = ald(P.rec + (rec0 - 1) * 4 + 2);  // the record's pivot: its smallest key
             __syncthreads();
@@ -1493,6 +1515,10 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #endif
                 if (!more) {
                     if (PS.err) break;
+                    if (capped) {  // empty below the cap: the pivot lies above it -> the call re-runs uncapped
+                        if (tid == 0) PS.err = 81;
+                        break;
+                    }
                     if (tid == 0) ast(colpiv + j, kParEss);  // zero column: essential
                     done = true;
                 }
@@ -1559,9 +1585,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #endif
             if (app) {
                 if constexpr (DIM == 1)
-                    col_cob<PACKED>(C, P, D, n, r, fv[0], fv[1], pd, z[0], z[1], &stash);
+                    col_cob<PACKED>(C, P, D, n, rc, fv[0], fv[1], pd, z[0], z[1], &stash);
                 else
-                    col_cob2<PACKED, WIDE>(C, P, Dr, n, r, fv[0], fv[1], fv[2], WIDE ? __uint_as_float(fsc) : pd, z, &stash);
+                    col_cob2<PACKED, WIDE>(C, P, Dr, n, rc, fv[0], fv[1], fv[2], WIDE ? __uint_as_float(fsc) : pd, z, &stash);
                 ++adds;
 #ifdef TDA_PROFILE
                 pf[3] += clock64() - t0;

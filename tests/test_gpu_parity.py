@@ -853,3 +853,21 @@ def test_foreign_caller_stream_is_refused(gpu):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("RC")][0]
     assert line.startswith("RC -3") and "caller stream" in line, line
+
+
+@pytest.mark.parametrize("capf", ["0.5", "0.02", "0"])
+def test_column_caps_exact_and_fallback(gpu, monkeypatch, capf):
+    """k_reduce_par column caps (r05): keys above birth + capf * thresh are
+    never stored.  The default cap (0.5), a cap far too small (0.02: the long
+    columns run empty below it, the launch aborts with code 81 and the call
+    re-runs uncapped) and no cap all give the committed oracle results:
+    torus1024 (configs[3], H0-H1) and grid144 (configs[4], H0-H2, where the
+    H2 columns are capped too).  The memo is off, so every call starts capped."""
+    monkeypatch.setenv("TDA_PAR_CAPF", capf)
+    monkeypatch.setenv("TDA_RETRY_MEMO", "0")
+    z = _large_golden()
+    for name in ("torus1024", "grid144"):
+        X, md = z[f"{name}__X"], int(z[f"{name}__maxdim"])
+        res = gpu.ripser_batch(X, maxdim=md)
+        for l in range(X.shape[0]):
+            assert_same_golden(res[l], z, name, l, md)

@@ -24,9 +24,11 @@ for wl in os.environ.get("AB_WL", "torus1024,grid144").split(","):
     cs = hash(tuple(tuple(r.checksum) for r in res)) & 0xFFFFFFFF
     print(f"  {wl}: device {statistics.median(ms):.3f} ms (min {min(ms):.3f}), checksum {cs:08x}", flush=True)
 '''
-for lib in sys.argv[1:]:
-    print(os.path.basename(lib), flush=True)
-    env = dict(os.environ, TDA_RIPS_LIB=os.path.abspath(lib))
+for spec in sys.argv[1:]:  # lib.so or lib.so:VAR=value,VAR=value (test knobs; TDA_TEST_OVERRIDES is set)
+    lib, _, kv = spec.partition(":")
+    print(os.path.basename(lib), kv, flush=True)
+    env = dict(os.environ, TDA_RIPS_LIB=os.path.abspath(lib), TDA_TEST_OVERRIDES="1")
+    env.update(dict(x.split("=", 1) for x in kv.split(",") if x))
     r = subprocess.run([sys.executable, "-c", CHILD, ROOT], env=env, timeout=300)
     if r.returncode:
         sys.exit(r.returncode)
