@@ -88,6 +88,12 @@ float par_capf() {
     const char* e = test_env("TDA_PAR_CAPF");
     return e ? (float)atof(e) : 0.5f;
 }
+// H1 apparent test of k_reduce_par through the per-edge partner table (1 MB per layer at
+// N = 1024) instead of the 22 MB triangle bitmap; TDA_PAR_APPV=0 (tests / A/B) keeps the bitmap.
+bool par_appv() {
+    const char* e = test_env("TDA_PAR_APPV");
+    return e ? atoi(e) != 0 : true;
+}
 unsigned par_grid_size() {
     const char* g = test_env("TDA_PAR_GRID");
     const unsigned v = g ? (unsigned)atoi(g) : kParGridDefault;
@@ -136,6 +142,7 @@ struct Plan {
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
+    size_t o_appv = 0;                    // H1 apparent-partner table (k_reduce_par, packed keys): 0xFF every call
 };
 
 bool getenv_is(const char* name, const char* val) {
@@ -320,6 +327,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         p.o_necnt = take(L * 4);
     }
     p.memset_hi = o;
+    if (p.par && p.packed && p.maxdim >= 1 && par_appv()) p.o_appv = take(L * p.ncand[1] * 2);
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
     p.o_tmp = take(L * 2 * p.max_rcap * 8);
     if (p.maxdim >= 1) {
@@ -780,14 +788,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(hipSetDevice(dev));
     Workspace& w = *get_ws(dev, a.slot);
     std::unique_lock<std::mutex> guard(w.mu);  // released before any retry (which re-enters)
-    // allocations (first call / growth) never overlap another slot's capture
+    // allocations, frees and graph drops (first call / growth) never overlap another slot's
+    // capture: g_capture_mu is held from here through the buffer growth below, and released
+    // before the input copies (the host-input memcpy serialised pipelined slots)
     std::unique_lock<std::mutex> rt_lock(g_capture_mu);
     if (int rc = ws_prepare(w, p)) return rc;
     if (int rc = set_lds_attrs(dev)) return rc;
     // all work runs on the library stream, ordered after the caller's stream
     hipStream_t s = w.stream;
-    if (a.x_on_device && input_kind != 2 && !(a.flags & TDA_FLAG_INPUT_READY))
-        if (int rc = order_after_caller(s, w.evin, a.stream, dev)) return rc;
     char* B = w.dbuf;
     const int n = (int)p.N, L = (int)p.L;
     float* dist = (float*)(B + p.o_dist);
@@ -800,11 +808,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 
     // host inputs go through a pinned staging buffer: a stable graph source
+    // (grown here, filled after the lock is released)
     const void* xsrc = host_or_dev;
     const int nparts = input_kind == 2 ? 0 : a.n_parts;
-    if (!a.x_on_device || input_kind == 2) {
-        const size_t xbytes = input_kind == 2 ? binom((uint64_t)n, 2) * 4
-                                              : (size_t)L * n * (input_kind == 1 ? (size_t)n : (size_t)p.D) * esz;
+    const bool host_in = !a.x_on_device || input_kind == 2;
+    const bool dev_parts = !host_in && nparts > 0;
+    const size_t xbytes = input_kind == 2 ? binom((uint64_t)n, 2) * 4
+                                          : (size_t)L * n * (input_kind == 1 ? (size_t)n : (size_t)p.D) * esz;
+    if (host_in) {
         if (w.hin_cap < xbytes) {
             drop_graphs(w);
             if (w.hin) HIPC(hipHostFree(w.hin));
@@ -812,17 +823,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipHostMalloc((void**)&w.hin, std::max<size_t>(xbytes, 1 << 16), hipHostMallocDefault));
             w.hin_cap = std::max<size_t>(xbytes, 1 << 16);
         }
-        if (nparts > 0) {  // parts: one after the other into the staging buffer
-            const size_t pb = xbytes / nparts;
-            for (int i = 0; i < nparts; ++i) std::memcpy((char*)w.hin + i * pb, a.x_parts[i], pb);
-        } else if (xbytes) {
-            std::memcpy(w.hin, host_or_dev, xbytes);
-        }
         xsrc = w.hin;
-    } else if (nparts > 0) {
-        // device parts: gathered into the workspace's own input buffer by one kernel on the
-        // library stream (ordered after the caller's stream above, outside any captured graph)
-        const size_t xbytes = (size_t)L * n * (input_kind == 1 ? (size_t)n : (size_t)p.D) * esz;
+    } else if (dev_parts) {
         if (w.xin_cap < xbytes) {
             drop_graphs(w);
             if (w.xin) HIPC(hipFree(w.xin));
@@ -830,12 +832,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipMalloc(&w.xin, xbytes));
             w.xin_cap = xbytes;
         }
-        PartList pl = {};
-        for (int i = 0; i < nparts; ++i) pl.p[i] = a.x_parts[i];
-        const uint64_t words = xbytes / nparts / 4;
-        const unsigned gx = (unsigned)std::min<uint64_t>(64, (words + 255) / 256);
-        hipLaunchKernelGGL(k_gather_parts, dim3(std::max(1u, gx), nparts), dim3(256), 0, s, pl, words, (uint32_t*)w.xin);
-        HIPC(hipGetLastError());
         xsrc = w.xin;
     }
 
@@ -869,7 +865,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             HIPC(hipHostGetDevicePointer((void**)&w.hsil_dev, w.hsil, 0));
             w.hsil_cap = std::max<size_t>(need, 1 << 12);
         }
-        std::memcpy(w.hsil, a.labels, (size_t)nls * n * 4);
     }
 
     // TwoNN estimates -> host-mapped buffer (stable address: a graph source)
@@ -892,7 +887,29 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     if (!serial_stages)
         if (int rc = ws_side_streams(w)) return rc;
 
-    rt_lock.unlock();  // host buffers are in place; the capture below re-takes it
+    rt_lock.unlock();  // buffers are in place; the capture below re-takes it
+
+    // input copies and ordering, outside the lock
+    if (a.x_on_device && input_kind != 2 && !(a.flags & TDA_FLAG_INPUT_READY))
+        if (int rc = order_after_caller(s, w.evin, a.stream, dev)) return rc;
+    if (host_in) {
+        if (nparts > 0) {  // parts: one after the other into the staging buffer
+            const size_t pb = xbytes / nparts;
+            for (int i = 0; i < nparts; ++i) std::memcpy((char*)w.hin + i * pb, a.x_parts[i], pb);
+        } else if (xbytes) {
+            std::memcpy(w.hin, host_or_dev, xbytes);
+        }
+    } else if (dev_parts) {
+        // device parts: gathered into the workspace's own input buffer by one kernel on the
+        // library stream (ordered after the caller's stream above, outside any captured graph)
+        PartList pl = {};
+        for (int i = 0; i < nparts; ++i) pl.p[i] = a.x_parts[i];
+        const uint64_t words = xbytes / nparts / 4;
+        const unsigned gx = (unsigned)std::min<uint64_t>(64, (words + 255) / 256);
+        hipLaunchKernelGGL(k_gather_parts, dim3(std::max(1u, gx), nparts), dim3(256), 0, s, pl, words, (uint32_t*)w.xin);
+        HIPC(hipGetLastError());
+    }
+    if (nls) std::memcpy(w.hsil, a.labels, (size_t)nls * n * 4);
 
     // serial_stages: the side streams are aliased to the main one here and restored on return
     struct StreamSwap {
@@ -958,6 +975,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(rec_t(w.ev0));
     if (int rc = tm.begin()) return rc;
     HIPC(hipMemsetAsync(B + p.memset_lo, 0, p.memset_hi - p.memset_lo, s));
+    if (p.o_appv) HIPC(hipMemsetAsync(B + p.o_appv, 0xFF, (size_t)p.L * p.ncand[1] * 2, s));
     MARK("memset");
 
     // ---- distances (+ row maxima for the enclosing radius)
@@ -1160,6 +1178,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         db[d].resid = (uint64_t*)(B + p.o_resid[d]);
         db[d].rcap = p.rcap[d];
         db[d].ncand = p.ncand[d];
+        db[d].appv = d == 1 && p.o_appv ? (uint16_t*)(B + p.o_appv) : nullptr;
     }
     // N <= 64 with H2: the H2 columns (apparent<2>, their sort, phase 1) run
     // on a third stream beside the H1 chain; they only need apparent<1>'s

@@ -521,9 +521,15 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
 }
 
 // min live front key (block-uniform; kEmpty64 if none): every slot, 16-B
-// reads.  (r05: group minima kept by the toggles -- ds_min on insert, a dirty
-// bit on removal, only dirty groups rescanned -- measured slower: the front
-// minimum 1.9 K -> 4.2 K cycles a step, torus1024 41.9 -> 49.2 ms.)
+// reads.  (r05, measured slower: group minima kept by the toggles -- ds_min on
+// insert, a dirty bit on removal, only dirty groups rescanned: the front
+// minimum 1.9 K -> 4.2 K cycles a step, torus1024 41.9 -> 49.2 ms; a minimum
+// cache listing the slots of every live key below a bound taken from the scan
+// (the smallest second-smallest key over the threads' slot sets, ~28 keys):
+// 1.9 K -> 3.0 K cycles, 37.4 -> 42.2 ms -- an addition cancels the keys just
+// above its pivot, so the cache empties within ~1.5 steps (a replay of the
+// longest column's key trace: 33 % of the minima served; 80 % would need the
+// 128 smallest keys, which no longer avoids a block-wide reduction).)
 __device__ __forceinline__ uint64_t front_min(ParRed& rd) {
     uint64_t b = kEmpty64;
 #pragma unroll
@@ -1527,6 +1533,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             // pivot: vertices, index, apparent facet fv
             P2_T(ps2);
             int fv[DIM + 1];
+            int pw_third = -1;
             uint64_t pidx;
             const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
             const float pd = WIDE ? __uint_as_float((uint32_t)ld_glb(dsort + (size_t)l * ecap, pk >> kWideIdxBits))
@@ -1541,6 +1548,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                     const int f = (int)(plo & 3u);
                     fv[0] = f == 0 ? t[1] : t[0];
                     fv[1] = f == 2 ? t[1] : t[2];
+                    pw_third = f == 0 ? t[0] : f == 1 ? t[1] : t[2];  // the vertex the apparent facet omits
                     pidx = encode<2>(t);
                 } else {
                     pidx = plo;
@@ -1573,10 +1581,20 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #pragma unroll
                 for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(Dr, (size_t)fv[i] * n + v) : 0.0f;
             }
-            // every thread reads the pivot's bitmap word (one address per wave): no barrier
-            const uint32_t pw = ld_glb(pivg, pidx >> 5);
+            // every thread reads the pivot's apparent flag (one address per wave): no barrier.  H1 with
+            // packed keys: the facet's apparent-partner vertex (a 2-byte word of a 1 MB per-layer
+            // table, L2-resident) instead of the pivot's bit in the 22 MB triangle bitmap
+            uint32_t pw;
+            bool app;
+            if (DIM == 1 && PACKED && b1.appv) {
+                const uint32_t w16 = ld_glb(b1.appv + (size_t)l * b1.ncand, (size_t)c2u(fv[0]) + (uint32_t)fv[1]);
+                pw = w16;
+                app = w16 == (uint32_t)pw_third;
+            } else {
+                pw = ld_glb(pivg, pidx >> 5);
+                app = (pw >> (pidx & 31)) & 1u;
+            }
             stash_flush(C, P, stash);  // the previous step's back keys, under this step's load latency
-            const bool app = (pw >> (pidx & 31)) & 1u;
             P2_DEP(pw);
             P2_ACC(2, ps2);
 #ifdef TDA_PROFILE
