@@ -173,23 +173,35 @@ def build(verbose: bool = False, out: str | None = None, extra_flags: tuple = ()
 
     ``out``/``extra_flags`` build variants (e.g. ``-DTDA_PROFILE`` into another
     path, selected at load time with TDA_RIPS_LIB)."""
+    import shutil
+    import tempfile
+
     out = out or LIB_PATH
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    src = os.path.join(CSRC, "rips.hip")
-    cmd = [
-        os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"),
-        "--offload-arch=gfx950",
-        "-O3",
-        "-std=c++17",
-        "-shared",
-        "-fPIC",
-        "-I" + INCLUDE,
-        *extra_flags,
-        "-o",
-        out + ".tmp",
-        src,
-    ]
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    # compile from a snapshot of the sources: hipcc reads them once for the device pass and again,
+    # minutes later, for the host pass, so an edit in between would give a library whose host
+    # and device sides disagree on the kernel argument structs
+    snap = tempfile.mkdtemp(prefix="tda_build_")
+    try:
+        shutil.copytree(CSRC, os.path.join(snap, "pkg", "csrc"))  # csrc/../../include stays the include dir
+        shutil.copytree(INCLUDE, os.path.join(snap, "include"))
+        src = os.path.join(snap, "pkg", "csrc", "rips.hip")
+        cmd = [
+            os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"),
+            "--offload-arch=gfx950",
+            "-O3",
+            "-std=c++17",
+            "-shared",
+            "-fPIC",
+            "-I" + os.path.join(snap, "include"),
+            *extra_flags,
+            "-o",
+            out + ".tmp",
+            src,
+        ]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+    finally:
+        shutil.rmtree(snap, ignore_errors=True)
     if r.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + r.stderr[-4000:])
     if verbose and r.stderr:

@@ -88,12 +88,6 @@ float par_capf() {
     const char* e = test_env("TDA_PAR_CAPF");
     return e ? (float)atof(e) : 0.5f;
 }
-// H1 apparent test of k_reduce_par through the per-edge partner table (1 MB per layer at
-// N = 1024) instead of the 22 MB triangle bitmap; TDA_PAR_APPV=0 (tests / A/B) keeps the bitmap.
-bool par_appv() {
-    const char* e = test_env("TDA_PAR_APPV");
-    return e ? atoi(e) != 0 : true;
-}
 unsigned par_grid_size() {
     const char* g = test_env("TDA_PAR_GRID");
     const unsigned v = g ? (unsigned)atoi(g) : kParGridDefault;
@@ -142,7 +136,6 @@ struct Plan {
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
-    size_t o_appv = 0;                    // H1 apparent-partner table (k_reduce_par, packed keys): 0xFF every call
 };
 
 bool getenv_is(const char* name, const char* val) {
@@ -327,7 +320,6 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         p.o_necnt = take(L * 4);
     }
     p.memset_hi = o;
-    if (p.par && p.packed && p.maxdim >= 1 && par_appv()) p.o_appv = take(L * p.ncand[1] * 2);
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
     p.o_tmp = take(L * 2 * p.max_rcap * 8);
     if (p.maxdim >= 1) {
@@ -975,7 +967,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     HIPC(rec_t(w.ev0));
     if (int rc = tm.begin()) return rc;
     HIPC(hipMemsetAsync(B + p.memset_lo, 0, p.memset_hi - p.memset_lo, s));
-    if (p.o_appv) HIPC(hipMemsetAsync(B + p.o_appv, 0xFF, (size_t)p.L * p.ncand[1] * 2, s));
     MARK("memset");
 
     // ---- distances (+ row maxima for the enclosing radius)
@@ -1178,7 +1169,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         db[d].resid = (uint64_t*)(B + p.o_resid[d]);
         db[d].rcap = p.rcap[d];
         db[d].ncand = p.ncand[d];
-        db[d].appv = d == 1 && p.o_appv ? (uint16_t*)(B + p.o_appv) : nullptr;
     }
     // N <= 64 with H2: the H2 columns (apparent<2>, their sort, phase 1) run
     // on a third stream beside the H1 chain; they only need apparent<1>'s

@@ -58,10 +58,6 @@ struct DimBufs {              // per reduction dim d (columns = d-simplices)
     uint64_t* resid;          // residual column keys [L][rcap]
     uint64_t rcap;
     uint64_t ncand;           // C(N, d+1)
-    // d = 1 with k_reduce_par (N <= 1024, r05): per edge, the third vertex of its apparent pivot
-    // triangle, 0xFFFF if the edge is not apparent ([L][C(N, 2)], 2 B each: 1 MB at N = 1024, where
-    // the triangle bitmap is 22 MB).  k_reduce_par's apparent test then reads 2 bytes that stay in L2.
-    uint16_t* appv;
 };
 
 // ------------------------------------------------------------------ distance
@@ -1436,7 +1432,6 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                             kind = 1;
                             uint64_t tix = cofacet_index<DIM>(vs, bv);
                             matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
-                            if (DIM == 1 && b.appv) st_glb(b.appv + (size_t)l * b.ncand, s, (uint16_t)bv);
                             acc_cs += pair_hash(s, tix);
                             acc_app += 1;
                         }

@@ -81,7 +81,15 @@ constexpr int kParRegs = 2048 / kParT;  // keys per thread per pass of refills a
 #define TDA_PAR_REFILL 2
 #endif
 constexpr int kParRefill = TDA_PAR_REFILL;          // a refill keeps up to kParRefill passes (4096 keys) in registers
+#ifndef TDA_PAR_NLB  // build-time A/B knob (tools/): refills relative to the bucket's lower bound instead of its minimum
+// (r05: torus1024 34.4 -> 32.6 ms, torus1024x32 78-81 -> 72.9 ms, grid144 5.44 -> 5.40 ms)
+#define TDA_PAR_NLB 1
+#endif
 constexpr int kParRV = 1024 / kParT;   // coboundary vertices per thread per round (1024 per round)
+// vertex of thread t in slot q of the coboundary round starting at v0.  (r05: the odd slots
+// mirrored -- wave w taking 64-vertex blocks w and 2 W - 1 - w, to spread the waves' unequal key
+// counts -- measured no faster: torus1024 34.3 ms either way)
+__device__ __forceinline__ int par_vert(int v0, int q) { return v0 + q * kParT + (int)threadIdx.x; }
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
 constexpr uint64_t kParEss = kEmpty64;        // colpiv: essential (zero column)
 constexpr uint64_t kParSkip = kEmpty64 - 1;   // colpiv: cleared column (H0 death)
@@ -196,6 +204,7 @@ struct ParLds {
     uint32_t cptr[kParLv][kParChunks];
     uint32_t hist[kParLv];
     uint64_t red[2][kParW];
+    uint64_t redm[3];  // TDA_PAR_MINV & 2: block minimum cells (triple-buffered LDS u64 atomic min)
     uint32_t wsum[2][kParW];
     uint32_t anyf[2][kParW];
     uint64_t bc[8];
@@ -248,8 +257,18 @@ __device__ __forceinline__ void lds_sync() {
     asm volatile("" ::: "memory");
 }
 
+#ifndef TDA_PAR_MINV  // build-time A/B knob (tools/): block minimum -- bit 0: wave minimum as two u32 passes; bit 1: cross-wave by an LDS atomic min
+// (r05, torus1024: 0 36.9 ms, 1 36.4, 2 35.4, 3 34.7; tools/ubench_min: 1.41 K -> 1.12 K cycles per minimum)
+#define TDA_PAR_MINV 3
+#endif
+__device__ __forceinline__ uint64_t wave_min_2p(uint64_t v) {  // u64 wave minimum: the hi words, then the lo words of the lanes that hold it
+    const uint32_t h = wave_min_u32((uint32_t)(v >> 32));
+    const uint32_t l = wave_min_u32((uint32_t)(v >> 32) == h ? (uint32_t)v : ~0u);
+    return ((uint64_t)h << 32) | l;
+}
 struct ParRed {  // double-buffered block reductions: one barrier each
     uint32_t par = 0;
+    uint32_t parm = 0;  // TDA_PAR_MINV & 2: the minimum cell of this reduction (mod 3)
     // block-wide OR of p (HIP's OR-barrier builtin lowers to three barriers)
     __device__ __forceinline__ bool any(bool p) {
         const uint64_t m = __ballot(p);
@@ -262,7 +281,19 @@ struct ParRed {  // double-buffered block reductions: one barrier each
         return r != 0;
     }
     __device__ __forceinline__ uint64_t min(uint64_t v) {
-        v = wave_min_u64(v);
+        v = (TDA_PAR_MINV & 1) ? wave_min_2p(v) : wave_min_u64(v);
+        if (TDA_PAR_MINV & 2) {
+            // cell parm was reset two reductions ago; the next one's cell was last read before the
+            // previous barrier, so it is reset here for the reduction after this one
+            const uint32_t c = parm, cn = c == 2 ? 0 : c + 1;
+            parm = cn;
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_fetch_min((TDA_LDS unsigned long long*)&PS.redm[c], (unsigned long long)v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (threadIdx.x == 0) PS.redm[cn] = kEmpty64;
+            lds_sync();
+            return PS.redm[c];
+        }
         const uint32_t b = par++ & 1;
         if ((threadIdx.x & 63) == 0) PS.red[b][threadIdx.x >> 6] = v;
         lds_sync();
@@ -848,6 +879,21 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
     uint64_t x[kParRefill][kParRegs];
     uint32_t vm[kParRefill] = {};
+#if TDA_PAR_NLB
+    // no minimum pass: the new reference is the smallest key with bucket b's common high bits
+    // (bits above b - 1 as `last`, bit b - 1 set), a lower bound of every key in the bucket, so
+    // the bucket's keys fall in levels < b and the higher buckets keep theirs.  (The exact
+    // minimum puts at least one key in the front; with the bound a refill may place none and
+    // the next one refines the lower buckets.)
+    const uint64_t lastv = PS.last;
+    const uint64_t nl = b >= 64 ? (1ull << 63) : (((lastv >> b) << b) | (1ull << (b - 1)));
+    if (inreg) {
+#pragma unroll
+        for (int h = 0; h < kParRefill; ++h) vm[h] = bucket_batch(P, (uint32_t)b, h * kPass, c, x[h]);
+    }
+    __syncthreads();  // the resets above are done
+    PAR_Q3(1);
+#else
     // pass 1: minimum (raw; a cancelled duplicate is still a lower bound of every live key)
     uint64_t mn = kEmpty64;
     if (inreg) {
@@ -868,6 +914,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     mn = C.rd.min(mn);  // barrier: the resets above are done too
     PAR_Q3(1);
     const uint64_t nl = mn;
+#endif
     // pass 2: histogram of the new levels (all < b); the front keeps the lowest
     // levels that hold at most kFrontFill keys.  (A binary search on the level
     // with block counts instead of the atomics measured slower: 7.1 vs 4.3 M
@@ -965,7 +1012,7 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
         float da[kParRV], db[kParRV];
 #pragma unroll
         for (int q = 0; q < kParRV; ++q) {
-            const int v = v0 + (int)threadIdx.x + q * kParT;
+            const int v = par_vert(v0, q);
             if (v0 == 0) {
                 da[q] = da0[q];
                 db[q] = db0[q];
@@ -980,7 +1027,7 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
         uint32_t vm = 0;
 #pragma unroll
         for (int q = 0; q < kParRV; ++q) {
-            const int v = v0 + (int)threadIdx.x + q * kParT;
+            const int v = par_vert(v0, q);
             key[q] = 0;
             if (v >= n || v == a || v == b) continue;
             const float cd = fmaxf(sd, fmaxf(da[q], db[q]));
@@ -1039,7 +1086,7 @@ __device__ __forceinline__ void col_cob2(ParCol& C, const ParBufs& P, const floa
         float da[kParRV], db[kParRV], dc[kParRV];
 #pragma unroll
         for (int q = 0; q < kParRV; ++q) {
-            const int v = v0 + (int)threadIdx.x + q * kParT;
+            const int v = par_vert(v0, q);
             if (v0 == 0) {
                 da[q] = r0[0][q];
                 db[q] = r0[1][q];
@@ -1055,7 +1102,7 @@ __device__ __forceinline__ void col_cob2(ParCol& C, const ParBufs& P, const floa
         uint32_t vm = 0;
 #pragma unroll
         for (int q = 0; q < kParRV; ++q) {
-            const int v = v0 + (int)threadIdx.x + q * kParT;
+            const int v = par_vert(v0, q);
             key[q] = 0;
             if (v >= n || v == a || v == b || v == c) continue;
             if constexpr (WIDE) {
@@ -1333,6 +1380,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
     if (tid == 0) {
         PS.err = 0;
         PS.wide = WIDE ? 1u : 0u;
+        PS.redm[0] = PS.redm[1] = PS.redm[2] = kEmpty64;
     }
     __syncthreads();
     const uint64_t total = ald(&P.ctl->total);
@@ -1459,7 +1507,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             float z[DIM + 1][kParRV];
 #pragma unroll
             for (int q = 0; q < kParRV; ++q) {
-                const int v = tid + q * kParT;
+                const int v = par_vert(0, q);
 #pragma unroll
                 for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(Dr, (size_t)sv[i] * n + v) : 0.0f;
             }
@@ -1533,7 +1581,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             // pivot: vertices, index, apparent facet fv
             P2_T(ps2);
             int fv[DIM + 1];
-            int pw_third = -1;
             uint64_t pidx;
             const uint32_t plo = 0xFFFFFFFFu - (uint32_t)pk;
             const float pd = WIDE ? __uint_as_float((uint32_t)ld_glb(dsort + (size_t)l * ecap, pk >> kWideIdxBits))
@@ -1548,7 +1595,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                     const int f = (int)(plo & 3u);
                     fv[0] = f == 0 ? t[1] : t[0];
                     fv[1] = f == 2 ? t[1] : t[2];
-                    pw_third = f == 0 ? t[0] : f == 1 ? t[1] : t[2];  // the vertex the apparent facet omits
                     pidx = encode<2>(t);
                 } else {
                     pidx = plo;
@@ -1577,24 +1623,16 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             float z[DIM + 1][kParRV];
 #pragma unroll
             for (int q = 0; q < kParRV; ++q) {
-                const int v = tid + q * kParT;
+                const int v = par_vert(0, q);
 #pragma unroll
                 for (int i = 0; i <= DIM; ++i) z[i][q] = v < n ? ld_glb(Dr, (size_t)fv[i] * n + v) : 0.0f;
             }
-            // every thread reads the pivot's apparent flag (one address per wave): no barrier.  H1 with
-            // packed keys: the facet's apparent-partner vertex (a 2-byte word of a 1 MB per-layer
-            // table, L2-resident) instead of the pivot's bit in the 22 MB triangle bitmap
-            uint32_t pw;
-            bool app;
-            if (DIM == 1 && PACKED && b1.appv) {
-                const uint32_t w16 = ld_glb(b1.appv + (size_t)l * b1.ncand, (size_t)c2u(fv[0]) + (uint32_t)fv[1]);
-                pw = w16;
-                app = w16 == (uint32_t)pw_third;
-            } else {
-                pw = ld_glb(pivg, pidx >> 5);
-                app = (pw >> (pidx & 31)) & 1u;
-            }
+            // every thread reads the pivot's bitmap word (one address per wave): no barrier.  (r05: a
+            // per-edge apparent-partner table, 2 B per edge -- 1 MB per layer at N = 1024 against the
+            // 22 MB triangle bitmap -- measured no faster: torus1024 37.0 vs 36.7 ms, dropped)
+            const uint32_t pw = ld_glb(pivg, pidx >> 5);
             stash_flush(C, P, stash);  // the previous step's back keys, under this step's load latency
+            const bool app = (pw >> (pidx & 31)) & 1u;
             P2_DEP(pw);
             P2_ACC(2, ps2);
 #ifdef TDA_PROFILE
