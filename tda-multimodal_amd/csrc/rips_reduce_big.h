@@ -45,24 +45,84 @@ constexpr uint64_t kWideIdxMask = (1ull << kWideIdxBits) - 1;
 constexpr uint32_t kCodeInf = (1u << 21) - 1;
 
 // ---- wide H2 keys: per-layer edge codes
-// k_edge_sort: one workgroup per layer sorts the f32 bits of its C(N,2) edge
-// lengths (row-major strict upper triangle) ascending: LDS bitonic chunks of
-// 16384 keys, then merge-path passes in HBM (block_sort).
+// The f32 bits of each layer's C(N,2) edge lengths (row-major strict upper
+// triangle), sorted ascending over the whole GPU: k_edge_keys writes them,
+// k_edge_chunks sorts 16384-key chunks in LDS (bitonic, one 1024-thread block
+// per chunk), then log2(C(N,2) / 16384) k_edge_merge passes double the sorted
+// runs (merge path: every thread finds its first output's split by binary
+// search and merges 16 outputs).  (r04-: one workgroup per layer sorted and
+// merged everything: 70.6 ms at N = 2048, L = 1.)
 constexpr int kEdgeSortLog2 = 14;
 constexpr size_t kEdgeSortLds = size_t(8) << kEdgeSortLog2;
-__global__ __launch_bounds__(1024) void k_edge_sort(const float* __restrict__ dist, int n, uint64_t* __restrict__ dsort,
-                                                    uint64_t* __restrict__ tmp, uint64_t ecap) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.x;
+constexpr uint32_t kMergePer = 16;                 // outputs per thread of a merge pass
+constexpr uint32_t kMergeSeg = 256 * kMergePer;    // outputs per block
+__global__ __launch_bounds__(256) void k_edge_keys(const float* __restrict__ dist, int n, uint64_t* __restrict__ keys, uint64_t ecap) {
+    const int l = blockIdx.y;
     const float* D = dist + (size_t)l * n * n;
-    uint64_t* keys = dsort + (size_t)l * ecap;
+    uint64_t* K = keys + (size_t)l * ecap;
     const uint32_t nn = (uint32_t)n * (uint32_t)n;
-    for (uint32_t q = threadIdx.x; q < nn; q += blockDim.x) {
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nn; q += gridDim.x * blockDim.x) {
         const uint32_t i = q / (uint32_t)n, j = q - i * (uint32_t)n;
-        if (j > i) st_glb(keys, (size_t)i * (2 * (size_t)n - i - 1) / 2 + (j - i - 1), (uint64_t)__float_as_uint(ld_glb(D, q)));
+        if (j > i) st_glb(K, (size_t)i * (2 * (size_t)n - i - 1) / 2 + (j - i - 1), (uint64_t)__float_as_uint(ld_glb(D, q)));
     }
+}
+__global__ __launch_bounds__(1024) void k_edge_chunks(uint64_t* __restrict__ keys, uint64_t E, uint64_t ecap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t* sk = (uint64_t*)smem;
+    const uint32_t t = threadIdx.x, T = blockDim.x;
+    const uint64_t c0 = (uint64_t)blockIdx.x << kEdgeSortLog2;
+    if (c0 >= E) return;
+    uint64_t* K = keys + (size_t)blockIdx.y * ecap + c0;
+    const uint32_t m = (uint32_t)min((uint64_t)1 << kEdgeSortLog2, E - c0);
+    uint32_t p2 = 1;
+    while (p2 < m) p2 <<= 1;
+    for (uint32_t e = t; e < p2; e += T) sk[e] = e < m ? ld_glb(K, e) : kEmpty64;
     __syncthreads();
-    block_sort<false>(keys, nullptr, binom((uint64_t)n, 2), tmp + (size_t)l * ecap, nullptr, (uint64_t*)smem, nullptr, kEdgeSortLog2);
+    for (uint32_t k = 2; k <= p2; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t e = t; e < p2; e += T) {
+                const uint32_t x = e ^ j;
+                if (x > e) {
+                    const bool up = (e & k) == 0;
+                    const uint64_t a = sk[e], b = sk[x];
+                    if ((a > b) == up) {
+                        sk[e] = b;
+                        sk[x] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t e = t; e < m; e += T) st_glb(K, e, sk[e]);
+}
+// runs of width w (a power of two >= kMergePer) -> 2 w; every thread's kMergePer outputs lie in one pair of runs
+__global__ __launch_bounds__(256) void k_edge_merge(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, uint64_t E, uint64_t ecap,
+                                                    uint64_t w) {
+    const uint64_t o0 = (uint64_t)blockIdx.x * kMergeSeg + (uint64_t)threadIdx.x * kMergePer;
+    if (o0 >= E) return;
+    const uint64_t* S = src + (size_t)blockIdx.y * ecap;
+    uint64_t* O = dst + (size_t)blockIdx.y * ecap;
+    const uint64_t o1 = min(o0 + kMergePer, E);
+    const uint64_t a0 = o0 / (2 * w) * (2 * w), a1 = min(a0 + w, E), b1 = min(a0 + 2 * w, E);
+    const uint64_t la = a1 - a0, lb = b1 - a1, d0 = o0 - a0;
+    // merge path: the first output's split (i from run A, d0 - i from run B)
+    uint64_t lo = d0 > lb ? d0 - lb : 0, hi = min(d0, la);
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (ld_glb(S, a0 + mid) <= ld_glb(S, a1 + d0 - mid - 1))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    uint64_t ia = lo, ib = d0 - lo;
+    for (uint64_t o = o0; o < o1; ++o) {
+        const bool takeA = ib >= lb || (ia < la && ld_glb(S, a0 + ia) <= ld_glb(S, a1 + ib));
+        st_glb(O, o, takeA ? ld_glb(S, a0 + ia) : ld_glb(S, a1 + ib));
+        if (takeA)
+            ++ia;
+        else
+            ++ib;
+    }
 }
 
 // k_edge_codes: code(i, j) = position of the first occurrence of d(i, j) in

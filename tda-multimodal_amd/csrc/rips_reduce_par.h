@@ -193,6 +193,7 @@ constexpr uint32_t kTabMax = kFrontLog * 3 / 4;  // filled slots allowed before 
 constexpr uint32_t kTabPer = kFrontLog / kParT;  // slots per thread in scans
 constexpr uint32_t kStageW = 64 * 4;            // per-wave staging of the keys one toggle pass hands to the table
 #endif
+
 struct ParLds {
     uint64_t log[kFrontLog];
 #if TDA_PAR_FRONT == 2
@@ -818,6 +819,9 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
     (void)stash;
     PAR_T0(tb0);
     P2_T(pb0);
+    // (r05: back keys staged per wave in LDS and appended in bulk, 256 or 128 per wave -- one
+    // slot-atomic / chunk / store chain per flush instead of per step -- measured slower:
+    // torus1024 32.2-32.6 -> 33.2 ms)
     bucket_append<R>(k, bb, bm, P);
     P2_ACC(4, pb0);
     PAR_ACC(2, tb0);
@@ -1493,7 +1497,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             prealloc = true;
         }
         for (uint32_t q = tid; q < kParLv; q += kParT) PS.bcnt[q] = 0;
-            uint32_t sc = 0;  // WIDE: the column's edge code
+        uint32_t sc = 0;  // WIDE: the column's edge code
         if constexpr (WIDE) {
             const uint32_t* Dc = (const uint32_t*)Dr;
             sc = max(ld_glb(Dc, (size_t)sv[0] * n + sv[1]), max(ld_glb(Dc, (size_t)sv[0] * n + sv[2]), ld_glb(Dc, (size_t)sv[1] * n + sv[2])));

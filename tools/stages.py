@@ -14,8 +14,9 @@ pkg = importlib.import_module("tda-multimodal_amd")
 wl = sys.argv[1]
 X = torch.from_numpy(bench.make_workload(wl)).to("cuda:0")
 md = int(sys.argv[2]) if len(sys.argv) > 2 else bench.WORKLOADS[wl][1]
+kw = dict(bench.CALL_KW.get(wl, {}))  # e.g. torus2048_h2's thresh
 for _ in range(2):
-    pkg.ripser_batch(X, maxdim=md)
-_, info = pkg.ripser_batch(X, maxdim=md, return_time=True, stage_times=True, stage_serial=True)
+    pkg.ripser_batch(X, maxdim=md, **kw)
+_, info = pkg.ripser_batch(X, maxdim=md, return_time=True, stage_times=True, stage_serial=True, **kw)
 tag = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith("TDA_"))
 print(f"[{wl} {tag}] device {info['device_ms']:.3f} ms: " + ", ".join(f"{n} {t:.3f}" for n, t in info["stages"]), flush=True)
