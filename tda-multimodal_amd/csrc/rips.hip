@@ -136,6 +136,11 @@ struct Plan {
            o_hsig = 0, o_rowmax = 0, o_pairs[4] = {0}, o_h0s = 0,
            o_fk = 0, o_fv = 0, o_pptr = 0, o_pcap = 0, o_outoff = 0, total = 0;
     size_t memset_lo = 0, memset_hi = 0;  // zeroed every call: stats .. pivbits
+    // H2 pivot bitmap too large to memset every call (>= 2 GB: C(N, 4) / 8 B per layer, 91 GB at
+    // N = 2048): kept zero between calls by k_clear_words over the words k_apparent<2> lists
+    bool piv2_sparse = false;
+    uint64_t clr_cap = 0;
+    size_t o_clr2 = 0;
 };
 
 bool getenv_is(const char* name, const char* val) {
@@ -311,7 +316,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     p.memset_lo = o;
     p.o_stats = take(L * sizeof(LayerStats));
     p.o_mst = take(L * p.mst_words * 4);
-    for (int d = 1; d <= p.maxdim; ++d) p.o_piv[d] = take(L * p.piv_words[d] * 4);
+    p.piv2_sparse = p.maxdim >= 2 && L * p.piv_words[2] * 4 >= (2ull << 30) && !test_env_is("TDA_PIV2_SPARSE", "0");
+    for (int d = 1; d <= p.maxdim; ++d)
+        if (!(d == 2 && p.piv2_sparse)) p.o_piv[d] = take(L * p.piv_words[d] * 4);
     p.o_rowmax = take(L * N * 4);
     p.o_p1used = take(L * 8);
     p.o_p1next = take(L * 4);
@@ -320,6 +327,12 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
         p.o_necnt = take(L * 4);
     }
     p.memset_hi = o;
+    if (p.piv2_sparse) {
+        p.o_piv[2] = take(L * p.piv_words[2] * 4);
+        // one entry per apparent H2 pair (at most one per triangle); an overflow only costs a memset
+        p.clr_cap = std::min<uint64_t>(std::max<uint64_t>(p.ncand[2], 1), 1ull << 28);
+        p.o_clr2 = take(L * p.clr_cap * 8);
+    }
     for (int d = 1; d <= p.maxdim; ++d) p.o_resid[d] = take(L * p.rcap[d] * 8);
     p.o_tmp = take(L * 2 * p.max_rcap * 8);
     if (p.maxdim >= 1) {
@@ -430,6 +443,10 @@ struct Workspace {
     OutPair* hout_dev = nullptr;
     size_t hout_cap = 0;      // in pairs
     LayerStats* hstats = nullptr;  // host-mapped: k_emit writes it
+    // sparse-cleared H2 pivot bitmap (Plan::piv2_sparse): the region known to be zero
+    bool piv2_dirty = true;
+    char* piv2_ptr = nullptr;
+    size_t piv2_bytes = 0;
     char* hsil = nullptr;          // host-mapped: silhouette labels [S][N] i32, then scores [L][S] f64
     char* hsil_dev = nullptr;
     size_t hsil_cap = 0;
@@ -636,6 +653,7 @@ int ws_prepare(Workspace& w, const Plan& p) {
     }
     if (w.dcap < p.total) {
         drop_graphs(w);
+        w.piv2_dirty = true;
         if (w.dbuf) HIPC(hipFree(w.dbuf));
         w.dbuf = nullptr;
         size_t cap = std::max<size_t>(p.total, w.dcap + w.dcap / 2);
@@ -713,7 +731,7 @@ int set_lds_attrs(int dev) {
     HIPC(hipFuncSetAttribute((const void*)k_reduce_par<2, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ParLds)));
 
     HIPC(hipFuncSetAttribute((const void*)k_h2_phase1, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-    HIPC(hipFuncSetAttribute((const void*)k_edge_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEdgeSortLds));
+    HIPC(hipFuncSetAttribute((const void*)k_edge_chunks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kEdgeSortLds));
     HIPC(hipFuncSetAttribute((const void*)k_silhouette, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
     HIPC(hipFuncSetAttribute((const void*)k_twonn, hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 4));
 #define TDA_ATTR_CHAIN(K, F) HIPC(hipFuncSetAttribute((const void*)k_h1_chain<K, F>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
@@ -1169,6 +1187,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         db[d].resid = (uint64_t*)(B + p.o_resid[d]);
         db[d].rcap = p.rcap[d];
         db[d].ncand = p.ncand[d];
+        db[d].clr = d == 2 && p.piv2_sparse ? (uint64_t*)(B + p.o_clr2) : nullptr;
+        db[d].clr_cap = d == 2 && p.piv2_sparse ? p.clr_cap : 0;
     }
     // N <= 64 with H2: the H2 columns (apparent<2>, their sort, phase 1) run
     // on a third stream beside the H1 chain; they only need apparent<1>'s
@@ -1428,8 +1448,20 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             gb.dsort = (const uint64_t*)(B + p.o_dsort);
             gb.ecap = p.ecap;
             if (p.wide) {  // edge codes of the wide H2 keys (thresholds are known: after the H0 join)
-                hipLaunchKernelGGL(k_edge_sort, dim3(L), dim3(1024), kEdgeSortLds, s, dist, n, (uint64_t*)(B + p.o_dsort),
-                                   (uint64_t*)(B + p.o_dtmp), p.ecap);
+                // the sorted lengths end in dsort: with an odd number of merge passes the keys start in dtmp
+                const uint64_t E = binom((uint64_t)n, 2), CH = 1ull << kEdgeSortLog2;
+                int passes = 0;
+                for (uint64_t w = CH; w < E; w <<= 1) ++passes;
+                uint64_t* ka = (uint64_t*)(B + ((passes & 1) ? p.o_dtmp : p.o_dsort));
+                uint64_t* kb = (uint64_t*)(B + ((passes & 1) ? p.o_dsort : p.o_dtmp));
+                const unsigned gk = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
+                hipLaunchKernelGGL(k_edge_keys, dim3(gk, L), dim3(256), 0, s, dist, n, ka, p.ecap);
+                hipLaunchKernelGGL(k_edge_chunks, dim3((unsigned)((E + CH - 1) / CH), L), dim3(1024), kEdgeSortLds, s, ka, E, p.ecap);
+                for (uint64_t w = CH; w < E; w <<= 1) {
+                    hipLaunchKernelGGL(k_edge_merge, dim3((unsigned)((E + kMergeSeg - 1) / kMergeSeg), L), dim3(256), 0, s, ka, kb, E,
+                                       p.ecap, w);
+                    std::swap(ka, kb);
+                }
                 HIPC(hipGetLastError());
                 MARK("k_edge_sort");
                 const unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
@@ -1525,6 +1557,12 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                        (uint32_t*)(B + p.o_fv), p.sstride, w.houtoff_dev, w.hout_dev, (uint64_t)w.hout_cap, w.hstats_dev);
     HIPC(hipGetLastError());
     MARK("k_emit");
+    if (p.piv2_sparse) {  // the H2 pivot bitmap back to zero: only the words this call set
+        hipLaunchKernelGGL(k_clear_words, dim3(1024, L), dim3(256), 0, s, stats, (const uint64_t*)(B + p.o_clr2), p.clr_cap,
+                           (uint32_t*)(B + p.o_piv[2]), p.piv_words[2]);
+        HIPC(hipGetLastError());
+        MARK("k_clear_words");
+    }
     HIPC(rec_t(w.ev1));
     return 0;
     };  // enqueue
@@ -1532,6 +1570,16 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     static const bool host_prof = getenv_is("TDA_HOST_PROF", "1");
     using hclk = std::chrono::steady_clock;
     const auto h0 = hclk::now();
+    if (p.piv2_sparse) {  // first use of the region, or the last call left it dirty: one full memset
+        char* pv2 = B + p.o_piv[2];
+        const size_t bytes = (size_t)L * p.piv_words[2] * 4;
+        if (w.piv2_dirty || w.piv2_ptr != pv2 || w.piv2_bytes < bytes) {
+            HIPC(hipMemsetAsync(pv2, 0, bytes, s));
+            w.piv2_ptr = pv2;
+            w.piv2_bytes = bytes;
+        }
+        w.piv2_dirty = true;  // until this call has cleared the words it set
+    }
     if (ge) {
         HIPC(hipEventRecord(w.ev0, s));
         HIPC(hipGraphLaunch(ge->exec, s));
@@ -1569,6 +1617,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
 
     int errs = 0;
     for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
+    if (p.piv2_sparse) {  // clean again unless a layer's word list overflowed
+        bool over = false;
+        for (int l = 0; l < L; ++l) over |= (uint64_t)w.hstats[l].n_clr2 > p.clr_cap;
+        w.piv2_dirty = over;
+    }
     if (errs == ERR_OUT_CAP) {
         size_t need = 0;
         for (int l = 0; l < L; ++l)

@@ -46,6 +46,7 @@ struct LayerStats {  // zeroed every call; copied to the host result
     int64_t nskip[4];      // residual columns cleared by the serial reduction (host: n_residual - nskip)
     uint64_t rmask[4];     // residual pivot map mask used by the dim's reducer (HBM map consumers)
     int64_t ntri;          // N <= 64: triangles <= thresh (k_prep_tables)
+    int64_t n_clr2;        // sparse-cleared H2 pivot bitmap: words k_apparent<2> listed for the end-of-call clear
     uint64_t prof[5][8];   // -DTDA_PROFILE builds: cycle counters (per dim; [3]: k_h0_wave, [4]: k_prep_layer)
 };
 enum : int32_t { ERR_RESID_CAP = 1, ERR_PAIR_CAP = 2, ERR_WORK_CAP = 4, ERR_VPOOL_CAP = 8, ERR_OUT_CAP = 16 };
@@ -58,6 +59,10 @@ struct DimBufs {              // per reduction dim d (columns = d-simplices)
     uint64_t* resid;          // residual column keys [L][rcap]
     uint64_t rcap;
     uint64_t ncand;           // C(N, d+1)
+    // d = 2 with a bitmap too large to memset every call (C(N, 4) / 8 B: 91 GB at N = 2048): the
+    // word of every bit k_apparent<2> sets, [L][clr_cap]; k_clear_words zeroes them at the end
+    uint64_t* clr;
+    uint64_t clr_cap;
 };
 
 // ------------------------------------------------------------------ distance
@@ -1381,6 +1386,7 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < b.ncand; base += stride) {
         const uint64_t s = base + threadIdx.x;
         int kind = 0;  // 0 skip, 1 apparent, 2 residual (incl. empty coboundary)
+        uint64_t tixv = 0;
         int vs[DIM + 1];
         float sd = 0.0f;
         if (s < b.ncand && !(cleared && ((ld_glb(cleared, s >> 5) >> (s & 31)) & 1u))) {
@@ -1432,6 +1438,7 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                             kind = 1;
                             uint64_t tix = cofacet_index<DIM>(vs, bv);
                             matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
+                            tixv = tix;
                             acc_cs += pair_hash(s, tix);
                             acc_app += 1;
                         }
@@ -1440,6 +1447,15 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
             }
         }
         acc_cols += (kind != 0);
+        if (DIM == 2 && b.clr) {  // sparse-cleared bitmap: list the words set (wave aggregated)
+            const uint64_t mc = __ballot(kind == 1);
+            if (mc) {
+                uint64_t cb = 0;
+                if (lane_id() == __builtin_ctzll(mc)) cb = atomicAdd((unsigned long long*)&st->n_clr2, (unsigned long long)__popcll(mc));
+                cb = shfl_u64(cb, __builtin_ctzll(mc)) + lanes_below(mc);
+                if (kind == 1 && cb < b.clr_cap) st_glb(b.clr + (size_t)l * b.clr_cap, cb, tixv >> 5);
+            }
+        }
         // residual append (wave aggregated)
         const uint64_t m = __ballot(kind == 2);
         if (m) {
@@ -1645,6 +1661,17 @@ __global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict_
 struct PartList {
     const void* p[TDA_MAX_PARTS];
 };
+// end of a call with a sparse-cleared H2 pivot bitmap: zero the words k_apparent<2> listed
+// (a layer whose list overflowed leaves the bitmap dirty: the host memsets it before the next call)
+__global__ __launch_bounds__(256) void k_clear_words(const LayerStats* __restrict__ stats, const uint64_t* __restrict__ clr, uint64_t cap,
+                                                     uint32_t* __restrict__ pivbits, uint64_t piv_words) {
+    const int l = blockIdx.y;
+    const uint64_t cnt = min((uint64_t)stats[l].n_clr2, cap);
+    const uint64_t* c = clr + (size_t)l * cap;
+    uint32_t* pv = pivbits + (size_t)l * piv_words;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) st_glb(pv, ld_glb(c, i), 0u);
+}
+
 __global__ __launch_bounds__(256) void k_gather_parts(PartList pl, uint64_t part_words, uint32_t* __restrict__ dst) {
     const int k = blockIdx.y;
     const uint32_t* src = (const uint32_t*)pl.p[k];

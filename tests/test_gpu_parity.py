@@ -446,6 +446,19 @@ def test_h2_n2048_finite_thresh_vs_committed_oracle(gpu, monkeypatch, name):
     assert_same_golden(res[0], z, name, 0, 2)
 
 
+def test_h2_sparse_pivot_bitmap_reused_across_calls(gpu, monkeypatch):
+    """At N = 2048 the H2 pivot bitmap (C(N, 4) / 8 B = 91 GB) is not memset
+    per call: k_clear_words zeroes the words k_apparent<2> listed, at the end
+    of the call.  Three calls on one workspace (t12, t16, t12 again), each
+    against the oracle: a word left set by a previous call would make a
+    triangle look apparent and change the pairs."""
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")
+    z = np.load(os.path.join(GOLDEN, "large_h2_2048.npz"))
+    for name in ("torus2048_t12", "torus2048_t16", "torus2048_t12"):
+        res = gpu.ripser_batch(z[f"{name}__X"], maxdim=2, thresh=float(z[f"{name}__user_thresh"]))
+        assert_same_golden(res[0], z, name, 0, 2)
+
+
 @pytest.mark.parametrize("wide,par2", [("0", "1"), ("1", "1"), ("0", "0"), ("1", "0")])
 def test_h2_wide_keys_forced_vs_oracle(gpu, oracle, monkeypatch, wide, par2):
     """The wide edge-code keys forced below N = 568 (TDA_H2_WIDE=1) must give
