@@ -18,7 +18,7 @@ for wl in os.environ.get("AB_WL", "torus1024,grid144").split(","):
     X = torch.from_numpy(bench.make_workload(wl)).to("cuda:0")
     ms = []
     for i in range(calls):
-        res, info = pkg.ripser_batch(X, maxdim=md, return_time=True)
+        res, info = pkg.ripser_batch(X, maxdim=md, return_time=True, **bench.CALL_KW.get(wl, {}))
         if i:
             ms.append(info["device_ms"])
     cs = hash(tuple(tuple(r.checksum) for r in res)) & 0xFFFFFFFF
