@@ -1194,14 +1194,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     // on a third stream beside the H1 chain; they only need apparent<1>'s
     // pivot bitmap, and the chain records its residual pivots separately
     const bool split2 = p.dense && p.maxdim >= 2;
-    auto launch_apparent = [&](int d, hipStream_t st) {
+    auto launch_apparent = [&](int d, hipStream_t st, uint64_t total_override = 0) {
         uint64_t blocks = (p.ncand[d] + 255) / 256;
         // total blocks over all layers: measured (r01, sweep48) 1024 beats 4096,
         // whose grid holds every CU while the critical small kernels wait; off
         // the dense path the apparent kernels run alone: 4096 (r02, grid144:
         // apparent<2> 1.08 -> 0.87 ms; staging the 83-KB matrix in LDS: 2.25 ms)
         const char* app_env = test_env("TDA_APP_GRID");
-        const uint64_t app_total = app_env ? strtoull(app_env, nullptr, 10) : (p.dense ? 1024 : 4096);
+        const uint64_t app_total = app_env ? strtoull(app_env, nullptr, 10) : total_override ? total_override : (p.dense ? 1024 : 4096);
         unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, std::max<uint64_t>(1, app_total / L)));
         const int app_lds_max = test_env("TDA_APP_LDS_MAXN") ? atoi(test_env("TDA_APP_LDS_MAXN")) : kAppLdsMaxN;
         const bool dl = n <= app_lds_max && 16 + (size_t)n * n * 4 <= (size_t)kLdsMax;
@@ -1295,9 +1295,22 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     if (p.maxdim < 1 || order >= 1)
         if (int rc = launch_side()) return rc;
     const bool h2_side = !p.dense && p.par && p.par2 && p.maxdim >= 2;
+    // the H2 branch forks once k_reduce_par<1> is about to start (after k_par_init), not after
+    // apparent<1>: launched together with the H1 prerequisites, the GPU-filling apparent<2> pass
+    // slowed them (torus2048_h2 trace: sort<1> 0.06 -> 7 ms, the edge chunk sort 0.5 -> 15 ms, the
+    // H1 reduction starting at 26.6 ms); after k_par_init it fills the CUs the H1 workers leave.
+    // The wide edge codes (H2 keys only) move onto the branch too.  TDA_H2_LATE=0: the r04 fork.
+    const bool h2_late = h2_side && !test_env_is("TDA_H2_LATE", "0");
+    // A k_reduce_par worker fills a CU (two 256-VGPR waves per SIMD), so apparent<2> blocks
+    // dispatched before the H1 workers keep them off every CU they hold (torus2048_h2: the H1
+    // reduction 124 -> 154 ms); on a small grid the pass itself crawls (128 blocks: 30 -> 194 ms).
+    // The branch starts after a short device-side delay instead, so the H1 workers are resident
+    // first and apparent<2> fills the CUs they leave as the column queue drains.
+    const uint64_t h2_late_grid = test_env("TDA_H2_LATE_GRID") ? strtoull(test_env("TDA_H2_LATE_GRID"), nullptr, 10) : 0;
+    const uint32_t h2_late_delay_us = test_env("TDA_H2_LATE_DELAY") ? (uint32_t)atoi(test_env("TDA_H2_LATE_DELAY")) : 50;
     auto launch_h2_columns = [&]() -> int {  // apparent<2> + their sort on the third stream
         if (int rc = tm3.begin()) return rc;
-        launch_apparent(2, w.stream3);
+        launch_apparent(2, w.stream3, h2_late ? h2_late_grid : 0);
         HIPC(hipGetLastError());
         if (int rc = tm3.mark("k_apparent<2>")) return rc;
         // beside k_reduce_par<1> (one 72-KB workgroup per CU) the sort's LDS chunk must fit next to
@@ -1385,6 +1398,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 HIPC(hipGetLastError());
                 MARK("k_sort_resid<1>");
             }
+        } else if (h2_side && h2_late) {
+            // (fork after k_par_init below)
+            launch_sort(1, 1, s);
+            HIPC(hipGetLastError());
+            MARK("k_sort_resid<1>");
         } else if (h2_side) {
             // parallel H1 and H2: the H2 columns' apparent pass and sort run on
             // the third stream beside the H1 reduction (k_reduce_par<2> joins
@@ -1447,7 +1465,8 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             gb.dcode = (const uint32_t*)(B + p.o_dcode);
             gb.dsort = (const uint64_t*)(B + p.o_dsort);
             gb.ecap = p.ecap;
-            if (p.wide) {  // edge codes of the wide H2 keys (thresholds are known: after the H0 join)
+            // edge codes of the wide H2 keys (thresholds are known: after the H0 join)
+            auto launch_edge_codes = [&](hipStream_t es, StageTimer& et) -> int {
                 // the sorted lengths end in dsort: with an odd number of merge passes the keys start in dtmp
                 const uint64_t E = binom((uint64_t)n, 2), CH = 1ull << kEdgeSortLog2;
                 int passes = 0;
@@ -1455,21 +1474,23 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 uint64_t* ka = (uint64_t*)(B + ((passes & 1) ? p.o_dtmp : p.o_dsort));
                 uint64_t* kb = (uint64_t*)(B + ((passes & 1) ? p.o_dsort : p.o_dtmp));
                 const unsigned gk = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
-                hipLaunchKernelGGL(k_edge_keys, dim3(gk, L), dim3(256), 0, s, dist, n, ka, p.ecap);
-                hipLaunchKernelGGL(k_edge_chunks, dim3((unsigned)((E + CH - 1) / CH), L), dim3(1024), kEdgeSortLds, s, ka, E, p.ecap);
+                hipLaunchKernelGGL(k_edge_keys, dim3(gk, L), dim3(256), 0, es, dist, n, ka, p.ecap);
+                hipLaunchKernelGGL(k_edge_chunks, dim3((unsigned)((E + CH - 1) / CH), L), dim3(1024), kEdgeSortLds, es, ka, E, p.ecap);
                 for (uint64_t w = CH; w < E; w <<= 1) {
-                    hipLaunchKernelGGL(k_edge_merge, dim3((unsigned)((E + kMergeSeg - 1) / kMergeSeg), L), dim3(256), 0, s, ka, kb, E,
+                    hipLaunchKernelGGL(k_edge_merge, dim3((unsigned)((E + kMergeSeg - 1) / kMergeSeg), L), dim3(256), 0, es, ka, kb, E,
                                        p.ecap, w);
                     std::swap(ka, kb);
                 }
                 HIPC(hipGetLastError());
-                MARK("k_edge_sort");
+                if (int rc = et.mark("k_edge_sort")) return rc;
                 const unsigned gx = (unsigned)std::min<uint64_t>(1024, ((uint64_t)n * n + 255) / 256);
-                hipLaunchKernelGGL(k_edge_codes, dim3(gx, L), dim3(256), 0, s, dist, n, stats, (const uint64_t*)(B + p.o_dsort), p.ecap,
+                hipLaunchKernelGGL(k_edge_codes, dim3(gx, L), dim3(256), 0, es, dist, n, stats, (const uint64_t*)(B + p.o_dsort), p.ecap,
                                    (uint32_t*)(B + p.o_dcode));
                 HIPC(hipGetLastError());
-                MARK("k_edge_codes");
-            }
+                return et.mark("k_edge_codes");
+            };
+            if (p.wide && !h2_late)
+                if (int rc = launch_edge_codes(s, tm)) return rc;
             int start_dim = 1;
             if (p.par) {
                 ParBufs pb;
@@ -1494,6 +1515,16 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);
                 HIPC(hipGetLastError());
                 MARK("k_par_init");
+                if (h2_late) {  // the H2 branch (and the wide edge codes) beside the H1 reduction
+                    HIPC(hipEventRecord(w.evs, s));
+                    HIPC(hipStreamWaitEvent(w.stream3, w.evs, 0));
+                    if (h2_late_delay_us && !serial_stages)
+                        hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, w.stream3, h2_late_delay_us);
+                    if (int rc = launch_h2_columns()) return rc;
+                    if (p.wide)
+                        if (int rc = launch_edge_codes(w.stream3, tm3)) return rc;
+                    HIPC(hipEventRecord(w.evp, w.stream3));
+                }
                 // persistent workers (one 71-KB-LDS workgroup per CU by default); the surplus exits at once
                 const unsigned par_grid = par_grid_size();
                 const uint32_t* no_clr = nullptr;

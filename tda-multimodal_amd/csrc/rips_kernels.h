@@ -1661,6 +1661,13 @@ __global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict_
 struct PartList {
     const void* p[TDA_MAX_PARTS];
 };
+// one wave that returns after `us` microseconds (s_memrealtime: 100 MHz), sleeping between
+// reads: orders a side stream's next launch after work the main stream dispatches meanwhile
+__global__ __launch_bounds__(64) void k_delay(uint32_t us) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), ticks = (uint64_t)us * 100;
+    for (uint32_t i = 0; i < (1u << 20) && __builtin_amdgcn_s_memrealtime() - t0 < ticks; ++i) __builtin_amdgcn_s_sleep(8);  // capped
+}
+
 // end of a call with a sparse-cleared H2 pivot bitmap: zero the words k_apparent<2> listed
 // (a layer whose list overflowed leaves the bitmap dirty: the host memsets it before the next call)
 __global__ __launch_bounds__(256) void k_clear_words(const LayerStats* __restrict__ stats, const uint64_t* __restrict__ clr, uint64_t cap,

@@ -496,9 +496,24 @@ __device__ __forceinline__ void front_reset() {
 }
 
 // toggle one key (the lane's own); returns 1 if it filled an EMPTY slot
+#ifndef TDA_PAR_CASFIRST  // build-time A/B knob (tools/): probe with the inserting CAS itself (one LDS round trip per empty slot)
+// (r05: torus1024 32.5 -> 31.8 ms, grid144 5.38 -> 5.31 ms; torus2048_h2 177 -> 179 ms.  Dropped: the
+// second wave of each SIMD at a higher issue priority, s_setprio 1 / 3: torus1024 32.1 -> 33.5-33.8 ms)
+#define TDA_PAR_CASFIRST 1
+#endif
 __device__ __forceinline__ uint32_t tab_toggle(uint64_t key) {
     uint32_t h = tab_hash(key);
     for (uint32_t it = 0; it < 4 * kFrontLog; ++it) {
+#if TDA_PAR_CASFIRST
+        // the CAS that inserts into an EMPTY slot also reads the slot: a present key
+        // comes back as itself (remove it), a tombstone or another key moves the probe on
+        const uint64_t v = atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)key);
+        if (v == kTabEmpty) return 1;
+        if (v == key) {
+            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)key, (unsigned long long)kTabTomb) == key) return 0;
+            continue;  // another toggle of this key won: look at the slot again
+        }
+#else
         const uint64_t v = PS.log[h];
         if (v == key) {
             if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)key, (unsigned long long)kTabTomb) == key) return 0;
@@ -508,6 +523,7 @@ __device__ __forceinline__ uint32_t tab_toggle(uint64_t key) {
             if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)key) == kTabEmpty) return 1;
             continue;
         }
+#endif
         h = (h + 1) & (kFrontLog - 1);
     }
     PS.err = 13;  // table full (front_room keeps it below kTabMax)
