@@ -984,6 +984,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     auto enqueue = [&]() -> int {
     HIPC(rec_t(w.ev0));
     if (int rc = tm.begin()) return rc;
+    MARK("event_gap");  // an empty interval: what two back-to-back events measure with no kernel between (bench.py subtracts it)
     HIPC(hipMemsetAsync(B + p.memset_lo, 0, p.memset_hi - p.memset_lo, s));
     MARK("memset");
 
@@ -1213,16 +1214,18 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 hipLaunchKernelGGL((k_apparent_small<1>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh);
             else
                 hipLaunchKernelGGL((k_apparent_small<2>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh);
-        } else if (d == 1) {
-            if (dl)
-                hipLaunchKernelGGL((k_apparent<1, true>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
-            else
-                hipLaunchKernelGGL((k_apparent<1, false>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
         } else {
-            if (dl)
-                hipLaunchKernelGGL((k_apparent<2, true>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
+            // L a multiple of 8: a 1-D grid whose blocks take their layers XCD by XCD (app_block)
+            const int xl = (L % 8 == 0 && !test_env_is("TDA_APP_XCD", "0")) ? L : 0;
+            const dim3 ag = xl ? dim3(gx * (unsigned)L) : dim3(gx, L);
+            if (d == 1 && dl)
+                hipLaunchKernelGGL((k_apparent<1, true>), ag, dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh, xl);
+            else if (d == 1)
+                hipLaunchKernelGGL((k_apparent<1, false>), ag, dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh, xl);
+            else if (dl)
+                hipLaunchKernelGGL((k_apparent<2, true>), ag, dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh, xl);
             else
-                hipLaunchKernelGGL((k_apparent<2, false>), dim3(gx, L), dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh);
+                hipLaunchKernelGGL((k_apparent<2, false>), ag, dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh, xl);
         }
     };
     Reduce2Bufs rb;
@@ -1510,6 +1513,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 pb.rq_cap = p.rq_cap;
                 pb.step_limit = step_limit();
                 pb.capf = capf;
+                pb.xq = (L % 8 == 0 && !test_env_is("TDA_PAR_XQ", "0")) ? 1 : 0;
                 pb.dbg = p.o_pdbg ? (uint64_t*)(B + p.o_pdbg) : nullptr;  // profile builds only
                 HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                 hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);

@@ -1363,11 +1363,29 @@ __global__ __launch_bounds__(64) void k_h0_wave(const float* __restrict__ dist, 
 // reduces to: every facet t\{u} with u > v has diam < diam(s).  Apparent
 // pairs are persistence pairs (zero persistence: never emitted), columns with
 // an empty coboundary are essential (emitted here), the rest go to k_reduce.
+// (layer, block within the layer, blocks per layer) of an apparent-pass block.  A 2-D grid is
+// (blocks per layer, L).  A 1-D grid of L x G blocks (L a multiple of 8, rips.hip) is XCD-aware:
+// blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, for speed only), so block b
+// takes layer (b mod 8) + 8 j and every XCD's L2 serves its own layers' distance matrices instead
+// of a slice of all of them (torus1024x32: 11.4 GB of HBM reads per 32-layer launch, 356 MB per
+// 4-MB matrix)
+struct AppBlock {
+    int l;
+    uint32_t bx, nbx;
+};
+__device__ __forceinline__ AppBlock app_block(int xcd_layers) {
+    if (xcd_layers <= 0) return {(int)blockIdx.y, blockIdx.x, gridDim.x};
+    const uint32_t G = gridDim.x / (uint32_t)xcd_layers, b = blockIdx.x, r = b >> 3;
+    return {(int)((b & 7u) + 8u * (r / G)), r % G, G};
+}
+
 template <int DIM, bool DLDS>
 __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
-                                                  DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh) {
+                                                  DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh,
+                                                  int xcd_layers) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int l = blockIdx.y;
+    const AppBlock ab = app_block(xcd_layers);  // 0: 2-D grid (blocks per layer, L)
+    const int l = ab.l;
     const float* Dg = dist + (size_t)l * n * n;
     const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
     float* Dsh = (float*)(smem + 16);
@@ -1381,9 +1399,9 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
     const uint32_t* cleared = b.cleared ? b.cleared + (size_t)l * b.cleared_words : nullptr;
     uint32_t* piv = b.pivbits + (size_t)l * b.piv_words;
     uint64_t* resid = b.resid + (size_t)l * b.rcap;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t stride = (uint64_t)ab.nbx * blockDim.x;
     uint64_t acc_cs = 0, acc_app = 0, acc_cols = 0;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < b.ncand; base += stride) {
+    for (uint64_t base = (uint64_t)ab.bx * blockDim.x; base < b.ncand; base += stride) {
         const uint64_t s = base + threadIdx.x;
         int kind = 0;  // 0 skip, 1 apparent, 2 residual (incl. empty coboundary)
         uint64_t tixv = 0;
