@@ -168,6 +168,14 @@ __device__ __forceinline__ uint32_t par_bucket(uint64_t key, uint64_t last) {
     const uint64_t x = key ^ last;
     return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u;
 }
+// smallest key of bucket b >= 1 relative to `last`: bits above b - 1 as last, bit b - 1 set.
+// (r05: two levels per bit -- 1 + 2 p + the key's bit p - 1 -- to halve the keys a refill moves,
+// is wrong as a radix heap: a refill of a sub-level-0 bucket re-references the column, and its
+// sibling bucket (same p, sub-level 1) then no longer holds keys of its own level; it failed the
+// torus256 H1 parity test.  It would need the two siblings refilled together.)
+__device__ __forceinline__ uint64_t par_bucket_floor(uint64_t last, uint32_t b) {
+    return b >= 64u ? (1ull << 63) : (((last >> b) << b) | (1ull << (b - 1)));
+}
 __device__ __forceinline__ uint32_t chunk_of(uint32_t s) { return 31u - (uint32_t)__builtin_clz((s >> 8) + 1u); }
 __host__ __device__ constexpr uint32_t chunk_start(uint32_t k) { return ((1u << k) - 1u) << 8; }
 
@@ -907,8 +915,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     // the bucket's keys fall in levels < b and the higher buckets keep theirs.  (The exact
     // minimum puts at least one key in the front; with the bound a refill may place none and
     // the next one refines the lower buckets.)
-    const uint64_t lastv = PS.last;
-    const uint64_t nl = b >= 64 ? (1ull << 63) : (((lastv >> b) << b) | (1ull << (b - 1)));
+    const uint64_t nl = par_bucket_floor(PS.last, (uint32_t)b);
     if (inreg) {
 #pragma unroll
         for (int h = 0; h < kParRefill; ++h) vm[h] = bucket_batch(P, (uint32_t)b, h * kPass, c, x[h]);
