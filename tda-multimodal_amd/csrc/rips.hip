@@ -1513,7 +1513,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 pb.rq_cap = p.rq_cap;
                 pb.step_limit = step_limit();
                 pb.capf = capf;
-                pb.xq = (L % 8 == 0 && !test_env_is("TDA_PAR_XQ", "0")) ? 1 : 0;
                 pb.dbg = p.o_pdbg ? (uint64_t*)(B + p.o_pdbg) : nullptr;  // profile builds only
                 HIPC(hipMemsetAsync(pb.rq, 0, p.rq_cap * 8, s));
                 hipLaunchKernelGGL(k_par_init, dim3(64, L), dim3(256), 0, s, stats, L, p.rcap[1], pb, 1);

@@ -109,7 +109,6 @@ struct ParCtl {  // zeroed by k_par_init
     unsigned long long total;    // items over all layers
     unsigned long long evictions;
     unsigned long long pad[6];
-    unsigned long long gnext[8], gtot[8];  // ParBufs::xq: fresh items of layer group g (layers = g mod 8) taken / in all
 };
 
 struct ParBufs {
@@ -129,7 +128,6 @@ struct ParBufs {
     uint64_t rq_cap;
     uint64_t step_limit;
     float capf;           // column caps: keys above birth + capf * thresh are dropped (0 = off); see k_reduce_par
-    int xq;               // L a multiple of 8: fresh columns by XCD layer group (workgroup b takes layers = b mod 8 first)
     uint64_t* dbg;        // -DTDA_PROFILE: [kParDbgCap][4] long-column timeline (layer << 40 | column, start, end, steps)
 };
 constexpr uint32_t kParDbgCap = 4096;
@@ -1440,28 +1438,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                     got = v;
                     break;
                 }
-                if (P.xq) {
-                    // Workgroups b and b + 8 share an XCD (blocks are dealt round-robin over the 8
-                    // XCDs; for speed only): workgroup b takes the columns of layers = b (mod 8) first,
-                    // layer by layer in column order, then the other groups' -- so an XCD's L2 serves
-                    // the distance rows of ~one layer at a time instead of all of them
-                    const uint32_t g0 = blockIdx.x & 7u;
-                    for (uint32_t k = 0; k < 8u && got == kEmpty64; ++k) {
-                        const uint32_t g = (g0 + k) & 7u;
-                        const uint64_t gt = ald(&P.ctl->gtot[g]);
-                        if (ald(&P.ctl->gnext[g]) >= gt) continue;
-                        uint64_t r = aadd(&P.ctl->gnext[g], 1);
-                        if (r >= gt) continue;
-                        for (int lq = (int)g; lq < L; lq += 8) {  // the group's r-th column
-                            const uint64_t b0 = ld_glb(P.item_base, lq), c = ld_glb(P.item_base, lq + 1) - b0;
-                            if (r < c) {
-                                got = (b0 + r) << 32;
-                                break;
-                            }
-                            r -= c;
-                        }
-                    }
-                } else if (ald(&P.ctl->next) < total) {
+                if (ald(&P.ctl->next) < total) {
                     const uint64_t c = aadd(&P.ctl->next, 1);
                     if (c < total) got = c << 32;
                 }
@@ -1853,7 +1830,6 @@ __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats
         for (int q = 0; q < (int)(sizeof(ParCtl) / 8); ++q) c[q] = 0;
         P.ctl->total = s;
         P.ctl->pad[0] = ~0ull;  // -DTDA_PROFILE: earliest workgroup start (atomicMin)
-        for (int q = 0; q < L; ++q) P.ctl->gtot[q & 7] += P.item_base[q + 1] - P.item_base[q];
     }
 }
 
