@@ -199,7 +199,7 @@ constexpr uint64_t kTabEmpty = kEmpty64;
 constexpr uint64_t kTabTomb = kEmpty64 - 1;
 constexpr uint32_t kTabMax = kFrontLog * 3 / 4;  // filled slots allowed before a rebuild
 constexpr uint32_t kTabPer = kFrontLog / kParT;  // slots per thread in scans
-constexpr uint32_t kStageW = 64 * 4;            // per-wave staging of the keys one toggle pass hands to the table
+constexpr uint32_t kStageW = 64 * (kParRegs > 4 ? kParRegs : 4);           // per-wave staging of the keys one toggle pass hands to the table
 #endif
 
 struct ParLds {
