@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TDA_RIPS_ABI_VERSION 7
+#define TDA_RIPS_ABI_VERSION 8
 
 /* error codes */
 #define TDA_OK 0
@@ -159,6 +159,13 @@ typedef struct tda_rips_result {
      * ripser.py hands back as dperm2all) when args.flags & TDA_FLAG_DIST64,
      * want_dist and float64 point clouds, else NULL */
     const double *dist64;
+    /* ABI >= 8: layers of this call re-run without column caps.  With the
+     * default threshold (enclosing radius) the parallel reducer stores only
+     * the keys of a column up to birth + 0.5 * thresh; a column whose pivot
+     * lies above that (a class living longer than half the radius) flags its
+     * layer, and the library re-runs that layer alone, uncapped, and splices
+     * it in.  Results are exact either way; this only reports the cost. */
+    int64_t n_cap_reruns;
 } tda_rips_result;
 
 #define TDA_FLAG_STAGE_TIMES 1

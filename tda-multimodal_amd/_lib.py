@@ -81,6 +81,7 @@ class RipsResult(ctypes.Structure):
         ("blob_bytes", ctypes.c_int64),
         ("n_pairs", ctypes.c_int64),
         ("dist64", ctypes.POINTER(ctypes.c_double)),
+        ("n_cap_reruns", ctypes.c_int64),  # ABI 8
     ]
 
 

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -478,7 +479,6 @@ struct Workspace {
         bool force_global, force_big;
         int no_par;
         int scale;
-        bool no_cap;
     };
     std::vector<Retry> retry;
     std::mutex mu;
@@ -780,10 +780,137 @@ std::string err_flags(int e) {
 }
 
 // ------------------------------------------------------------------ pipeline
+// (re)point the public result at its one-allocation blob (tda_rips.h layout)
+void point_result(ResultImpl& R, size_t total) {
+    tda_rips_result& o = R.pub;
+    const size_t S = (size_t)o.L * (o.maxdim + 1);
+    const size_t o_ne = 7 * S, o_idx = o_ne + o.L, o_thr = o_idx + 2 * total, o_bd = o_thr + (o.L + 1) / 2;
+    int64_t* m = (int64_t*)R.blob.data();
+    o.count = m;
+    o.offset = m + S;
+    o.checksum = (const uint64_t*)(m + 2 * S);
+    o.n_all_pairs = m + 3 * S;
+    o.n_columns = m + 4 * S;
+    o.n_residual = m + 5 * S;
+    o.n_adds = m + 6 * S;
+    o.num_edges = (const int64_t*)(R.blob.data() + o_ne);
+    o.birth_idx = (const int64_t*)(R.blob.data() + o_idx);
+    o.death_idx = o.birth_idx + total;
+    o.thresh = (const float*)(R.blob.data() + o_thr);
+    o.birth = (const float*)(R.blob.data() + o_bd);
+    o.death = o.birth + total;
+    o.blob = R.blob.data();
+    o.blob_bytes = (int64_t)(R.blob.size() * 8);
+    o.n_pairs = (int64_t)total;
+}
+
+// Layers ls[i] of R replaced by the one-layer results subs[i] (same N and maxdim): every
+// per-layer block of the blob is rebuilt in layer order.  Distances, silhouettes and TwoNN
+// stay R's (they do not depend on the reduction).
+void splice_layers(ResultImpl& R, const std::vector<int>& ls, const std::vector<tda_rips_result*>& subs) {
+    const tda_rips_result& o = R.pub;
+    const int L = (int)o.L, nd = (int)o.maxdim + 1;
+    std::vector<const tda_rips_result*> src((size_t)L, &o);
+    std::vector<int> sl((size_t)L);
+    for (int l = 0; l < L; ++l) sl[l] = l;
+    for (size_t i = 0; i < ls.size(); ++i) src[ls[i]] = subs[i], sl[ls[i]] = 0;
+    size_t total = 0;
+    for (int l = 0; l < L; ++l)
+        for (int d = 0; d < nd; ++d) total += (size_t)src[l]->count[sl[l] * nd + d];
+    const size_t S = (size_t)L * nd;
+    const size_t o_ne = 7 * S, o_idx = o_ne + L, o_thr = o_idx + 2 * total, o_bd = o_thr + (L + 1) / 2;
+    std::vector<uint64_t> blob(o_bd + total, 0);
+    int64_t* m = (int64_t*)blob.data();
+    float* thr = (float*)(blob.data() + o_thr);
+    int64_t* ne = (int64_t*)(blob.data() + o_ne);
+    int64_t* idx = (int64_t*)(blob.data() + o_idx);
+    float* bd = (float*)(blob.data() + o_bd);
+    size_t e = 0;
+    for (int l = 0; l < L; ++l) {
+        const tda_rips_result& q = *src[l];
+        const int k = sl[l];
+        thr[l] = q.thresh[k];
+        ne[l] = q.num_edges[k];
+        for (int d = 0; d < nd; ++d) {
+            const size_t a = (size_t)l * nd + d, b = (size_t)k * nd + d;
+            const int64_t c = q.count[b];
+            m[a] = c;
+            m[S + a] = (int64_t)e;
+            ((uint64_t*)m)[2 * S + a] = q.checksum[b];
+            m[3 * S + a] = q.n_all_pairs[b];
+            m[4 * S + a] = q.n_columns[b];
+            m[5 * S + a] = q.n_residual[b];
+            m[6 * S + a] = q.n_adds[b];
+            const int64_t f = q.offset[b];
+            for (int64_t i = 0; i < c; ++i, ++e) {
+                bd[e] = q.birth[f + i];
+                bd[total + e] = q.death[f + i];
+                idx[e] = q.birth_idx[f + i];
+                idx[total + e] = q.death_idx[f + i];
+            }
+        }
+    }
+    R.blob.swap(blob);
+    point_result(R, total);
+}
+
+int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
+                 bool force_global, int scale, bool force_big, int no_par, bool no_cap);
+
+// Column caps missed on some layers (ERR_CAP_MISS: a column's pivot lies above its cap -- a
+// class that lives longer than capf * thresh, e.g. the one loop of a circle): each such layer is
+// re-run ALONE without caps and spliced into the batch's result; the other layers keep their
+// capped (exact) reductions.  A one-layer call simply re-runs without caps.
+int rerun_cap_missed(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out, ResultImpl* R,
+                     const std::vector<int>& ls, bool force_global, int scale, bool force_big, int no_par) {
+    std::unique_ptr<ResultImpl> own(R);
+    if (getenv("TDA_DEBUG")) fprintf(stderr, "[tda] column cap missed on %zu of %lld layers: re-run without caps\n", ls.size(), (long long)a.L);
+    if (a.L == 1 || input_kind == 2) {
+        const double dms = R->pub.device_ms;
+        if (int rc = run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, no_par, true)) return rc;
+        (*out)->n_cap_reruns = a.L;
+        (*out)->device_ms += dms;
+        return 0;
+    }
+    const size_t esz = a.dtype == TDA_F64 ? 8 : 4;
+    const size_t lb = (size_t)a.N * (input_kind == 1 ? (size_t)a.N : (size_t)a.D) * esz;  // bytes per layer
+    const int64_t per = a.n_parts > 0 ? a.L / a.n_parts : a.L;
+    std::vector<tda_rips_result*> subs;
+    struct Free {
+        std::vector<tda_rips_result*>& v;
+        ~Free() {
+            for (auto* r : v) delete reinterpret_cast<ResultImpl*>(r);
+        }
+    } free_subs{subs};
+    double dms = R->pub.device_ms;
+    for (int l : ls) {
+        tda_rips_args b = a;
+        const char* base = (const char*)(a.n_parts > 0 ? a.x_parts[l / per] : host_or_dev);
+        b.x = base + (size_t)(a.n_parts > 0 ? l % per : l) * lb;
+        b.L = 1;
+        b.n_parts = 0;
+        b.x_parts = nullptr;
+        b.flags = (a.flags | TDA_FLAG_INPUT_READY) & ~TDA_FLAG_DIST64;  // the batch's call ordered and read it already
+        b.want_dist = 0;
+        b.labels = nullptr;
+        b.n_label_sets = 0;
+        b.want_twonn = 0;
+        tda_rips_result* sub = nullptr;
+        if (int rc = run_pipeline(b, input_kind, b.x, &sub, force_global, scale, force_big, no_par, true)) return rc;
+        subs.push_back(sub);
+        dms += sub->device_ms;
+    }
+    splice_layers(*R, ls, subs);
+    R->pub.n_cap_reruns = (int64_t)ls.size();
+    R->pub.device_ms = dms;
+    *out = &own.release()->pub;
+    return 0;
+}
+
 // input_kind: 0 = points (dtype), 1 = square distance (dtype), 2 = condensed f32
 // no_cap: k_reduce_par without column caps (a capped column ran empty below its cap: code 81)
 int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev, tda_rips_result** out,
-                 bool force_global = false, int scale = 0, bool force_big = false, int no_par = 0, bool no_cap = false) {
+                 bool force_global, int scale, bool force_big, int no_par, bool no_cap) {
     const auto h_entry = std::chrono::steady_clock::now();
     Plan p;
     p.L = a.L;
@@ -955,7 +1082,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     gk.no_cap = no_cap;
     // column caps only with ripser's default threshold (the enclosing radius: no essential
     // H1 / H2 class); a finite user threshold can leave classes essential (k_reduce_par)
-    const float capf = (no_cap || !(std::isinf(a.thresh) || a.thresh == 3.402823466e+38f)) ? 0.0f : par_capf();
+    // caps also off when H2 runs on the serial k_reduce_big after a parallel H1 (TDA_PAR2=0, or an H2
+    // abort): that kernel reads every layer's H1 pivots, so no layer's H1 may be left unfinished
+    const bool h2_serial = p.par && p.maxdim >= 2 && !p.par2;
+    const float capf = (no_cap || h2_serial || !(std::isinf(a.thresh) || a.thresh == 3.402823466e+38f)) ? 0.0f : par_capf();
     gk.capf = capf;
     gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0) |
                  (p.wide ? 1 << 10 : 0) | (p.want64 ? 1 << 11 : 0);
@@ -1650,11 +1780,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     const auto h2 = hclk::now();
 
     int errs = 0;
-    for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
+    for (int l = 0; l < L; ++l) errs |= w.hstats[l].err & ~ERR_CAP_MISS;
     if (p.piv2_sparse) {  // clean again unless a layer's word list overflowed
         bool over = false;
         for (int l = 0; l < L; ++l) over |= (uint64_t)w.hstats[l].n_clr2 > p.clr_cap;
-        w.piv2_dirty = over;
+        // only k_apparent<2> lists the words it sets: when H2 was reduced by k_reduce_big<2>
+        // (TDA_PAR2=0, or no_par >= 1 after a k_reduce_par abort) that kernel also set residual-pivot
+        // bits nobody listed, so the next call must start from a full memset
+        w.piv2_dirty = over || !p.par2;
     }
     if (errs == ERR_OUT_CAP) {
         size_t need = 0;
@@ -1671,7 +1804,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         HIPC(hipGetLastError());
         HIPC(hipStreamSynchronize(s));
         errs = 0;
-        for (int l = 0; l < L; ++l) errs |= w.hstats[l].err;
+        for (int l = 0; l < L; ++l) errs |= w.hstats[l].err & ~ERR_CAP_MISS;
     }
     if (errs && getenv("TDA_DEBUG"))
         fprintf(stderr, "[tda] N=%d L=%d errs=%s force_global=%d scale=%d\n", n, L, err_flags(errs).c_str(), (int)force_global, scale);
@@ -1688,10 +1821,6 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             fprintf(stderr, "[tda] k_reduce_par aborted: code %llu, evictions %llu, records %llu, pools %llu / %llu keys\n", c.err,
                     c.evictions, c.rec_used, c.rpool_used, c.bpool_used);
         const unsigned code = (unsigned)(c.err & 0xFFFF);
-        if (code == 81 && !no_cap) {  // a capped column ran empty below its cap: the same call without caps
-            guard.unlock();
-            return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale, force_big, no_par, true);
-        }
         const bool capacity = code == 21 || code == 22 || code == 41 || code == 53;  // pools / requeue slots
         if (capacity && scale < 2) {  // the same parallel reduction with larger pools
             guard.unlock();
@@ -1846,7 +1975,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
 #endif
 
-    if (force_global || scale || force_big || no_par || no_cap) {  // remember what this shape needed
+    // remember what this shape needed (capacity / reducer retries; column caps are not
+    // remembered: a cap miss re-runs only its own layers, below, and every call starts capped)
+    if (force_global || scale || force_big || no_par) {
         bool seen = false;
         for (auto& m : w.retry)
             if (m.N == p.N && m.maxdim == p.maxdim && m.input_kind == input_kind) {
@@ -1854,11 +1985,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 m.force_big = m.force_big || force_big;
                 m.no_par = std::max(m.no_par, no_par);
                 m.scale = std::max(m.scale, scale);
-                m.no_cap = m.no_cap || no_cap;
                 seen = true;
             }
-        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale, no_cap});
+        if (!seen) w.retry.push_back({p.N, p.maxdim, input_kind, force_global, force_big, no_par, scale});
     }
+    std::vector<int> cap_miss;  // layers whose capped reduction missed (ERR_CAP_MISS): re-run below without caps
+    for (int l = 0; l < L; ++l)
+        if (w.hstats[l].err & ERR_CAP_MISS) cap_miss.push_back(l);
 
     // ---- result
     auto* R = new ResultImpl();
@@ -2002,13 +2135,18 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     }
     o.stage_name = R->stage_name.data();
     o.stage_ms = R->stage_ms.data();
+    o.n_cap_reruns = 0;
+    if (!cap_miss.empty()) {
+        guard.unlock();
+        return rerun_cap_missed(a, input_kind, host_or_dev, out, R, cap_miss, force_global, scale, force_big, no_par);
+    }
     *out = &R->pub;
     return 0;
 }
 
 // entry: start from the configuration an earlier call of this shape ended on
 int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_result** out) {
-    bool fg = false, fb = false, nc = false;
+    bool fg = false, fb = false;
     int np = 0;
     int sc = 0;
     // not when a test forces a reducer (the memo would override what it asks for)
@@ -2022,10 +2160,9 @@ int run_entry(const tda_rips_args& a, int input_kind, const void* src, tda_rips_
                 fb = m.force_big;
                 np = m.no_par;
                 sc = m.scale;
-                nc = m.no_cap;
             }
     }
-    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np, nc);
+    return run_pipeline(a, input_kind, src, out, fg, sc, fb, np, false);
 }
 
 int validate(const tda_rips_args* a) {

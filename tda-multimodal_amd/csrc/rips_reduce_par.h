@@ -52,39 +52,25 @@ namespace tda {
 #endif
 constexpr int kParT = TDA_PAR_T;
 constexpr int kParW = kParT / 64;
-#ifndef TDA_PAR_LOG  // build-time A/B knobs (tools/): front capacity and refill target
-#define TDA_PAR_LOG 4096
-#endif
-#ifndef TDA_PAR_FILL
+// Sizes (build-time constants; tools/build_variants.py times other values).  Variants that
+// were measured and dropped (the r02-r04 key log + hashed index front, deferred back-key
+// appends, exact-minimum refills, sc1 bucket stores, read-then-CAS probing, one-pass block
+// minima) are described in DESIGN.md §6.8 and no longer in the source.
+#ifndef TDA_PAR_FILL  // refill / spill target (front keys)
 #define TDA_PAR_FILL 768
 #endif
-#ifndef TDA_PAR_FRONT  // build-time A/B knob (tools/): 1 = key log + hashed index (r02-r04), 2 = one open-addressing toggle table
-#define TDA_PAR_FRONT 2
-#endif
-#if TDA_PAR_FRONT == 2
-#ifndef TDA_PAR_TAB  // build-time A/B knob (tools/): toggle-table slots
+#ifndef TDA_PAR_TAB  // toggle-table slots
 #define TDA_PAR_TAB 4096
 #endif
-#undef TDA_PAR_LOG
-#define TDA_PAR_LOG TDA_PAR_TAB
-#endif
-constexpr uint32_t kFrontLog = TDA_PAR_LOG;          // front log entries (live + cancelled) / toggle-table slots
-#ifndef TDA_PAR_IDX  // build-time A/B knob (tools/): front index slots per log entry
-#define TDA_PAR_IDX 2
-#endif
-constexpr uint32_t kFrontIdx = TDA_PAR_LOG * TDA_PAR_IDX;  // front index slots (kFrontIdx / 8 buckets x 8)
-constexpr uint32_t kFrontLive = TDA_PAR_LOG * 7 / 16;  // live front keys that trigger a spill (1792 at 4096)
+constexpr uint32_t kFrontLog = TDA_PAR_TAB;          // toggle-table slots
+constexpr uint32_t kFrontLive = kFrontLog * 7 / 16;  // live front keys that trigger a spill (1792 at 4096)
 constexpr uint32_t kFrontFill = TDA_PAR_FILL;        // refill / spill target
 constexpr int kParChunks = 22;         // chunk k of an HBM bucket holds 256 << k keys
 constexpr int kParRegs = 2048 / kParT;  // keys per thread per pass of refills and record adds (2048 per pass)
-#ifndef TDA_PAR_REFILL  // build-time A/B knob (tools/): refill passes kept in registers
+#ifndef TDA_PAR_REFILL  // refill passes kept in registers
 #define TDA_PAR_REFILL 2
 #endif
 constexpr int kParRefill = TDA_PAR_REFILL;          // a refill keeps up to kParRefill passes (4096 keys) in registers
-#ifndef TDA_PAR_NLB  // build-time A/B knob (tools/): refills relative to the bucket's lower bound instead of its minimum
-// (r05: torus1024 34.4 -> 32.6 ms, torus1024x32 78-81 -> 72.9 ms, grid144 5.44 -> 5.40 ms)
-#define TDA_PAR_NLB 1
-#endif
 constexpr int kParRV = 1024 / kParT;   // coboundary vertices per thread per round (1024 per round)
 // vertex of thread t in slot q of the coboundary round starting at v0.  (r05: the odd slots
 // mirrored -- wave w taking 64-vertex blocks w and 2 W - 1 - w, to spread the waves' unequal key
@@ -97,8 +83,13 @@ constexpr uint32_t kParSpin = 1u << 22;       // polls before a wait on another 
 
 // k_reduce_par aborted: the host re-runs the call with k_reduce_big (ERR_PAR:
 // the H1 launch aborted, both dimensions go serial; ERR_PAR2: the H2 launch
-// aborted, H1 stays parallel and H2 goes serial)
-enum : int32_t { ERR_PAR = 128, ERR_PAR2 = 256 };
+// aborted, H1 stays parallel and H2 goes serial).  ERR_CAP_MISS (per layer): a
+// capped column ran empty below its cap; the layer's remaining columns are
+// dropped and the host re-runs that layer alone without caps.
+enum : int32_t { ERR_PAR = 128, ERR_PAR2 = 256, ERR_CAP_MISS = 512 };
+__device__ __forceinline__ uint32_t layer_cap_missed(const LayerStats* st) {
+    return (uint32_t)__hip_atomic_load(&st->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (uint32_t)ERR_CAP_MISS;
+}
 
 struct ParCtl {  // zeroed by k_par_init
     unsigned long long next;     // next fresh item
@@ -190,8 +181,7 @@ __device__ __forceinline__ uint32_t tri_lo(int x, int y, int z, int f) {
 }
 
 // ------------------------------------------------------------------ LDS
-#if TDA_PAR_FRONT == 2
-// FRONT 2: `log` is an open-addressing table of kFrontLog slots holding the
+// The front: `log` is an open-addressing table of kFrontLog slots holding the
 // live front keys; kTabEmpty / kTabTomb (a removed key) are above every key
 // (keys < kDead), so the front minimum is the plain minimum of all slots.
 // fcnt counts the slots ever filled since the last rebuild (live + tombstones).
@@ -200,28 +190,24 @@ constexpr uint64_t kTabTomb = kEmpty64 - 1;
 constexpr uint32_t kTabMax = kFrontLog * 3 / 4;  // filled slots allowed before a rebuild
 constexpr uint32_t kTabPer = kFrontLog / kParT;  // slots per thread in scans
 constexpr uint32_t kStageW = 64 * (kParRegs > 4 ? kParRegs : 4);           // per-wave staging of the keys one toggle pass hands to the table
-#endif
 
 struct ParLds {
     uint64_t log[kFrontLog];
-#if TDA_PAR_FRONT == 2
     uint64_t stage[kParW][kStageW];
-#else
-    uint64_t idx[kFrontIdx];
-#endif
     uint32_t bcnt[kParLv];
     uint32_t cptr[kParLv][kParChunks];
     uint32_t hist[kParLv];
     uint64_t red[2][kParW];
-    uint64_t redm[3];  // TDA_PAR_MINV & 2: block minimum cells (triple-buffered LDS u64 atomic min)
+    uint64_t redm[3];  // block minimum cells (triple-buffered LDS u64 atomic min)
     uint32_t wsum[2][kParW];
     uint32_t anyf[2][kParW];
     uint64_t bc[8];
     uint64_t last;  // radix reference: a lower bound of every key of the column
-    uint32_t fcnt;  // front log length
+    uint32_t fcnt;  // front slots filled since the last rebuild
     uint32_t kf;    // front holds levels 0..kf
     int32_t err;
     uint32_t wide;  // wide H2 keys: the low 32 bits (index fingerprint) are not unique -> verify hits
+    uint32_t lfail; // the column's layer missed a column cap (ERR_CAP_MISS): drop its work
 };
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
@@ -266,10 +252,9 @@ __device__ __forceinline__ void lds_sync() {
     asm volatile("" ::: "memory");
 }
 
-#ifndef TDA_PAR_MINV  // build-time A/B knob (tools/): block minimum -- bit 0: wave minimum as two u32 passes; bit 1: cross-wave by an LDS atomic min
-// (r05, torus1024: 0 36.9 ms, 1 36.4, 2 35.4, 3 34.7; tools/ubench_min: 1.41 K -> 1.12 K cycles per minimum)
-#define TDA_PAR_MINV 3
-#endif
+// Block minimum: the wave minimum as two u32 passes, then the cross-wave step as an LDS atomic
+// min into a triple-buffered cell (r05, torus1024: 36.9 -> 34.7 ms against one u64 wave pass +
+// a per-wave LDS array; tools/ubench_min: 1.41 K -> 1.12 K cycles per minimum)
 __device__ __forceinline__ uint64_t wave_min_2p(uint64_t v) {  // u64 wave minimum: the hi words, then the lo words of the lanes that hold it
     const uint32_t h = wave_min_u32((uint32_t)(v >> 32));
     const uint32_t l = wave_min_u32((uint32_t)(v >> 32) == h ? (uint32_t)v : ~0u);
@@ -277,7 +262,7 @@ __device__ __forceinline__ uint64_t wave_min_2p(uint64_t v) {  // u64 wave minim
 }
 struct ParRed {  // double-buffered block reductions: one barrier each
     uint32_t par = 0;
-    uint32_t parm = 0;  // TDA_PAR_MINV & 2: the minimum cell of this reduction (mod 3)
+    uint32_t parm = 0;  // the minimum cell of this reduction (mod 3)
     // block-wide OR of p (HIP's OR-barrier builtin lowers to three barriers)
     __device__ __forceinline__ bool any(bool p) {
         const uint64_t m = __ballot(p);
@@ -290,26 +275,17 @@ struct ParRed {  // double-buffered block reductions: one barrier each
         return r != 0;
     }
     __device__ __forceinline__ uint64_t min(uint64_t v) {
-        v = (TDA_PAR_MINV & 1) ? wave_min_2p(v) : wave_min_u64(v);
-        if (TDA_PAR_MINV & 2) {
-            // cell parm was reset two reductions ago; the next one's cell was last read before the
-            // previous barrier, so it is reset here for the reduction after this one
-            const uint32_t c = parm, cn = c == 2 ? 0 : c + 1;
-            parm = cn;
-            if ((threadIdx.x & 63) == 0)
-                __hip_atomic_fetch_min((TDA_LDS unsigned long long*)&PS.redm[c], (unsigned long long)v, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (threadIdx.x == 0) PS.redm[cn] = kEmpty64;
-            lds_sync();
-            return PS.redm[c];
-        }
-        const uint32_t b = par++ & 1;
-        if ((threadIdx.x & 63) == 0) PS.red[b][threadIdx.x >> 6] = v;
+        v = wave_min_2p(v);
+        // cell parm was reset two reductions ago; the next one's cell was last read before the
+        // previous barrier, so it is reset here for the reduction after this one
+        const uint32_t c = parm, cn = c == 2 ? 0 : c + 1;
+        parm = cn;
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_min((TDA_LDS unsigned long long*)&PS.redm[c], (unsigned long long)v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (threadIdx.x == 0) PS.redm[cn] = kEmpty64;
         lds_sync();
-        uint64_t m = PS.red[b][0];
-#pragma unroll
-        for (int w = 1; w < kParW; ++w) m = PS.red[b][w] < m ? PS.red[b][w] : m;
-        return m;
+        return PS.redm[c];
     }
     __device__ __forceinline__ uint64_t sum(uint64_t v) {
         v = wave_sum_u64(v);
@@ -347,143 +323,7 @@ struct ParRed {  // double-buffered block reductions: one barrier each
 };
 
 // ------------------------------------------------------------------ front
-#if TDA_PAR_FRONT == 1
-// Index: 8-slot buckets of u64 entries fp << 32 | (log pos + 1), claimed by
-// CAS on the first empty slot (slots of a bucket fill in order and are only
-// cleared by a full reset), so a probe stops at the first empty slot.
-constexpr uint32_t kFrontBkts = kFrontIdx / 8;
-
-__device__ __forceinline__ void front_reset() {
-    for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
-    if (threadIdx.x == 0) PS.fcnt = 0;
-    __syncthreads();
-}
-
-// Toggle up to R keys per thread (bit r of vmask) into the front, with NO
-// workgroup barrier: every key first gets its own log entry (one LDS atomic
-// per wave), written dead; a key found in the index flips the found entry; a
-// new key makes its entry live and claims an index slot by CAS.  Keys may
-// repeat within the pass (bucket refills and records are raw multisets): a
-// copy that loses the CAS to the same key kills its own entry and flips the
-// winner's.  The index only ever points at fully written log entries (a
-// wave's LDS operations complete in order).  Callers put a barrier between
-// this and the next read of the front.  Precondition: fcnt + R * kParT <= kFrontLog.
-template <int R>
-__device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vmask) {
-    constexpr uint32_t bmask = kFrontBkts - 1;
-    const int ln = threadIdx.x & 63;
-    // log entries for every key of the pass
-    uint64_t m[R];
-    uint32_t wtot = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        m[r] = __ballot((vmask >> r) & 1u);
-        wtot += (uint32_t)__popcll(m[r]);
-    }
-    if (!wtot) return;
-    uint32_t base = 0;
-    if (ln == 0) base = atomicAdd(&PS.fcnt, wtot);
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);  // lane 0 is active: the whole wave runs this
-    uint32_t off = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t pos = base + off + lanes_below(m[r]);
-        off += (uint32_t)__popcll(m[r]);
-        if ((vmask >> r) & 1u) PS.log[pos < kFrontLog ? pos : kFrontLog - 1] = k[r] | kDead;
-    }
-    if (base + wtot > kFrontLog) {  // precondition violated (callers make room)
-        PS.err = 12;
-        return;
-    }
-    // the wave's keys now sit at log[base, base + wtot): lanes take them round
-    // robin, so every lane runs ceil(wtot / 64) probe chains whatever the
-    // spread of front keys over the lanes (a wave's LDS operations complete in
-    // order, so the entries written above are visible to every lane)
-    for (uint32_t pos = base + (uint32_t)ln; pos < base + wtot; pos += 64) {
-        const uint64_t kk = PS.log[pos] & ~kDead;
-        const uint32_t fp = (uint32_t)kk;
-        const uint64_t mine = ((uint64_t)fp << 32) | (pos + 1);
-        uint32_t bk = mix32(fp) & bmask;
-        for (uint32_t it = 0; it < 8 * kFrontBkts; ++it) {
-            const uint32_t bo = bk * 8;
-            // the whole bucket in four independent 16-B reads (one LDS round trip)
-            const u64x2 q0 = *(const TDA_LDS u64x2*)&PS.idx[bo], q1 = *(const TDA_LDS u64x2*)&PS.idx[bo + 2];
-            const u64x2 q2 = *(const TDA_LDS u64x2*)&PS.idx[bo + 4], q3 = *(const TDA_LDS u64x2*)&PS.idx[bo + 6];
-            const uint64_t ev[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
-            int found = -1, empty = -1;
-            uint64_t fe = 0;
-#pragma unroll
-            for (int u = 7; u >= 0; --u) {  // first empty / first match, branch-free selects
-                if (ev[u] == 0) empty = u;
-                if (ev[u] != 0 && (uint32_t)(ev[u] >> 32) == fp && (!PS.wide || (PS.log[(uint32_t)ev[u] - 1] & ~kDead) == kk))
-                    found = u, fe = ev[u];
-            }
-            if (empty >= 0 && found > empty) found = -1;  // slots fill in order: nothing lives past the first empty
-            if (found >= 0) {  // present: flip it (this entry stays dead)
-                __hip_atomic_fetch_xor(&PS.log[(uint32_t)fe - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                break;
-            }
-            if (empty < 0) {  // bucket full: next one
-                bk = (bk + 1) & bmask;
-                continue;
-            }
-            PS.log[pos] = kk;  // live, then publish
-            const uint64_t old = atomicCAS((unsigned long long*)&PS.idx[bo + empty], 0ull, (unsigned long long)mine);
-            if (old == 0) break;  // inserted
-            PS.log[pos] = kk | kDead;
-            if ((uint32_t)(old >> 32) == fp && (!PS.wide || (PS.log[(uint32_t)old - 1] & ~kDead) == kk)) {  // the same key, inserted by another copy of this pass
-                __hip_atomic_fetch_xor(&PS.log[(uint32_t)old - 1], kDead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                break;
-            }
-            // another key took the slot: probe this bucket again
-        }
-    }
-}
-
-// min live front key (block-uniform; kEmpty64 if none)
-__device__ __forceinline__ uint64_t front_min(ParRed& rd) {
-    const uint32_t c = PS.fcnt;
-    uint64_t b = kEmpty64;
-    for (uint32_t e = threadIdx.x; e < c; e += kParT) {
-        const uint64_t x = PS.log[e];
-        b = x < b ? x : b;
-    }
-    b = b < kDead ? b : kEmpty64;
-    return rd.min(b);
-}
-
-// Keep the live front keys of level <= keep (relative to PS.last), in log
-// order; rebuild the index.  Returns the new length (block-uniform).
-__device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
-    __syncthreads();
-    const uint32_t c = PS.fcnt;
-    const uint64_t last = PS.last;
-    uint32_t w = 0;
-    for (uint32_t e0 = 0; e0 < c; e0 += kParT) {
-        const uint32_t e = e0 + threadIdx.x;
-        const uint64_t x = e < c ? PS.log[e] : kEmpty64;
-        const bool lv = x < kDead && par_bucket(x, last) <= keep;
-        uint32_t tot;
-        const uint32_t o = rd.prefix(lv ? 1u : 0u, &tot);  // barrier: the chunk has been read
-        if (lv) PS.log[w + o] = x;                        // w + o <= e
-        w += tot;
-    }
-    for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
-    __syncthreads();
-    constexpr uint32_t bmask = kFrontBkts - 1;
-    for (uint32_t e = threadIdx.x; e < w; e += kParT) {  // distinct keys: claim the first free slot
-        const uint32_t fp = (uint32_t)PS.log[e];
-        const uint64_t v = ((uint64_t)fp << 32) | (e + 1);
-        uint32_t h = (mix32(fp) & bmask) * 8;
-        for (uint32_t it = 0; it < kFrontIdx; ++it, h = (h + 1) & (kFrontIdx - 1))
-            if (PS.idx[h] == 0 && atomicCAS((unsigned long long*)&PS.idx[h], 0ull, (unsigned long long)v) == 0) break;
-    }
-    if (threadIdx.x == 0) PS.fcnt = w;
-    __syncthreads();
-    return w;
-}
-
-#else  // TDA_PAR_FRONT == 2: one open-addressing Z/2 toggle table
+// One open-addressing Z/2 toggle table.
 // A toggle flips the presence of its key with ONE successful CAS on the key's
 // probe chain: EMPTY -> key (insert) or key -> TOMB (remove); a failed CAS
 // re-reads the same slot.  Slots never return to EMPTY between rebuilds, so a
@@ -504,15 +344,12 @@ __device__ __forceinline__ void front_reset() {
 }
 
 // toggle one key (the lane's own); returns 1 if it filled an EMPTY slot
-#ifndef TDA_PAR_CASFIRST  // build-time A/B knob (tools/): probe with the inserting CAS itself (one LDS round trip per empty slot)
-// (r05: torus1024 32.5 -> 31.8 ms, grid144 5.38 -> 5.31 ms; torus2048_h2 177 -> 179 ms.  Dropped: the
-// second wave of each SIMD at a higher issue priority, s_setprio 1 / 3: torus1024 32.1 -> 33.5-33.8 ms)
-#define TDA_PAR_CASFIRST 1
-#endif
+// Probing with the inserting CAS itself: one LDS round trip per empty slot (r05: torus1024 32.5 ->
+// 31.8 ms, grid144 5.38 -> 5.31 ms against a read, then a CAS).  Also measured and dropped: the
+// second wave of each SIMD at a higher issue priority, s_setprio 1 / 3: torus1024 32.1 -> 33.5-33.8 ms.
 __device__ __forceinline__ uint32_t tab_toggle(uint64_t key) {
     uint32_t h = tab_hash(key);
     for (uint32_t it = 0; it < 4 * kFrontLog; ++it) {
-#if TDA_PAR_CASFIRST
         // the CAS that inserts into an EMPTY slot also reads the slot: a present key
         // comes back as itself (remove it), a tombstone or another key moves the probe on
         const uint64_t v = atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)key);
@@ -521,17 +358,6 @@ __device__ __forceinline__ uint32_t tab_toggle(uint64_t key) {
             if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)key, (unsigned long long)kTabTomb) == key) return 0;
             continue;  // another toggle of this key won: look at the slot again
         }
-#else
-        const uint64_t v = PS.log[h];
-        if (v == key) {
-            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)key, (unsigned long long)kTabTomb) == key) return 0;
-            continue;  // another toggle of this key won: read the slot again
-        }
-        if (v == kTabEmpty) {
-            if (atomicCAS((unsigned long long*)&PS.log[h], (unsigned long long)kTabEmpty, (unsigned long long)key) == kTabEmpty) return 1;
-            continue;
-        }
-#endif
         h = (h + 1) & (kFrontLog - 1);
     }
     PS.err = 13;  // table full (front_room keeps it below kTabMax)
@@ -631,12 +457,8 @@ __device__ __forceinline__ uint32_t front_compact(ParRed& rd, uint32_t keep) {
     __syncthreads();
     return w;
 }
-#endif  // TDA_PAR_FRONT
 
 // ------------------------------------------------------------------ HBM buckets
-#ifndef TDA_PAR_STORE_SC1  // build-time A/B knob (tools/): bucket appends as sc1 (L2-dropping) stores
-#define TDA_PAR_STORE_SC1 0
-#endif
 // (r05: the slot's chunk pointer read from a per-bucket "current chunk" cache
 // beside the slot atomic -- one LDS round trip instead of two -- measured no
 // faster: torus1024 49.2 vs 49.4 ms; dropped)
@@ -672,14 +494,8 @@ __device__ __forceinline__ void bucket_append(const uint64_t (&k)[R], const uint
             PS.err = 21;
             continue;
         }
-#if TDA_PAR_STORE_SC1
-        // write-through store: the bucket line leaves this XCD's L2 (MI355X_MICROARCH.md: sc1 stores
-        // DROP the line, plain ones keep it), so ~600 keys a step do not evict the distance rows the
-        // next steps load
-        ast(P.bpool + (uint64_t)cp * 256 + (slot[r] - chunk_start(kc)), k[r]);
-#else
+        // (r05: sc1 write-through stores that drop the line from this XCD's L2, measured within noise)
         st_glb(P.bpool, (uint64_t)cp * 256 + (slot[r] - chunk_start(kc)), k[r]);
-#endif
     }
 }
 
@@ -733,11 +549,7 @@ __device__ __forceinline__ uint32_t p2_now() {
 
 // Barrier, then room in the front for `need` more log entries: compact, and
 // spill the highest front levels to HBM if too many keys are live.
-#if TDA_PAR_FRONT == 2
 constexpr uint32_t kFrontRoom = kTabMax;
-#else
-constexpr uint32_t kFrontRoom = kFrontLog;
-#endif
 __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t need) {
     lds_sync();
     if (PS.fcnt + need <= kFrontRoom) return;
@@ -754,12 +566,8 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
         for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
         __syncthreads();
         const uint64_t last = PS.last;
-#if TDA_PAR_FRONT == 2
         for (uint32_t e = threadIdx.x; e < kFrontLog; e += kParT)
             if (PS.log[e] < kDead) atomicAdd(&PS.hist[par_bucket(PS.log[e], last)], 1u);
-#else
-        for (uint32_t e = threadIdx.x; e < w; e += kParT) atomicAdd(&PS.hist[par_bucket(PS.log[e], last)], 1u);
-#endif
         __syncthreads();
         int keep = par_keep_level(PS.hist, (int)min(PS.kf + 1u, 64u), kFrontFill);
         if (keep < 0) {  // the exact-diameter level alone is too large for the front
@@ -769,11 +577,7 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
         __syncthreads();
         if (PS.err) return;
         // move the levels above `keep` out to their HBM buckets, then drop them from the front
-#if TDA_PAR_FRONT == 2
         const uint32_t ns = kFrontLog;  // every slot (tombstones and EMPTY are skipped)
-#else
-        const uint32_t ns = w;
-#endif
         for (uint32_t e0 = 0; e0 < ns; e0 += kParT) {
             const uint32_t e = e0 + threadIdx.x;
             uint64_t x[1] = {e < ns ? PS.log[e] : kEmpty64};
@@ -790,21 +594,8 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
 // Insert keys (bit r of vmask; all >= the current pivot) into the working
 // column: front levels toggle in LDS, the rest append to HBM buckets.  No
 // barrier: the caller made room (front_room) for every key of the pass.
-// Back keys of one coboundary round kept in registers: appended to their HBM
-// buckets during the NEXT step, while that step's row loads are in flight
-// (they never affect the next pivot: every back key is above every front key).
-#ifndef TDA_PAR_STASH  // build-time A/B knob (tools/): 1 = r04's deferred back-key appends (stash)
-#define TDA_PAR_STASH 0
-#endif
-struct ParStash {
-    uint64_t k[kParRV];
-    uint32_t b[kParRV];
-    uint32_t m = 0;
-};
-
 template <int R>
-__device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask,
-                                        ParStash* stash = nullptr) {
+__device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
     const uint64_t last = PS.last;
     const uint32_t kf = PS.kf;
     uint32_t fm = 0, bm = 0, bb[R];
@@ -819,28 +610,11 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
 #ifdef TDA_PROFILE
     C.q[7] += (wave_sum_u64((uint64_t)__builtin_popcount(fm)) << 32) | wave_sum_u64((uint64_t)__builtin_popcount(bm));  // wave 0's front / back keys
 #endif
-#if TDA_PAR_STASH
-    PAR_T0(tf0);
-    front_toggle<R>(k, fm);
-    PAR_ACC(1, tf0);
-    if constexpr (R == kParRV) {
-        if (stash) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) stash->k[r] = k[r], stash->b[r] = bb[r];
-            stash->m = bm;
-            return;
-        }
-    }
-    PAR_T0(tb0);
-    bucket_append<R>(k, bb, bm, P);
-    PAR_ACC(2, tb0);
-#else
     // back keys first: their stores are issued as early as possible, so they are
     // acknowledged before the next step waits for its row loads (gfx950 has no
     // separate store counter: a load's s_waitcnt vmcnt also waits for every
-    // store issued before it -- with the r04 stash, the previous step's ~600
-    // bucket stores went out right after the row loads and sat in their wait)
-    (void)stash;
+    // store issued before it -- with the r04 deferred appends, the previous step's
+    // ~600 bucket stores went out right after the row loads and sat in their wait)
     PAR_T0(tb0);
     P2_T(pb0);
     // (r05: back keys staged per wave in LDS and appended in bulk, 256 or 128 per wave -- one
@@ -854,14 +628,6 @@ __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint6
     front_toggle<R>(k, fm);
     P2_ACC(5, pf0);
     PAR_ACC(1, tf0);
-#endif
-}
-
-__device__ __forceinline__ void stash_flush(ParCol& C, const ParBufs& P, ParStash& st) {
-    PAR_T0(tb0);
-    bucket_append<kParRV>(st.k, st.b, st.m, P);
-    st.m = 0;
-    PAR_ACC(2, tb0);
 }
 
 // kParRegs keys per thread of bucket b at [e0, c), loads all in flight
@@ -877,10 +643,11 @@ __device__ __forceinline__ uint32_t bucket_batch(const ParBufs& P, uint32_t b, u
 }
 
 // Front empty: redistribute the lowest non-empty bucket relative to its
-// minimum.  Returns false when the working column is zero.  A bucket of up
+// lower bound.  Returns false when the working column is zero.  A bucket of up
 // to kParRefill * kParT * kParRegs keys is read once into registers; larger
-// ones stream three times (minimum, level histogram, distribution), 8 loads
-// in flight per thread.
+// ones stream twice (level histogram, distribution), kParRegs loads in flight
+// per thread.  (r05: relative to the bucket's exact minimum, one more pass and
+// a block reduction: torus1024 34.4 vs 32.6 ms.)
 __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     __syncthreads();
 #ifdef TDA_PROFILE
@@ -898,16 +665,10 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
 #ifdef TDA_PROFILE
     C.q[6] += c;
 #endif
-#if TDA_PAR_FRONT == 2
     front_clear();
-#else
-    for (uint32_t e = threadIdx.x; e < kFrontIdx; e += kParT) PS.idx[e] = 0;
-    if (threadIdx.x == 0) PS.fcnt = 0;
-#endif
     for (uint32_t q = threadIdx.x; q < kParLv; q += kParT) PS.hist[q] = 0;
     uint64_t x[kParRefill][kParRegs];
     uint32_t vm[kParRefill] = {};
-#if TDA_PAR_NLB
     // no minimum pass: the new reference is the smallest key with bucket b's common high bits
     // (bits above b - 1 as `last`, bit b - 1 set), a lower bound of every key in the bucket, so
     // the bucket's keys fall in levels < b and the higher buckets keep theirs.  (The exact
@@ -920,28 +681,6 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     }
     __syncthreads();  // the resets above are done
     PAR_Q3(1);
-#else
-    // pass 1: minimum (raw; a cancelled duplicate is still a lower bound of every live key)
-    uint64_t mn = kEmpty64;
-    if (inreg) {
-#pragma unroll
-        for (int h = 0; h < kParRefill; ++h) vm[h] = bucket_batch(P, (uint32_t)b, h * kPass, c, x[h]);
-#pragma unroll
-        for (int h = 0; h < kParRefill; ++h)
-#pragma unroll
-            for (int r = 0; r < kParRegs; ++r) mn = x[h][r] < mn ? x[h][r] : mn;
-    } else {
-        for (uint32_t e0 = 0; e0 < c; e0 += kPass) {
-            uint64_t y[kParRegs];
-            (void)bucket_batch(P, (uint32_t)b, e0, c, y);
-#pragma unroll
-            for (int r = 0; r < kParRegs; ++r) mn = y[r] < mn ? y[r] : mn;
-        }
-    }
-    mn = C.rd.min(mn);  // barrier: the resets above are done too
-    PAR_Q3(1);
-    const uint64_t nl = mn;
-#endif
     // pass 2: histogram of the new levels (all < b); the front keeps the lowest
     // levels that hold at most kFrontFill keys.  (A binary search on the level
     // with block counts instead of the atomics measured slower: 7.1 vs 4.3 M
@@ -1034,7 +773,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
 // Round 0's rows may already be in registers (da0 / db0, prefetched with the pivot).
 template <bool PACKED>
 __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float* __restrict__ D, int n, float r, int a, int b, float sd,
-                        const float (&da0)[kParRV], const float (&db0)[kParRV], ParStash* stash = nullptr) {
+                        const float (&da0)[kParRV], const float (&db0)[kParRV]) {
     for (int v0 = 0; v0 < n; v0 += kParT * kParRV) {
         float da[kParRV], db[kParRV];
 #pragma unroll
@@ -1083,7 +822,7 @@ __device__ __forceinline__ void col_cob(ParCol& C, const ParBufs& P, const float
         P2_DEP(vm);
         P2_ACC(3, pk0);
         PAR_ACC(0, tk0);
-        col_add<kParRV>(C, P, key, vm, v0 == 0 ? stash : nullptr);  // no barrier: the caller made room for all n keys
+        col_add<kParRV>(C, P, key, vm);  // no barrier: the caller made room for all n keys
     }
 }
 
@@ -1104,7 +843,7 @@ __device__ __forceinline__ uint32_t tet_lo(uint64_t idx, int f) {
 // slots), sd is the triangle's code, keys are code << 42 | (2^42 - 1 - index).
 template <bool PACKED, bool WIDE = false>
 __device__ __forceinline__ void col_cob2(ParCol& C, const ParBufs& P, const float* __restrict__ D, int n, float r, int a, int b, int c,
-                                         float sd, const float (&r0)[3][kParRV], ParStash* stash = nullptr) {
+                                         float sd, const float (&r0)[3][kParRV]) {
     // the triangle's own edges (facet diameters of its cofacets)
     const float eab = WIDE ? 0.0f : ld_glb(D, (size_t)a * n + b), eac = WIDE ? 0.0f : ld_glb(D, (size_t)a * n + c),
                 ebc = WIDE ? 0.0f : ld_glb(D, (size_t)b * n + c);
@@ -1161,7 +900,7 @@ __device__ __forceinline__ void col_cob2(ParCol& C, const ParBufs& P, const floa
             vm |= 1u << q;
         }
         PAR_ACC(0, tk0);
-        col_add<kParRV>(C, P, key, vm, v0 == 0 ? stash : nullptr);
+        col_add<kParRV>(C, P, key, vm);
     }
 }
 
@@ -1187,11 +926,7 @@ __device__ __forceinline__ int64_t col_save(ParCol& C, const ParBufs& P, uint64_
 #ifdef TDA_PROFILE
     const uint64_t tsv = clock64();
 #endif
-#if TDA_PAR_FRONT == 2
     const uint32_t c = kFrontLog;  // every slot (only live keys are < kDead)
-#else
-    const uint32_t c = PS.fcnt;
-#endif
     uint32_t lv = 0;
     for (uint32_t e = threadIdx.x; e < c; e += kParT) lv += PS.log[e] < kDead;
     const uint64_t nfront = C.rd.sum(lv);
@@ -1469,6 +1204,13 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         uint64_t nres_l = ld_glb(P.item_base, l + 1) - ld_glb(P.item_base, l);
         const uint64_t omask = par_omask(nres_l, P.ostride);
         uint64_t* colpiv = P.colpiv + (size_t)l * b1.rcap;
+        // a layer that missed a column cap is re-run without caps by the host: its columns are dropped
+        if (tid == 0) PS.lfail = layer_cap_missed(st);
+        __syncthreads();
+        if (PS.lfail) {
+            if (tid == 0) ast(colpiv + j, kParSkip);
+            continue;
+        }
         const uint64_t ckey = ld_glb(resid, j);
         const uint64_t sidx = key_idx(ckey);
         const float sdm = key_diam(ckey);
@@ -1479,9 +1221,11 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         // because pivots only grow along a column's reduction.  The records j adds come from
         // EARLIER columns (larger births, so larger caps: they hold every key j keeps), and an
         // evicted column re-adds the record of an earlier one (the same order).  A column that
-        // runs empty below its cap has its pivot above it: the launch aborts (code 81) and the
-        // host re-runs the call without caps (remembered for the shape).  90 % of the keys the
-        // longest torus1024 column generates lie above its final pivot (tools/front_sim.py).
+        // runs empty below its cap has its pivot above it: its layer is flagged (ERR_CAP_MISS), the
+        // layer's other columns are dropped, and the host re-runs that layer alone without caps --
+        // the other layers of the launch are unaffected (a missed column never claims a pivot, and
+        // a column of another layer never reads this layer's records).  90 % of the keys the longest
+        // torus1024 column generates lie above its final pivot (tools/front_sim.py).
         float rc = r;
         bool capped = false;
         if (!WIDE && P.capf > 0.0f) {
@@ -1559,7 +1303,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #endif
         uint64_t step = 0;
         const uint32_t need = par_need(n);
-        ParStash stash;
 #ifdef TDA_PROF2
         for (int q = 0; q < 8; ++q) C.tp[q] = 0;
 #endif
@@ -1588,17 +1331,25 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 ++nref;
 #endif
                 P2_T(ps6);
-                stash_flush(C, P, stash);  // the refill reads every bucket count
+                if (tid == 0) PS.lfail = layer_cap_missed(st);  // read behind col_refill's first barrier
                 const bool more = col_refill(C, P);
                 P2_ACC(6, ps6);
 #ifdef TDA_PROFILE
                 pf[4] += clock64() - t0;
 #endif
+                if (PS.lfail) {  // another column of this layer missed its cap: the layer re-runs
+                    done = true;
+                    continue;
+                }
                 if (!more) {
                     if (PS.err) break;
-                    if (capped) {  // empty below the cap: the pivot lies above it -> the call re-runs uncapped
-                        if (tid == 0) PS.err = 81;
-                        break;
+                    if (capped) {  // empty below the cap: the pivot lies above it -> this layer re-runs uncapped
+                        if (tid == 0) {
+                            atomicOr(&st->err, ERR_CAP_MISS);
+                            ast(colpiv + j, kParSkip);
+                        }
+                        done = true;
+                        continue;
                     }
                     if (tid == 0) ast(colpiv + j, kParEss);  // zero column: essential
                     done = true;
@@ -1658,7 +1409,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             // per-edge apparent-partner table, 2 B per edge -- 1 MB per layer at N = 1024 against the
             // 22 MB triangle bitmap -- measured no faster: torus1024 37.0 vs 36.7 ms, dropped)
             const uint32_t pw = ld_glb(pivg, pidx >> 5);
-            stash_flush(C, P, stash);  // the previous step's back keys, under this step's load latency
             const bool app = (pw >> (pidx & 31)) & 1u;
             P2_DEP(pw);
             P2_ACC(2, ps2);
@@ -1668,9 +1418,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #endif
             if (app) {
                 if constexpr (DIM == 1)
-                    col_cob<PACKED>(C, P, D, n, rc, fv[0], fv[1], pd, z[0], z[1], &stash);
+                    col_cob<PACKED>(C, P, D, n, rc, fv[0], fv[1], pd, z[0], z[1]);
                 else
-                    col_cob2<PACKED, WIDE>(C, P, Dr, n, rc, fv[0], fv[1], fv[2], WIDE ? __uint_as_float(fsc) : pd, z, &stash);
+                    col_cob2<PACKED, WIDE>(C, P, Dr, n, rc, fv[0], fv[1], fv[2], WIDE ? __uint_as_float(fsc) : pd, z);
                 ++adds;
 #ifdef TDA_PROFILE
                 pf[3] += clock64() - t0;
@@ -1859,8 +1609,9 @@ __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stat
     }
     map.lds = false;
     const bool failed = P.ctl->abort != 0;
+    const bool missed = (st->err & ERR_CAP_MISS) != 0;  // the host re-runs this layer without caps
     uint64_t cs = 0, np = 0, nskip = 0;
-    if (!failed) {
+    if (!failed && !missed) {
         for (uint64_t j = tid; j < nres; j += blockDim.x) {
             const uint64_t cp = colpiv[j];
             const uint64_t key = resid[j];
@@ -1904,7 +1655,7 @@ __global__ __launch_bounds__(1024) void k_par_emit(LayerStats* __restrict__ stat
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) a += red[0][w], b += red[1][w], c += red[2][w];
         if (failed) {
             atomicOr(&st->err, DIM == 1 ? ERR_PAR : ERR_PAR2);
-        } else {
+        } else if (!missed) {
             atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)a);
             atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)b);
             atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)(0ull - c));

@@ -167,7 +167,7 @@ def _unpack(res_p, want_dist: bool, n_sets: int = 0) -> tuple[list, dict]:
     out = list(map(LayerResult, zip(repeat(b, L), range(L))))
     ns = r.n_stages
     stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(ns)] if ns else []
-    return out, {"device_ms": r.device_ms, "stages": stages}
+    return out, {"device_ms": r.device_ms, "stages": stages, "cap_reruns": int(r.n_cap_reruns)}
 
 
 def _call_batch(args: _lib.RipsArgs, want_dist: bool):

@@ -71,3 +71,23 @@ def activations(n_layers: int = 32, n: int = 144, d: int = 4096, seed: int = 0) 
         X[:, rng.integers(0, d, max(1, d // 64))] *= 20.0
         out[l] = X
     return out
+
+
+def circle(n: int = 1024, seed: int = 0, noise: float = 0.02) -> np.ndarray:
+    """Known-answer cloud: a noisy unit circle in R^3, one long
+    H1 class that dies near sqrt(3) ~ 0.87 of the enclosing radius."""
+    rng = np.random.default_rng(seed)
+    th = rng.uniform(0, 2 * np.pi, n)
+    X = np.stack([np.cos(th), np.sin(th), np.zeros(n)], 1) + rng.normal(0.0, noise, (n, 3))
+    return X.astype(np.float32)
+
+
+def sphere(n: int = 1024, seed: int = 0, noise: float = 0.0) -> np.ndarray:
+    """Known-answer cloud: uniform points on the unit sphere S^2,
+    one long H2 class."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, 3))
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    if noise:
+        X = X + rng.normal(0.0, noise, (n, 3))
+    return X.astype(np.float32)

@@ -42,7 +42,7 @@ def test_library_is_gfx950_code_object(built_lib):
 
 def test_version_and_no_device_here(pkg, built_lib):
     L = pkg.lib()
-    assert L.tda_version() == 7  # ABI 7: caller stream NULL = null stream + TDA_FLAG_INPUT_READY (6: input parts, 5: workspace slot, 4: dist64, 3: TwoNN, 2: silhouettes)
+    assert L.tda_version() == 8  # ABI 8: n_cap_reruns; 7: caller stream NULL = null stream + TDA_FLAG_INPUT_READY; 6: input parts; 5: workspace slot; 4: dist64; 3: TwoNN; 2: silhouettes
     assert L.tda_device_ok(12345) == 0
 
 

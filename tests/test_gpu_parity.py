@@ -872,10 +872,10 @@ def test_foreign_caller_stream_is_refused(gpu):
 def test_column_caps_exact_and_fallback(gpu, monkeypatch, capf):
     """k_reduce_par column caps (r05): keys above birth + capf * thresh are
     never stored.  The default cap (0.5), a cap far too small (0.02: the long
-    columns run empty below it, the launch aborts with code 81 and the call
-    re-runs uncapped) and no cap all give the committed oracle results:
-    torus1024 (configs[3], H0-H1) and grid144 (configs[4], H0-H2, where the
-    H2 columns are capped too).  The memo is off, so every call starts capped."""
+    columns run empty below it, their layers are flagged and re-run one by one
+    without caps, then spliced into the batch's result) and no cap all give the
+    committed oracle results: torus1024 (configs[3], H0-H1) and grid144
+    (configs[4], H0-H2, where the H2 columns are capped too)."""
     monkeypatch.setenv("TDA_PAR_CAPF", capf)
     monkeypatch.setenv("TDA_RETRY_MEMO", "0")
     z = _large_golden()
@@ -884,3 +884,47 @@ def test_column_caps_exact_and_fallback(gpu, monkeypatch, capf):
         res = gpu.ripser_batch(X, maxdim=md)
         for l in range(X.shape[0]):
             assert_same_golden(res[l], z, name, l, md)
+
+
+def _cap_miss_batch(gpu):
+    """32 tori at N = 256 (every H1 class well under the cap) with one noisy
+    circle (layer 7: one loop from 0.07 to 0.86 of the enclosing radius, so its
+    column runs empty below birth + 0.5 * thresh)."""
+    syn = gpu.synthetic
+    X = np.stack([syn.torus(256, seed=s) for s in range(32)])
+    X[7] = syn.circle(256, seed=1)
+    return X
+
+
+def test_cap_miss_reruns_only_its_layer(gpu, oracle, monkeypatch):
+    """a capped column whose pivot lies above its cap flags
+    its layer only; the library re-runs that layer alone without caps and
+    splices it in.  One 32-layer batch with one circle layer: every layer equals
+    the oracle, exactly one layer was re-run, and a second call (no shape memo)
+    re-runs it again while the other layers stay capped.  Host numpy input,
+    device input and device input in parts (the SweepPipeline path)."""
+    import torch
+
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")  # the parallel reducer itself must succeed
+    X = _cap_miss_batch(gpu)
+    exp = [oracle.rips(X[l], maxdim=1) for l in range(32)]
+    Xd = torch.from_numpy(X).to("cuda:0")
+    for tag, inp in (("host", X), ("host again", X), ("device", Xd), ("device parts", [Xd[:16], Xd[16:]])):
+        res, info = gpu.ripser_batch(inp, maxdim=1, return_time=True)
+        assert info["cap_reruns"] == 1, (tag, info["cap_reruns"])
+        for l in range(32):
+            assert_same(res[l], exp[l], 1, (tag, l))
+
+
+def test_cap_miss_h2_sphere_and_circle(gpu, oracle, monkeypatch):
+    """H2 columns are capped too (N <= 568): a sphere (one void from 0.29 to
+    0.83 of the enclosing radius) misses an H2 cap, a circle an H1 cap; the
+    torus layers beside them do not.  Every layer equals the oracle, two layers
+    were re-run."""
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")
+    syn = gpu.synthetic
+    X = np.stack([syn.torus(256, seed=0), syn.sphere(256, seed=2), syn.torus(256, seed=1), syn.circle(256, seed=1)])
+    res, info = gpu.ripser_batch(X, maxdim=2, return_time=True)
+    assert info["cap_reruns"] == 2, info["cap_reruns"]
+    for l in range(4):
+        assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, l)
