@@ -1,23 +1,30 @@
 """Benchmark of the hot path: per-layer pairwise distance + Vietoris-Rips
 persistence H0-H2 (BASELINE.json metric "layers/sec ... at 1/2/4/8 MI355X").
 
-A step = one pass of the hot path over one batch, inputs already resident in
-HBM, diagrams returned to the host:
-  * primary (``value``): the reference's 32-layer sweep (debug_tda_pipeline.py:
-    92-150) of 48-point clouds, configs[1] per layer (48 points, D=3, H0-H2);
-  * ``workloads`` (N=1 only): configs[4] grid144 (32 layers x 144 points,
-    H0-H2) and configs[3] torus1024 (one 1024-point layer, H0-H1), each with
-    its own roofline and CPU baseline.
+A step = one pass of the hot path over one 32-layer sweep, diagrams returned
+to the host:
+  * primary (``value``, SURVEY 8(d) as written): ``sweep48_host`` -- the
+    reference's 32-layer sweep (debug_tda_pipeline.py:92-150) of 48-point
+    clouds, configs[1] per layer (48 points, D=3, H0-H2), host numpy array in,
+    every layer's ``dgms`` list materialised on the host; each step submits a
+    DIFFERENT sweep (8 noise seeds of the generator, rotated);
+  * ``workloads`` (N=1 only): the same sweep HBM-resident (``sweep48``),
+    configs[4] grid144, configs[3] torus1024, the top of the N range, the
+    drop-in ``ripser()`` call itself at the reference's N = 36 and the
+    adversarial N = 324 (``ripser36`` / ``ripser324``), each with its own
+    roofline and CPU baseline.
 Multi-GPU: one process per GPU (torchrun).  ``--scaling weak`` (default):
-every rank runs its own 32-layer sweep; ``strong``: the 32 layers are sharded
+every rank runs its own 32-layer sweeps; ``strong``: the 32 layers are sharded
 (configs[2]: 4 layers/GPU at 8 GPUs).  Either way a step ends with the one
 gather of per-layer records to rank 0 (distributed.sharded_sweep_step); at
-N > 1 a strong-scaling record is added next to the weak one.
+N > 1 a strong-scaling record is added next to the weak one, the CPU baseline
+is measured by the launching process before any rank touches a GPU, and rank 0
+runs the stage pass that gives the line its roofline.
 
 CPU baseline: the oracle (oracle/rips_oracle.c, a C restatement of the
 ripser semantics; "kind": "port") on the same inputs, 1 core and P worker
-processes (the host CPUs this job may use, at most 16 per GPU on the box),
-on bounded samples.  Prints ONE JSON line on rank 0.
+processes (the host CPUs this job may use: 16 per GPU, the whole host at
+8 GPUs), on bounded samples.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -66,6 +73,13 @@ WORKLOADS = {
     # raw hidden states (no UMAP): distance on the FP64 matrix cores + TwoNN + H0
     "raw4096": (32, 0, "32 layers x 144 tokens x 4096 raw hidden-state features: distance (FP64 MFMA) + H0 + TwoNN "
                        "intrinsic dimension (metrics.py:113-208)", 100, 3),
+    # the drop-in itself at the reference's own call: ripser(cloud, maxdim=1) once per layer, numpy (N, 3) f32 in,
+    # the full ripser.py dict out (dgms, num_edges, dperm2all, ...), one call at a time (debug_tda_pipeline.py:109-110)
+    "ripser36": (32, 1, "ripser(cloud, maxdim=1) per layer on the reference's 32 committed UMAP clouds (N=36, D=3), "
+                        "one call per layer, full dict out (debug_tda_pipeline.py:109-110)", 10, 2),
+    # ... and at the adversarial experiment's N = 324 (analyze_adversarial_tda.py:100)
+    "ripser324": (32, 1, "ripser(cloud, maxdim=1) per layer on 32 UMAP clouds of 324 prompts (N=324, D=3; "
+                         "analyze_adversarial_tda.py:100), one call per layer, full dict out", 5, 1),
 }
 DATA = {
     "sweep48": "synthetic: reference UMAP clouds (tda-output/point_clouds_3d) resampled to 48 points + noise",
@@ -79,9 +93,13 @@ DATA = {
     "torus2048": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 3",
     "torus2048_h2": "synthetic: uniform angles on S1 x S1 (R=2, r=1), seed 3",
     "raw4096": "synthetic: activation-like f32 clouds (heavy-tailed feature scales, offsets, outlier features)",
+    "ripser36": "the reference's own 32 UMAP clouds (tda-output/point_clouds_3d, tests/golden/reference_clouds.npz)",
+    "ripser324": "synthetic: this build's umap_batch (cosine, n_neighbors 6, 3 components) of 18 x 18 two-factor activation "
+                 "clouds (tests/golden/adv_clouds.npz, tools/make_adv_clouds.py)",
 }
 NPOINTS = {"torus1024x32": 1024, "sweep48": 48, "sweep48x4": 48, "sweep48_host": 48, "sweep48_L4": 48, "sweep48_L1": 48,
-           "grid144": 144, "torus1024": 1024, "raw4096": 144, "torus2048": 2048, "torus2048_h2": 2048}
+           "grid144": 144, "torus1024": 1024, "raw4096": 144, "torus2048": 2048, "torus2048_h2": 2048, "ripser36": 36,
+           "ripser324": 324}
 DIMS = {w: (4096 if w == "raw4096" else 3) for w in WORKLOADS}  # point dimension D of each workload (make_workload)
 CALL_KW = {"raw4096": {"twonn": True}, "torus2048_h2": {"thresh": 1.2}}
 # dynamic batching of consecutive steps (ripser.SweepPipeline): every step submits one 32-layer sweep;
@@ -112,7 +130,11 @@ def pipe_shape(name: str, steps: int) -> tuple:
 
 
 # workloads whose layers are the same clouds as another's: one CPU baseline serves both
-CPU_SAME = {"sweep48_host": "sweep48", "sweep48_L4": "sweep48", "sweep48x4": "sweep48", "sweep48_L1": "sweep48"}
+CPU_SAME = {"sweep48": "sweep48_host", "sweep48_L4": "sweep48_host", "sweep48x4": "sweep48_host", "sweep48_L1": "sweep48_host"}
+# distinct sweeps per step: step i runs sweep i % K -- K noise seeds of the same generator
+# (synthetic.sweep48 / sweep144 `variant`), so no step resubmits the previous step's array.  K = 8 keeps a
+# slot's captured graphs (one per device input address without parts) well under its limit of 16.
+ROTATE = {w: 8 for w in ("sweep48", "sweep48_host", "sweep48_L4", "sweep48_L1", "sweep48x4", "grid144")}
 
 
 def algo_bytes_per_layer(n: int, d: int, maxdim: int) -> int:
@@ -137,7 +159,8 @@ def mfma_executed(n: int, d: int, L: int, ms: float) -> dict:
 # (the reference runs one ripser call per layer and ripser is single-threaded);
 # a sweep (many independent layers per step) against the CPU running its
 # layers in parallel, one per worker process (P processes, the box's CPU share).
-BAR_BASIS = {"torus1024": "one_core", "torus2048": "one_core", "torus2048_h2": "one_core", "sweep48_L1": "one_core"}
+BAR_BASIS = {"torus1024": "one_core", "torus2048": "one_core", "torus2048_h2": "one_core", "sweep48_L1": "one_core",
+             "ripser36": "one_core", "ripser324": "one_core"}
 
 
 def speedups(value: float, cb: dict, name: str) -> dict:
@@ -152,13 +175,18 @@ def speedups(value: float, cb: dict, name: str) -> dict:
     return sp
 
 
-def make_workload(name: str, layers: int | None = None):
+def make_workload(name: str, layers: int | None = None, variant: int = 0):
     syn = importlib.import_module("tda-multimodal_amd.synthetic")
     L = layers or WORKLOADS[name][0]
     if name in ("sweep48", "sweep48x4", "sweep48_host", "sweep48_L4", "sweep48_L1"):
-        return syn.sweep48(L)
+        return syn.sweep48(L, variant)
     if name == "grid144":
-        return syn.sweep144(L)
+        return syn.sweep144(L, variant)
+    if name == "ripser36":
+        return syn.reference_clouds()[:L]
+    if name == "ripser324":
+        z = np.load(os.path.join(ROOT, "tests", "golden", "adv_clouds.npz"))
+        return z["n324"][:L].astype(np.float32)
     if name == "torus1024":
         return syn.torus(1024)[None].repeat(L, 0)
     if name == "torus1024x32":
@@ -168,6 +196,16 @@ def make_workload(name: str, layers: int | None = None):
     if name == "raw4096":
         return syn.activations(L, 144, 4096)
     raise ValueError(name)
+
+
+def workload_sweeps(name: str, layers: int | None = None) -> list:
+    """The sweeps a workload's steps rotate through (ROTATE; one otherwise)."""
+    return [make_workload(name, layers, v) for v in range(ROTATE.get(name, 1))]
+
+
+def workload_layers(name: str, layers: int | None = None) -> np.ndarray:
+    """Every layer the workload's steps run, concatenated (the CPU baseline's inputs)."""
+    return np.concatenate(workload_sweeps(name, layers))
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -180,7 +218,7 @@ def _cpu_layers(task):
     from oracle import oracle
 
     if name not in _WORKER_CACHE:
-        _WORKER_CACHE[name] = make_workload(name)
+        _WORKER_CACHE[name] = workload_layers(name)
     X = _WORKER_CACHE[name]
     oracle.lib()
     if hi > lo:
@@ -249,13 +287,14 @@ def cpu_baseline(pool, P: int, name: str, X, maxdim: int, seconds: float) -> dic
 
 
 # ---------------------------------------------------------------- GPU measurement
-def _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_index, coalesce=1):
+def _timed_steps(pkg, torch, Xs, maxdim, kw, steps, warmup, depth, host_in, dev_index, coalesce=1):
     """K steps (sequential, or through ripser.SweepPipeline: `depth` calls in flight on separate
     workspace slots, each call covering up to `coalesce` consecutive steps' sweeps) between two
-    syncs; returns (elapsed s, device ms per step)."""
+    syncs; step i runs sweep Xs[i % len(Xs)].  Returns (elapsed s, device ms per step)."""
     import collections
 
     dev_ms = []
+    K = len(Xs)
 
     def done(res, info):
         if host_in:  # debug_tda_pipeline.py:110: dgms = result['dgms'] for every layer
@@ -264,73 +303,42 @@ def _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, depth, host_in, dev_i
         dev_ms.append(info["device_ms"] / info.get("coalesced", 1))
 
     if depth <= 1 and coalesce <= 1:
-        for _ in range(warmup):
-            pkg.ripser_batch(X, maxdim=maxdim, **kw)
+        for i in range(max(warmup, K)):  # every input address once (a device input's graph is keyed by it)
+            pkg.ripser_batch(Xs[i % K], maxdim=maxdim, **kw)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            done(*pkg.ripser_batch(X, maxdim=maxdim, return_time=True, **kw))
+        for i in range(steps):
+            done(*pkg.ripser_batch(Xs[i % K], maxdim=maxdim, return_time=True, **kw))
         torch.cuda.synchronize()
         return time.perf_counter() - t0, dev_ms
     inflight = depth * coalesce  # steps submitted and not yet waited on
     with pkg.SweepPipeline(depth=depth, device=dev_index, coalesce=coalesce, maxdim=maxdim, return_time=True, **kw) as pipe:
-        for f in [pipe.submit(X) for _ in range(max(warmup, 1) * inflight)]:  # every slot captures its graph
+        n_warm = max(max(warmup, 1) * inflight, K * depth)  # every slot captures its graphs (and sees every input)
+        for f in [pipe.submit(Xs[i % K]) for i in range(n_warm)]:
             f.result()
         torch.cuda.synchronize()
         dev_ms.clear()
         t0 = time.perf_counter()
         q = collections.deque()
-        for _ in range(steps):
+        for i in range(steps):
             if len(q) == inflight:
                 done(*q.popleft().result())
-            q.append(pipe.submit(X))
+            q.append(pipe.submit(Xs[i % K]))
         while q:
             done(*q.popleft().result())
         torch.cuda.synchronize()
         return time.perf_counter() - t0, dev_ms
 
 
-def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | None = None) -> dict:
-    L, maxdim, desc, _, _ = WORKLOADS[name]
-    L = layers or L
-    X_host = make_workload(name, L)
-    n, d = X_host.shape[1], X_host.shape[2]
-    host_in = name.endswith("_host")
-    # resident in HBM before the timed region -- except the host-in record, which passes the numpy array
-    X = X_host if host_in else torch.from_numpy(X_host).to(dev)
-    torch.cuda.synchronize()
-    kw = dict(CALL_KW.get(name, {}))
-    if os.environ.get("TDA_BENCH_READY", "1") == "1" and not host_in:
-        # X was synchronised above (resident in HBM before the timed region): no per-call event on
-        # torch's stream, whose hardware queue a pipeline slot may share (TDA_BENCH_READY=0: with it)
-        kw["input_ready"] = True
-    depth, coalesce = pipe_shape(name, steps)
-    kw_pipe = dict(kw)
-    if os.environ.get("TDA_BENCH_ONE_STREAM") in ("0", "1"):  # else SweepPipeline's default (one stream when depth > 1)
-        kw_pipe["one_stream"] = os.environ["TDA_BENCH_ONE_STREAM"] == "1"
-    dev_index = dev.index if dev.index is not None else 0
-    seq = None
-    piped = depth > 1 or coalesce > 1
-    # TDA_BENCH_STAGE_ONLY=1 (profiling): only the stage pass below runs, so a rocprof trace of the
-    # command holds exactly the launches the roofline's kernel_avg_ms is taken from (profiles/*_stage.csv)
-    stage_only = os.environ.get("TDA_BENCH_STAGE_ONLY") == "1"
-    if piped and os.environ.get("TDA_BENCH_NO_SEQ") != "1" and not stage_only:  # the one-call-at-a-time figure next to the pipelined one
-        # (TDA_BENCH_NO_SEQ=1: profiling runs, so every launch in the trace is the pipeline's batch)
-        el_s, dm_s = _timed_steps(pkg, torch, X, maxdim, kw, steps, warmup, 1, host_in, dev_index)
-        seq = {"value": L * steps / el_s, "ms_per_step": el_s / steps * 1e3, "device_ms_per_step": sum(dm_s) / len(dm_s)}
-    if stage_only:
-        el, dev_ms = float("nan"), [float("nan")]
-    else:
-        el, dev_ms = _timed_steps(pkg, torch, X, maxdim, kw_pipe if piped else kw, steps, warmup, depth, host_in, dev_index, coalesce)
-    # per-kernel durations: HIP events around every kernel with all stages on
-    # ONE stream (each interval brackets exactly one kernel), same batch,
-    # after the timed region; the dominant kernel has the largest mean
-    # (a coalesced pipeline launches every kernel over `coalesce` sweeps: the stage pass runs that batch too)
-    Xst, Lk = ([X] * coalesce, L * coalesce) if coalesce > 1 else (X, L)
+def stage_roofline(run, name: str, X, Lk: int, n: int, d: int, maxdim: int, kw: dict, calls: int) -> dict:
+    """Per-kernel durations of one batch (`Lk` layers): HIP events around every kernel with all
+    stages on ONE stream (each interval brackets exactly one kernel), median over `calls` calls;
+    the dominant kernel (largest median) against its roofline.  `run` is ripser_batch (or a
+    multi-rank rehearsal's stand-in with the same interface)."""
     acc: dict = {}
-    pkg.ripser_batch(Xst, maxdim=maxdim, stage_times=True, stage_serial=True, **kw)  # untimed: first use of this schedule
-    for _ in range(max(1, min(steps, 10))):
-        _, info = pkg.ripser_batch(Xst, maxdim=maxdim, return_time=True, stage_times=True, stage_serial=True, **kw)
+    run(X, maxdim=maxdim, stage_times=True, stage_serial=True, **kw)  # untimed: first use of this schedule
+    for _ in range(max(1, calls)):
+        _, info = run(X, maxdim=maxdim, return_time=True, stage_times=True, stage_serial=True, **kw)
         for k, ms in info["stages"]:
             acc.setdefault(k, []).append(ms)
     stages = {k: float(np.median(v)) for k, v in acc.items()}  # median: one slow outlier (a profiler hiccup) no longer sets it
@@ -391,9 +399,6 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
                      "algo_flops_per_layer": fpl, "layers_per_launch": Lk, "kernel_avg_ms": kern[gram],
                      **mfma_executed(n, d, Lk, kern[gram])}
     return {
-        "value": L * steps / el, "unit": "layers/s", "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warmup,
-        "device_ms_per_step": sum(dev_ms) / len(dev_ms), "X_host": X_host, "maxdim": maxdim,
-        "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim},
         "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
                      "frac": achieved / peak, "traffic": traffic, **per_layer, "lds_occupancy": lds_occ,
                      "layers_per_launch": Lk, "kernel_avg_ms": kern[dom], "kernel_mean_ms": dom_mean,
@@ -403,13 +408,93 @@ def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | N
                                       "(kernel_mean_ms) of the stage pass's calls, less the median empty event "
                                       "interval (event_gap_ms; kernel_avg_ms_events is the raw median).  The same "
                                       "launches alone under rocprofv3: profiles/<round>_kernel_stats_<workload>_stage.csv"},
-        "stages_ms": {k: round(v, 5) for k, v in stages.items()},
         "roofline_mfma": mfma_roof,
+        "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+    }
+
+
+def measure(pkg, torch, dev, name: str, steps: int, warmup: int, layers: int | None = None) -> dict:
+    L, maxdim, desc, _, _ = WORKLOADS[name]
+    L = layers or L
+    if name.startswith("ripser"):
+        return measure_dropin(pkg, torch, name, steps, warmup, L)
+    sweeps = workload_sweeps(name, L)
+    X_host = sweeps[0]
+    n, d = X_host.shape[1], X_host.shape[2]
+    host_in = name.endswith("_host")
+    # resident in HBM before the timed region -- except the host-in record, which passes numpy arrays
+    Xs = sweeps if host_in else [torch.from_numpy(x).to(dev) for x in sweeps]
+    torch.cuda.synchronize()
+    kw = dict(CALL_KW.get(name, {}))
+    if os.environ.get("TDA_BENCH_READY", "1") == "1" and not host_in:
+        # Xs were synchronised above (resident in HBM before the timed region): no per-call event on
+        # torch's stream, whose hardware queue a pipeline slot may share (TDA_BENCH_READY=0: with it)
+        kw["input_ready"] = True
+    depth, coalesce = pipe_shape(name, steps)
+    kw_pipe = dict(kw)
+    if os.environ.get("TDA_BENCH_ONE_STREAM") in ("0", "1"):  # else SweepPipeline's default (one stream when depth > 1)
+        kw_pipe["one_stream"] = os.environ["TDA_BENCH_ONE_STREAM"] == "1"
+    dev_index = dev.index if dev.index is not None else 0
+    seq = None
+    piped = depth > 1 or coalesce > 1
+    # TDA_BENCH_STAGE_ONLY=1 (profiling): only the stage pass below runs, so a rocprof trace of the
+    # command holds exactly the launches the roofline's kernel_avg_ms is taken from (profiles/*_stage.csv)
+    stage_only = os.environ.get("TDA_BENCH_STAGE_ONLY") == "1"
+    if piped and os.environ.get("TDA_BENCH_NO_SEQ") != "1" and not stage_only:  # the one-call-at-a-time figure next to the pipelined one
+        # (TDA_BENCH_NO_SEQ=1: profiling runs, so every launch in the trace is the pipeline's batch)
+        el_s, dm_s = _timed_steps(pkg, torch, Xs, maxdim, kw, steps, warmup, 1, host_in, dev_index)
+        seq = {"value": L * steps / el_s, "ms_per_step": el_s / steps * 1e3, "device_ms_per_step": sum(dm_s) / len(dm_s)}
+    if stage_only:
+        el, dev_ms = float("nan"), [float("nan")]
+    else:
+        el, dev_ms = _timed_steps(pkg, torch, Xs, maxdim, kw_pipe if piped else kw, steps, warmup, depth, host_in, dev_index,
+                                  coalesce)
+    # per-kernel durations after the timed region, same batch (a coalesced pipeline launches every
+    # kernel over `coalesce` sweeps: the stage pass runs that batch too)
+    Xst, Lk = ([Xs[i % len(Xs)] for i in range(coalesce)], L * coalesce) if coalesce > 1 else (Xs[0], L)
+    sr = stage_roofline(pkg.ripser_batch, name, Xst, Lk, n, d, maxdim, kw, max(1, min(steps, 10)))
+    return {
+        "value": L * steps / el, "unit": "layers/s", "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warmup,
+        "device_ms_per_step": sum(dev_ms) / len(dev_ms), "X_host": np.concatenate(sweeps), "maxdim": maxdim,
+        "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim,
+                   "distinct_sweeps": len(sweeps)},
+        **sr,
         "pipeline": {"depth": depth, "coalesce": coalesce, "one_stream": kw_pipe.get("one_stream", depth > 1), "sequential": seq,
                      "note": "value: every step submits one sweep to ripser.SweepPipeline; up to `coalesce` consecutive "
                              "sweeps run as one call over their concatenated layers (each step's future returns its own "
                              "sweep), `depth` calls in flight on separate workspace slots; sequential: one "
                              "ripser_batch call per step, one at a time"} if piped else None,
+    }
+
+
+def measure_dropin(pkg, torch, name: str, steps: int, warmup: int, L: int) -> dict:
+    """The drop-in at the reference's own call: a step is the reference's
+    layer loop -- ``result = ripser(cloud, maxdim=1); dgms = result['dgms']`` for each of the L
+    layers, one call per layer (debug_tda_pipeline.py:109-110; analyze_adversarial_tda.py:100):
+    host numpy (N, 3) f32 in, ripser.py's full dict out (dgms, num_edges, the (N, N) dperm2all
+    distance matrix, ...).  One call at a time, so the rate is the per-call latency floor."""
+    _, maxdim, desc, _, _ = WORKLOADS[name]
+    X = make_workload(name, L)
+    n, d = X.shape[1], X.shape[2]
+    for i in range(max(warmup, 1) * L):
+        pkg.ripser(X[i % L], maxdim=maxdim)["dgms"]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for l in range(L):
+            dgms = pkg.ripser(X[l], maxdim=maxdim)["dgms"]  # noqa: F841  (the reference reads result['dgms'])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    sr = stage_roofline(pkg.ripser_batch, name, X[:1], 1, n, d, maxdim, {}, 10)
+    return {
+        "value": L * steps / el, "unit": "layers/s", "ms_per_step": el / steps * 1e3, "steps": steps, "warmup": warmup,
+        "ms_per_call": el / (steps * L) * 1e3, "device_ms_per_step": None, "X_host": X, "maxdim": maxdim,
+        "config": {"workload": desc, "layers_per_gpu_step": L, "n_points": int(n), "dim": int(d), "maxdim": maxdim,
+                   "calls_per_step": L},
+        **sr, "pipeline": None,
+        "note": "one ripser() call per layer, one at a time: the rate is set by the per-call latency (host wrapper, "
+                "input copy, the captured graph's launch and its device time, result copy incl. dperm2all), not by "
+                "throughput -- ripser_batch / SweepPipeline are the throughput entries",
     }
 
 
@@ -486,15 +571,40 @@ def summary(out: dict) -> dict:
     return rows
 
 
+def parent_cpu_baseline(args) -> str | None:
+    """``--gpus N`` without torchrun: the launching process measures the
+    CPU baseline BEFORE any rank touches a GPU -- 1 core and P = 16 x N worker processes (the
+    job's host share, 16 per GPU), the whole host (os.cpu_count()) at N >= 8 -- and hands it to
+    rank 0 through a file.  Returns the file path (None with --no-cpu)."""
+    if args.no_cpu:
+        return None
+    import multiprocessing as mp
+    import tempfile
+
+    nproc = os.cpu_count() or 1
+    P = int(os.environ.get("TDA_CPU_WORKERS", 0)) or (nproc if args.gpus >= 8 else min(nproc, 16 * args.gpus))
+    L, maxdim = args.layers or WORKLOADS[args.workload][0], WORKLOADS[args.workload][1]
+    X = workload_layers(args.workload, L)
+    with mp.get_context("spawn").Pool(P) as pool:
+        pool.map(_cpu_layers, [(args.workload, 0, 0, 0)] * P)  # warm: imports, oracle load
+        cb = cpu_baseline(pool, P, args.workload, X, maxdim, args.cpu_seconds)
+    cb.update(cpu_info())
+    cb["measured_by"] = f"the launching process, before the {args.gpus} ranks started (P = {P} worker processes measured)"
+    fd, path = tempfile.mkstemp(prefix="tda_bench_cpu_", suffix=".json")
+    with os.fdopen(fd, "w") as f:
+        json.dump(cb, f)
+    return path
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: the workload's own (WORKLOADS)")
     ap.add_argument("--warmup", type=int, default=None, help="default: the workload's own (WORKLOADS)")
     ap.add_argument("--layers", type=int, default=None)
-    ap.add_argument("--workload", default="sweep48", choices=list(WORKLOADS))
-    ap.add_argument("--extra", default="sweep48_L1,sweep48_L4,grid144,torus1024,torus1024x32,torus2048,torus2048_h2,raw4096,"
-                                       "umap36,sweep48x4,sweep48_host",
+    ap.add_argument("--workload", default="sweep48_host", choices=list(WORKLOADS))
+    ap.add_argument("--extra", default="sweep48,sweep48_L1,sweep48_L4,grid144,torus1024,torus1024x32,torus2048,torus2048_h2,"
+                                       "raw4096,umap36,sweep48x4,ripser36,ripser324",
                     help="secondary workloads measured at N=1 (comma list, '' for none)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -507,7 +617,15 @@ def main():
         args.warmup = WORKLOADS[args.workload][4]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))  # the ranks print the JSON line (rank 0)
+        cpu_file = parent_cpu_baseline(args)  # before any process touches the GPU
+        try:
+            env_argv = sys.argv[1:]
+            if cpu_file:
+                os.environ["TDA_BENCH_CPU_FILE"] = cpu_file
+            sys.exit(launch_ranks(args.gpus, env_argv))  # the ranks print the JSON line (rank 0)
+        finally:
+            if cpu_file and os.path.exists(cpu_file):
+                os.unlink(cpu_file)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -555,35 +673,39 @@ def main():
 
     L, maxdim, desc, _, _ = WORKLOADS[args.workload]
     L = args.layers or L
-    prim, strong = None, None
+    prim, strong, multi_roof = None, None, None
     if world == 1:
         prim = measure(pkg, torch, dev, args.workload, args.steps, args.warmup, args.layers)
         value, el_ms = prim["value"], prim["ms_per_step"]
     else:
-        X_host = make_workload(args.workload, L)
-        X = X_host if standin else torch.from_numpy(X_host).to(dev)
+        host_in = args.workload.endswith("_host")
+        sweeps = workload_sweeps(args.workload, L)
+        Xs = sweeps if (standin or host_in) else [torch.from_numpy(x).to(dev) for x in sweeps]
         # the same dynamic batching as the one-GPU record (bench PIPE): each rank's steps through a SweepPipeline
         slots, coalesce = pipe_shape(args.workload, args.steps)
         sync = (lambda: None) if standin else torch.cuda.synchronize
+        gpu_ix = None if standin else local
+        K = len(Xs)
 
         def run_multi(shard: bool):
             sync()
-            for _ in range(args.warmup):
-                pkg.distributed.sharded_sweep_step(X, maxdim, rank, world, device=coll_dev, shard=shard, run=standin)
+            for i in range(args.warmup):
+                pkg.distributed.sharded_sweep_step(Xs[i % K], maxdim, rank, world, device=coll_dev, shard=shard, run=standin,
+                                                   gpu=gpu_ix)
             if slots > 1 or coalesce > 1:  # every slot captures its graphs before the timed region
-                warm = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
-                                                      coalesce=coalesce, run=standin)
-                for _ in range(max(args.warmup, 1) * slots * coalesce):
-                    warm.step()
+                warm = pkg.distributed.PipelinedSweep(Xs[0], maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
+                                                      coalesce=coalesce, run=standin, gpu=gpu_ix)
+                for i in range(max(max(args.warmup, 1) * slots * coalesce, K * slots)):
+                    warm.step(Xs[i % K])
                 warm.close()
             dist.barrier()
             sync()
             t0 = time.perf_counter()
             # every step's records are exchanged; the exchange of step i overlaps the GPU work of later steps
-            pipe = pkg.distributed.PipelinedSweep(X, maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
-                                                  coalesce=coalesce, run=standin)
-            for _ in range(args.steps):
-                pipe.step()
+            pipe = pkg.distributed.PipelinedSweep(Xs[0], maxdim, rank, world, device=coll_dev, shard=shard, slots=slots,
+                                                  coalesce=coalesce, run=standin, gpu=gpu_ix)
+            for i in range(args.steps):
+                pipe.step(Xs[i % K])
             pipe.close()
             sync()
             dist.barrier()
@@ -597,6 +719,18 @@ def main():
         el_s = run_multi(True) if args.scaling == "weak" else el
         strong = {"value": L * args.steps / el_s, "unit": "layers/s", "ms_per_step": el_s / args.steps * 1e3,
                   "scaling": "strong", "layers_total": L, "layers_per_gpu": -(-L // world)}
+        if rank == 0:
+            # the line's roofline: rank 0's own GPU, the weak step's per-rank batch (the same stage pass as the
+            # one-GPU record), after every rank's timed region
+            Lk = L * coalesce if coalesce > 1 else L
+            Xst = [Xs[i % K] for i in range(coalesce)] if coalesce > 1 else Xs[0]
+            run = standin or pkg.ripser_batch
+            kw = dict(CALL_KW.get(args.workload, {}))
+            if not standin:
+                kw["device"] = local
+            multi_roof = stage_roofline(run, args.workload, Xst, Lk, int(sweeps[0].shape[1]), int(sweeps[0].shape[2]), maxdim,
+                                        kw, max(1, min(args.steps, 10)))
+        dist.barrier()
 
     out = None
     if rank == 0:
@@ -607,15 +741,17 @@ def main():
             "config": {"workload": desc, "workload_name": args.workload,
                        "layers_per_gpu_step": L if args.scaling == "weak" else -(-L // world),
                        "n_points": NPOINTS[args.workload], "dim": DIMS[args.workload], "maxdim": maxdim,
+                       "distinct_sweeps": ROTATE.get(args.workload, 1),
                        "parallelism": f"layers sharded ({args.scaling}), {world} process(es) on {n_gpus} GPU(s), "
                                       f"{'RCCL' if backend == 'nccl' else backend} gather of per-layer records "
                                       f"(overlapped with the next step's GPU work)"},
-            "roofline": prim["roofline"] if prim else None,
+            "roofline": prim["roofline"] if prim else (multi_roof or {}).get("roofline"),
             "cpu_baseline": None,
         }
         if standin:
             out["rehearsal"] = {"kind": "cpu stand-in (no GPU)", "standin": os.environ["TDA_BENCH_STANDIN"],
-                                "note": "multi-rank launch + gloo collectives rehearsed on the CPU; not a GPU measurement"}
+                                "note": "multi-rank launch + gloo collectives rehearsed on the CPU; not a GPU measurement "
+                                        "(the roofline's stages are the stand-in's)"}
         elif world > n_gpus:
             out["rehearsal"] = {"kind": f"{world} ranks on {n_gpus} GPU(s) over gloo", "note": "not a multi-GPU measurement"}
         if prim:
@@ -624,12 +760,24 @@ def main():
             out["device_ms_per_step"] = prim["device_ms_per_step"]
             out["stages_ms"] = prim["stages_ms"]
             out["pipeline"] = prim["pipeline"]
+        elif multi_roof:
+            out["stages_ms"] = multi_roof["stages_ms"]
+            if multi_roof.get("roofline_mfma"):
+                out["roofline_mfma"] = multi_roof["roofline_mfma"]
         if strong:
             out["strong"] = strong
         if world > 1 and (slots > 1 or coalesce > 1):
             out["pipeline"] = {"depth": slots, "coalesce": coalesce, "note": "each rank's steps through ripser.SweepPipeline "
                                "(as the one-GPU record); the records of every `coalesce` steps exchanged in one "
                                "all-reduce + gather, in step order"}
+        cpu_file = os.environ.get("TDA_BENCH_CPU_FILE")
+        if world > 1 and cpu_file and os.path.exists(cpu_file):  # measured by the launching process
+            with open(cpu_file) as f:
+                cb = json.load(f)
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu"] = speedups(value, cb, args.workload)
+            if strong:
+                strong["speedup_vs_cpu"] = speedups(strong["value"], cb, args.workload)
     if rank == 0 and world == 1:
         cpu_done = {}
         if do_cpu:
@@ -643,12 +791,15 @@ def main():
             if w == "umap36":
                 out["workloads"][w] = measure_umap(pkg, torch, dev)
                 continue
+            if w == "ripser324" and not os.path.exists(os.path.join(ROOT, "tests", "golden", "adv_clouds.npz")):
+                continue
             _, _, _, st, wu = WORKLOADS[w]
             m = measure(pkg, torch, dev, w, st, wu)
             rec = {k: m[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "device_ms_per_step",
-                                     "config", "roofline", "roofline_mfma", "stages_ms", "pipeline")}
-            if rec["roofline_mfma"] is None:
-                del rec["roofline_mfma"]
+                                     "config", "roofline", "roofline_mfma", "stages_ms", "pipeline", "ms_per_call", "note")
+                   if k in m}
+            if rec.get("roofline_mfma") is None:
+                rec.pop("roofline_mfma", None)
             rec["data"] = DATA[w]
             if do_cpu:
                 same = CPU_SAME.get(w)

@@ -575,10 +575,14 @@ int hip_runtimes_loaded() {
 // handle from another runtime, a destroyed stream or garbage is refused with
 // TDA_E_HIP instead of being dereferenced by hipEventRecord.
 int order_after_caller(hipStream_t lib, hipEvent_t ev, void* caller, int dev) {
+    // counted once per process (dl_iterate_phdr + stat per call cost ~10 us).  With
+    // a second runtime mapped, NULL would be THIS runtime's null stream, not the caller's default
+    // stream, so neither a handle nor NULL orders anything: the caller must pass the input ready
+    static const int n_rt = hip_runtimes_loaded();
+    if (n_rt > 1)
+        return fail(TDA_E_HIP, "two HIP runtimes are loaded in this process: the caller's stream (a handle or NULL) cannot "
+                               "be ordered against (pass the input ready instead, TDA_FLAG_INPUT_READY)");
     if (caller) {
-        if (hip_runtimes_loaded() > 1)
-            return fail(TDA_E_HIP, "two HIP runtimes are loaded in this process: a caller stream handle cannot be trusted "
-                                   "(pass the input ready instead, TDA_FLAG_INPUT_READY)");
         hipDevice_t d = -1;
         const hipError_t e = hipStreamGetDevice((hipStream_t)caller, &d);
         if (e != hipSuccess) {

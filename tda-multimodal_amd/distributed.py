@@ -104,7 +104,7 @@ def gather_records(records: list, n_layers: int, dist=None, device=None) -> list
 
 
 def sharded_sweep_step(X, maxdim: int, rank: int, world: int, dist=None, device=None, layer_base: int = 0,
-                       shard: bool = True, run=None):
+                       shard: bool = True, run=None, gpu: int | None = None):
     """One multi-GPU step of the layer sweep (bench.py runs exactly this).
 
     X: the (L, N, D) sweep (resident on this rank's GPU, or numpy).
@@ -114,12 +114,16 @@ def sharded_sweep_step(X, maxdim: int, rank: int, world: int, dist=None, device=
                 [rank * L, (rank + 1) * L) of a world * L sweep.
     run: the per-shard batch call (default ``ripser_batch``; CPU tests pass
     an oracle-backed stand-in with the same result interface).
+    gpu: the GPU ordinal of this rank for host (numpy) input (a CUDA tensor
+    runs on its own device).
     Returns the gathered packed rows (sorted by layer) and the capacity on
     rank 0, (None, None) elsewhere.
     """
+    import functools
+
     from .ripser import ripser_batch
 
-    run = run or ripser_batch
+    run = run or (functools.partial(ripser_batch, device=gpu) if gpu is not None else ripser_batch)
     L = int(X.shape[0])
     if shard:
         lo, hi = shard_range(L, rank, world)
@@ -153,14 +157,15 @@ class PipelinedSweep:
     """
 
     def __init__(self, X, maxdim: int, rank: int, world: int, dist=None, device=None, layer_base: int = 0,
-                 shard: bool = True, run=None, depth: int = 2, slots: int = 1, coalesce: int = 1):
+                 shard: bool = True, run=None, depth: int = 2, slots: int = 1, coalesce: int = 1, gpu: int | None = None):
+        import functools
         import queue
         import threading
 
         from .ripser import ripser_batch
 
         self.X, self.maxdim, self.dist, self.device = X, maxdim, dist, device
-        self.run = run or ripser_batch
+        self.run = run or (functools.partial(ripser_batch, device=gpu) if gpu is not None else ripser_batch)
         L = int(X.shape[0])
         if shard:
             self.lo, self.hi = shard_range(L, rank, world)
@@ -173,7 +178,8 @@ class PipelinedSweep:
         if slots > 1 or coalesce > 1:
             from .ripser import SweepPipeline
 
-            gpu = getattr(X, "is_cuda", False)
+            on_gpu = getattr(X, "is_cuda", False)
+
             def prun(Xs, maxdim, **_):  # a stand-in batch call takes one array: join the parts
                 if isinstance(Xs, list):
                     Xs = np.concatenate([np.asarray(x) for x in Xs]) if not getattr(Xs[0], "is_cuda", False) else \
@@ -182,13 +188,13 @@ class PipelinedSweep:
 
             prun = None if run is None else prun
             extra = {}
-            if gpu and run is None:  # X is fixed for every step: complete it once, then no per-call stream event
+            if on_gpu and run is None:  # the inputs are complete before the first step: no per-call stream event
                 import torch
 
                 torch.cuda.current_stream(X.device).synchronize()
                 extra["input_ready"] = True
-            self.pipe = SweepPipeline(depth=slots, device=X.device.index if gpu else 0, coalesce=coalesce, maxdim=maxdim,
-                                      run=prun, **extra)
+            self.pipe = SweepPipeline(depth=slots, device=X.device.index if on_gpu else (gpu or 0), coalesce=coalesce,
+                                      maxdim=maxdim, run=prun, **extra)
         self.q = queue.Queue(maxsize=max(1, depth) + (slots * coalesce if self.pipe else 0))
         self.group = coalesce if self.pipe else 1  # steps per exchange
         self.world = world
@@ -238,15 +244,18 @@ class PipelinedSweep:
         last[:, 0] -= (k - 1) * self.total
         self.last = (last, cap)
 
-    def step(self):
+    def step(self, X=None):
+        """One step over X (default: the constructor's X; another sweep of the same
+        shape, e.g. the bench's rotation of distinct sweeps)."""
         if self.err is not None:
             raise self.err
+        X = self.X if X is None else X
         if self.hi <= self.lo:
             res = []
         elif self.pipe is not None:
-            res = self.pipe.submit(self.X[self.lo:self.hi])
+            res = self.pipe.submit(X[self.lo:self.hi])
         else:
-            res = self.run(self.X[self.lo:self.hi], maxdim=self.maxdim)
+            res = self.run(X[self.lo:self.hi], maxdim=self.maxdim)
         self.q.put(res)  # blocks while the worker is `depth` exchanges (+ the pipeline's steps in flight) behind
         self.steps += 1
 

@@ -496,7 +496,6 @@ class SweepPipeline:
         self._n = 0
         self._lock = threading.Lock()
         self._pending = []  # (X, args, future, producer event or None) not yet dispatched
-        self._streams = [None] * depth  # per executor: the side stream its calls order their reads after
         self._pkey = None
         self._run = run  # the batch call (default ripser_batch; CPU tests pass a stand-in)
 
@@ -570,21 +569,16 @@ class SweepPipeline:
         evs = [b[3] for b in batch if b[3] is not None]
         X = Xs[0] if len(Xs) == 1 else Xs  # parts: gathered on the device by the library (ABI 6)
         if evs:
-            # every part's producer, as recorded at its submit(): the call runs on a side stream
-            # of this executor that waits on all of them, and the library orders its reads
-            # after that stream
-            import torch
-
-            dev = Xs[0].device
-            if self._streams[e] is None:
-                self._streams[e] = torch.cuda.Stream(dev)
-            ws = self._streams[e]
+            # every part's producer, as recorded at its submit(): the slot's worker thread waits
+            # for those events on the host, then calls with the input marked complete -- no extra
+            # HIP stream per slot, whose hardware queue could be shared with another slot's
+            # library stream
+            args["input_ready"] = True
 
             def call():
                 for ev in evs:
-                    ws.wait_event(ev)
-                with torch.cuda.stream(ws):
-                    return run(X, device=self.device, slot=s, **args)
+                    ev.synchronize()
+                return run(X, device=self.device, slot=s, **args)
 
             cf = self._ex[e].submit(call)
         else:

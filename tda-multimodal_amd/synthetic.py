@@ -22,17 +22,18 @@ def reference_clouds() -> np.ndarray:
     return np.stack([z[f"layer_{l}"] for l in range(32)]).astype(np.float32)
 
 
-def layer48(l: int, clouds: np.ndarray | None = None) -> np.ndarray:
-    """C1/C2/C3: 48-point layer = cloud_l[i % 36] + N(0, (0.02 std(cloud_l))^2), seed 1000+l."""
+def layer48(l: int, clouds: np.ndarray | None = None, variant: int = 0) -> np.ndarray:
+    """C1/C2/C3: 48-point layer = cloud_l[i % 36] + N(0, (0.02 std(cloud_l))^2), seed 1000+l
+    (variant v > 0: seed 1000 + l + 100000 v -- another sweep of the same shape)."""
     c = reference_clouds()[l] if clouds is None else clouds[l]
-    rng = np.random.default_rng(1000 + l)
+    rng = np.random.default_rng(1000 + l + 100000 * variant)
     idx = np.arange(48) % 36
     return (c[idx] + rng.normal(0.0, 0.02 * c.std(), (48, 3))).astype(np.float32)
 
 
-def sweep48(n_layers: int = 32) -> np.ndarray:
+def sweep48(n_layers: int = 32, variant: int = 0) -> np.ndarray:
     clouds = reference_clouds()
-    return np.stack([layer48(l % 32, clouds) for l in range(n_layers)])
+    return np.stack([layer48(l % 32, clouds, variant) for l in range(n_layers)])
 
 
 def torus(n: int = 1024, seed: int = 0, R: float = 2.0, r: float = 1.0) -> np.ndarray:
@@ -43,9 +44,10 @@ def torus(n: int = 1024, seed: int = 0, R: float = 2.0, r: float = 1.0) -> np.nd
     return np.stack([(R + r * np.cos(ph)) * np.cos(th), (R + r * np.cos(ph)) * np.sin(th), r * np.sin(ph)], 1).astype(np.float32)
 
 
-def grid144(l: int) -> np.ndarray:
-    """C5: 12 x 12 torus grid + N(0, 0.02^2) + random rotation, seed l."""
-    rng = np.random.default_rng(l)
+def grid144(l: int, variant: int = 0) -> np.ndarray:
+    """C5: 12 x 12 torus grid + N(0, 0.02^2) + random rotation, seed l (variant v > 0:
+    seed l + 100000 v)."""
+    rng = np.random.default_rng(l + 100000 * variant)
     i, j = np.meshgrid(np.arange(12), np.arange(12), indexing="ij")
     th = 2 * np.pi * i.ravel() / 12
     ph = 2 * np.pi * j.ravel() / 12
@@ -55,8 +57,8 @@ def grid144(l: int) -> np.ndarray:
     return (X @ Q).astype(np.float32)
 
 
-def sweep144(n_layers: int = 32) -> np.ndarray:
-    return np.stack([grid144(l) for l in range(n_layers)])
+def sweep144(n_layers: int = 32, variant: int = 0) -> np.ndarray:
+    return np.stack([grid144(l, variant) for l in range(n_layers)])
 
 
 def activations(n_layers: int = 32, n: int = 144, d: int = 4096, seed: int = 0) -> np.ndarray:
