@@ -363,7 +363,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
             // k_reduce_par: owner maps, final pivots, records, bucket chunks, requeue slots
             const uint64_t prc = p.par2 ? std::max(p.rcap[1], p.rcap[2]) : p.rcap[1];
             p.ostride = next_pow2(2 * prc + 16);
-            p.rec_cap = 2 * (uint64_t)L * prc + 4096;
+            p.rec_cap = (2 * (uint64_t)L * prc + 4096) << scale;  // a capacity retry (scale) grows every pool
             // bucket chunks: every workgroup keeps its peak bucket sizes (torus N=1024 needs ~2^26 keys
             // in all, N=2048 ~2^28); records: raw copies of the paired columns.  HBM is 288 GB.
             auto clampp = [](uint64_t x, int lo, int hi) { return std::min<uint64_t>(std::max<uint64_t>(next_pow2(x), 1ull << lo), 1ull << hi); };
@@ -379,7 +379,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
             // H2 records as well: grid144 (32 layers) stores ~4.4 M keys of reduced H2 columns
             p.rpool_cap = clampp(std::max<uint64_t>(N * N * 64 * std::min<uint64_t>(L, 8), p.par2 ? L * N * N * 8 : 0), 22, 29)
                           << (scale + big4);
-            p.rq_cap = 1ull << 16;
+            p.rq_cap = 1ull << (16 + 2 * scale);
             p.o_pctl = take(sizeof(ParCtl));
             p.o_pitem = take((L + 1) * 8);
             p.o_pokey = take(L * p.ostride * 8);

@@ -72,6 +72,15 @@ constexpr int kParRegs = 2048 / kParT;  // keys per thread per pass of refills a
 #endif
 constexpr int kParRefill = TDA_PAR_REFILL;          // a refill keeps up to kParRefill passes (4096 keys) in registers
 constexpr int kParRV = 1024 / kParT;   // coboundary vertices per thread per round (1024 per round)
+#ifndef TDA_PAR_SB  // r06 A/B: the room check's LDS reads batched with the front scan (one round trip less per step)
+#define TDA_PAR_SB 0
+#endif
+#ifndef TDA_PAR_TF  // r06 A/B: toggles skip the wave stage when no lane holds two front keys
+#define TDA_PAR_TF 0
+#endif
+#ifndef TDA_PAR_RS  // r06 A/B: refill barriers that only order LDS do not wait for the bucket stores
+#define TDA_PAR_RS 0
+#endif
 // vertex of thread t in slot q of the coboundary round starting at v0.  (r05: the odd slots
 // mirrored -- wave w taking 64-vertex blocks w and 2 W - 1 - w, to spread the waves' unequal key
 // counts -- measured no faster: torus1024 34.3 ms either way)
@@ -382,8 +391,13 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
     }
     if (!wtot) return;
     uint32_t ins = 0;
-    if (wtot <= 64 && R == 1) {  // one key per lane already
-        if (vmask & 1u) ins = tab_toggle(k[0]);
+    uint64_t two = 0;  // lanes holding more than one key of the pass
+#pragma unroll
+    for (int r = 1; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < r; ++q) two |= m[r] & m[q];
+    if (R == 1 || (TDA_PAR_TF && R == 2 && !two)) {  // at most one key per lane: toggle it in place (no stage round trip)
+        if (vmask) ins = tab_toggle((vmask & 1u) ? k[0] : k[R - 1]);
     } else {
         uint32_t off = 0;
 #pragma unroll
@@ -412,7 +426,7 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
 // above its pivot, so the cache empties within ~1.5 steps (a replay of the
 // longest column's key trace: 33 % of the minima served; 80 % would need the
 // 128 smallest keys, which no longer avoids a block-wide reduction).)
-__device__ __forceinline__ uint64_t front_min(ParRed& rd) {
+__device__ __forceinline__ uint64_t front_scan() {  // this thread's share of the front minimum
     uint64_t b = kEmpty64;
 #pragma unroll
     for (uint32_t q = 0; q < kTabPer; q += 2) {  // slots 2 t, 2 t + 1 of each 2 kParT block
@@ -420,9 +434,9 @@ __device__ __forceinline__ uint64_t front_min(ParRed& rd) {
         b = v.x < b ? v.x : b;
         b = v.y < b ? v.y : b;
     }
-    b = b < kDead ? b : kEmpty64;
-    return rd.min(b);
+    return b < kDead ? b : kEmpty64;
 }
+__device__ __forceinline__ uint64_t front_min(ParRed& rd) { return rd.min(front_scan()); }
 
 // Rebuild the table with the live keys of level <= keep (relative to
 // PS.last): read every slot, clear, re-insert.  Returns the live count kept
@@ -550,9 +564,14 @@ __device__ __forceinline__ uint32_t p2_now() {
 // Barrier, then room in the front for `need` more log entries: compact, and
 // spill the highest front levels to HBM if too many keys are live.
 constexpr uint32_t kFrontRoom = kTabMax;
+__device__ __forceinline__ void front_room_slow(ParCol& C, const ParBufs& P, uint32_t need);
 __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t need) {
     lds_sync();
     if (PS.fcnt + need <= kFrontRoom) return;
+    front_room_slow(C, P, need);
+}
+// compact the front, and spill its highest levels to HBM if too many keys are live
+__device__ __forceinline__ void front_room_slow(ParCol& C, const ParBufs& P, uint32_t need) {
     PAR_T0(tc0);
     uint32_t w = front_compact(C.rd, kParLv);
 #ifdef TDA_PROFILE
@@ -583,7 +602,11 @@ __device__ __forceinline__ void front_room(ParCol& C, const ParBufs& P, uint32_t
             uint64_t x[1] = {e < ns ? PS.log[e] : kEmpty64};
             uint32_t b[1] = {x[0] < kDead ? par_bucket(x[0], last) : 0};
             bucket_append<1>(x, b, (x[0] < kDead && b[0] > (uint32_t)keep) ? 1u : 0u, P);
+#if TDA_PAR_RS
+            lds_sync();  // chunk pointers opened by this pass (LDS only: the stores stay in flight)
+#else
             __syncthreads();  // chunk pointers opened by this pass
+#endif
         }
         if (threadIdx.x == 0) PS.kf = (uint32_t)keep;
         front_compact(C.rd, (uint32_t)keep);
@@ -726,7 +749,11 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     // pass 3: distribute (front: toggles; below b: appends to empty lower buckets)
     auto distribute = [&](const uint64_t (&y)[kParRegs], uint32_t ym) {
         // the front takes at most kFrontLive keys in all: compaction keeps room
+#if TDA_PAR_RS
+        lds_sync();  // chunk pointers opened by the previous pass (LDS only: its bucket stores stay in flight)
+#else
         __syncthreads();  // chunk pointers opened by the previous pass
+#endif
         if (PS.fcnt + kParRegs * kParT > kFrontRoom) front_compact(C.rd, kParLv);
         PAR_Q3(6);
         uint32_t fm = 0, bm = 0, bb[kParRegs];
@@ -760,7 +787,11 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
             distribute(y, ym);
         }
     }
+#if TDA_PAR_RS
+    lds_sync();  // the front and the counters; the bucket stores are ordered by the next refill's full barrier
+#else
     __syncthreads();
+#endif
 #ifdef TDA_PROFILE
     C.q2[5] += clock64() - t3;
 #endif
@@ -1308,9 +1339,24 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #endif
         for (; !done; ++step) {
             P2_T(ps0);
+#if TDA_PAR_SB
+            // the barrier, then the room check's reads issued with the front scan (one LDS round trip)
+            lds_sync();  // the previous step's toggles and appends are done
+            const uint32_t fc0 = PS.fcnt;
+            const int32_t er0 = PS.err;
+            uint64_t lmin = front_scan();
+            if (er0) break;
+            if (fc0 + need > kFrontRoom) {
+                front_room_slow(C, P, need);
+                if (PS.err) break;
+                lmin = front_scan();
+            }
+            P2_ACC(0, ps0);
+#else
             front_room(C, P, need);  // barrier: the previous step's toggles and appends are done
             P2_ACC(0, ps0);
             if (PS.err) break;
+#endif
             if (step > P.step_limit) {
                 if (tid == 0) PS.err = 61;
                 break;
@@ -1320,7 +1366,11 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             uint64_t t0 = clock64();
 #endif
             P2_T(ps1);
+#if TDA_PAR_SB
+            uint64_t pk = C.rd.min(lmin);
+#else
             uint64_t pk = front_min(C.rd);
+#endif
             P2_ACC(1, ps1);
 #ifdef TDA_PROFILE
             pf[1] += clock64() - t0;
