@@ -189,6 +189,7 @@ ReduceAllCfg reduce_cfg(int n, int maxdim, const uint64_t* piv_words, bool lds_m
     return c;
 }
 
+constexpr int kMaxParScale = 4;  // k_reduce_par capacity retries: pools up to 16x
 // no_par: 0 = k_reduce_par for H1 and H2, 1 = H1 only (an H2 launch aborted), 2 = none
 int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par) {
     const uint64_t N = (uint64_t)p.N, L = (uint64_t)p.L;
@@ -203,10 +204,13 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     p.pcap[0] = N + 1;
     p.max_rcap = std::max<uint64_t>(p.max_rcap, 1);
     p.rmap_stride = next_pow2(2 * p.max_rcap + 16);
-    p.vpool_cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 16, 32 * p.max_rcap), 1ull << 27) << scale;
+    // capacity retries: `scale` grows the parallel reducer's pools up to 16x (kMaxParScale); the
+    // other work buffers (serial reducers) grow up to 4x
+    const int s2 = std::min(scale, 2);
+    p.vpool_cap = std::min<uint64_t>(std::max<uint64_t>(1ull << 16, 32 * p.max_rcap), 1ull << 27) << s2;
     p.lds_mode = p.N <= kSmallN && !force_global;
     p.rcfg = reduce_cfg((int)N, p.maxdim, p.piv_words, p.lds_mode);
-    p.wcap_g = (N <= 256 ? 1ull << 17 : (N <= 640 ? 1ull << 21 : 1ull << 23)) << (2 * scale);
+    p.wcap_g = (N <= 256 ? 1ull << 17 : (N <= 640 ? 1ull << 21 : 1ull << 23)) << (2 * s2);
     {
         const char* m = test_env("TDA_REDUCE");
         // measured (r01): one wave per layer beats the serial radix heap up to
@@ -379,7 +383,7 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
             // H2 records as well: grid144 (32 layers) stores ~4.4 M keys of reduced H2 columns
             p.rpool_cap = clampp(std::max<uint64_t>(N * N * 64 * std::min<uint64_t>(L, 8), p.par2 ? L * N * N * 8 : 0), 22, 29)
                           << (scale + big4);
-            p.rq_cap = 1ull << (16 + 2 * scale);
+            p.rq_cap = 1ull << (16 + scale);  // memset per launch: 0.5 MB at scale 0
             p.o_pctl = take(sizeof(ParCtl));
             p.o_pitem = take((L + 1) * 8);
             p.o_pokey = take(L * p.ostride * 8);
@@ -631,6 +635,56 @@ void drop_graphs(Workspace& w) {
     ++w.gen;
 }
 
+// ------------------------------------------------------------------ build consistency
+// hipcc compiles this file twice (device pass, then host pass minutes later) and both read the
+// headers; an edit in between once gave a library whose host side packed kernel arguments
+// differently from what the device side read.  The first workspace of the
+// process checks the sizes of every structure that crosses the host/device boundary, as the
+// device code sees them, against the host's: a skewed build fails loudly instead of faulting.
+#define TDA_LAYOUT_STRUCTS(X)                                                                                     \
+    X(LayerStats) X(DimBufs) X(Pair) X(PairSet) X(OutPair) X(AppBlock) X(PartList) X(SortArgs) X(Reduce2Bufs)  \
+    X(Reduce2Cfg) X(ReduceAllCfg) X(SmallBufs) X(BigBufs) X(DenseBufs) X(ParCtl) X(ParBufs) X(ParLds)
+#define TDA_LAYOUT_COUNT(T) +1
+constexpr int kLayoutN = 0 TDA_LAYOUT_STRUCTS(TDA_LAYOUT_COUNT);
+__global__ void k_layout_probe(uint32_t* out) {
+    if (threadIdx.x != 0) return;
+    int i = 0;
+#define TDA_LAYOUT_DEV(T) out[i++] = (uint32_t)sizeof(T);
+    TDA_LAYOUT_STRUCTS(TDA_LAYOUT_DEV)
+#undef TDA_LAYOUT_DEV
+}
+int check_layout(hipStream_t s) {
+    static std::mutex mu;
+    static bool done = false;
+    std::lock_guard<std::mutex> g(mu);
+    if (done) return 0;
+    uint32_t* d = nullptr;
+    uint32_t h[kLayoutN] = {};
+    HIPC(hipMalloc(&d, sizeof(h)));
+    hipLaunchKernelGGL(k_layout_probe, dim3(1), dim3(64), 0, s, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(TDA_E_HIP, std::string("layout probe: ") + hipGetErrorString(e));
+    static const char* names[kLayoutN] = {
+#define TDA_LAYOUT_NAME(T) #T,
+        TDA_LAYOUT_STRUCTS(TDA_LAYOUT_NAME)
+#undef TDA_LAYOUT_NAME
+    };
+    const uint32_t host[kLayoutN] = {
+#define TDA_LAYOUT_HOST(T) (uint32_t)sizeof(T),
+        TDA_LAYOUT_STRUCTS(TDA_LAYOUT_HOST)
+#undef TDA_LAYOUT_HOST
+    };
+    for (int i = 0; i < kLayoutN; ++i)
+        if (h[i] != host[i])
+            return fail(TDA_E_HIP, std::string("library build is inconsistent: sizeof(") + names[i] + ") is " + std::to_string(host[i]) +
+                                       " on the host and " + std::to_string(h[i]) + " on the device (rebuild from one source tree)");
+    done = true;
+    return 0;
+}
+
 int ws_side_streams(Workspace& w) {
     if (w.stream2) return 0;
     HIPC(hipStreamCreateWithFlags(&w.stream2, hipStreamNonBlocking));
@@ -653,6 +707,7 @@ int ws_prepare(Workspace& w, const Plan& p) {
         HIPC(hipEventCreateWithFlags(&w.evf, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evj, hipEventDisableTiming));
         HIPC(hipEventCreateWithFlags(&w.evin, hipEventDisableTiming));
+        if (int rc = check_layout(w.stream)) return rc;
         w.init = true;
     }
     if (w.dcap < p.total) {
@@ -1826,7 +1881,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                     c.evictions, c.rec_used, c.rpool_used, c.bpool_used);
         const unsigned code = (unsigned)(c.err & 0xFFFF);
         const bool capacity = code == 21 || code == 22 || code == 41 || code == 53;  // pools / requeue slots
-        if (capacity && scale < 2) {  // the same parallel reduction with larger pools
+        // (a noisy circle at N = 1024 needs ~450 M bucket keys for its one long column, 4x the
+        // first pool; a sphere's H2 at N = 1024 more: tools/cap_miss.py)
+        if (capacity && scale < kMaxParScale) {  // the same parallel reduction with larger pools
             guard.unlock();
             return run_pipeline(a, input_kind, host_or_dev, out, force_global, scale + 1, force_big, no_par, no_cap);
         }

@@ -72,15 +72,6 @@ constexpr int kParRegs = 2048 / kParT;  // keys per thread per pass of refills a
 #endif
 constexpr int kParRefill = TDA_PAR_REFILL;          // a refill keeps up to kParRefill passes (4096 keys) in registers
 constexpr int kParRV = 1024 / kParT;   // coboundary vertices per thread per round (1024 per round)
-#ifndef TDA_PAR_SB  // r06 A/B: the room check's LDS reads batched with the front scan (one round trip less per step)
-#define TDA_PAR_SB 0
-#endif
-#ifndef TDA_PAR_TF  // r06 A/B: toggles skip the wave stage when no lane holds two front keys
-#define TDA_PAR_TF 0
-#endif
-#ifndef TDA_PAR_RS  // r06 A/B: refill barriers that only order LDS do not wait for the bucket stores
-#define TDA_PAR_RS 0
-#endif
 // vertex of thread t in slot q of the coboundary round starting at v0.  (r05: the odd slots
 // mirrored -- wave w taking 64-vertex blocks w and 2 W - 1 - w, to spread the waves' unequal key
 // counts -- measured no faster: torus1024 34.3 ms either way)
@@ -391,13 +382,10 @@ __device__ __forceinline__ void front_toggle(const uint64_t (&k)[R], uint32_t vm
     }
     if (!wtot) return;
     uint32_t ins = 0;
-    uint64_t two = 0;  // lanes holding more than one key of the pass
-#pragma unroll
-    for (int r = 1; r < R; ++r)
-#pragma unroll
-        for (int q = 0; q < r; ++q) two |= m[r] & m[q];
-    if (R == 1 || (TDA_PAR_TF && R == 2 && !two)) {  // at most one key per lane: toggle it in place (no stage round trip)
-        if (vmask) ins = tab_toggle((vmask & 1u) ? k[0] : k[R - 1]);
+    // (r06: lanes with at most one key toggling it in place, skipping the stage, measured no faster:
+    // torus1024 33.45 vs 33.43 ms)
+    if (wtot <= 64 && R == 1) {  // one key per lane already
+        if (vmask & 1u) ins = tab_toggle(k[0]);
     } else {
         uint32_t off = 0;
 #pragma unroll
@@ -602,11 +590,7 @@ __device__ __forceinline__ void front_room_slow(ParCol& C, const ParBufs& P, uin
             uint64_t x[1] = {e < ns ? PS.log[e] : kEmpty64};
             uint32_t b[1] = {x[0] < kDead ? par_bucket(x[0], last) : 0};
             bucket_append<1>(x, b, (x[0] < kDead && b[0] > (uint32_t)keep) ? 1u : 0u, P);
-#if TDA_PAR_RS
-            lds_sync();  // chunk pointers opened by this pass (LDS only: the stores stay in flight)
-#else
             __syncthreads();  // chunk pointers opened by this pass
-#endif
         }
         if (threadIdx.x == 0) PS.kf = (uint32_t)keep;
         front_compact(C.rd, (uint32_t)keep);
@@ -749,11 +733,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
     // pass 3: distribute (front: toggles; below b: appends to empty lower buckets)
     auto distribute = [&](const uint64_t (&y)[kParRegs], uint32_t ym) {
         // the front takes at most kFrontLive keys in all: compaction keeps room
-#if TDA_PAR_RS
-        lds_sync();  // chunk pointers opened by the previous pass (LDS only: its bucket stores stay in flight)
-#else
         __syncthreads();  // chunk pointers opened by the previous pass
-#endif
         if (PS.fcnt + kParRegs * kParT > kFrontRoom) front_compact(C.rd, kParLv);
         PAR_Q3(6);
         uint32_t fm = 0, bm = 0, bb[kParRegs];
@@ -787,11 +767,7 @@ __device__ __forceinline__ bool col_refill(ParCol& C, const ParBufs& P) {
             distribute(y, ym);
         }
     }
-#if TDA_PAR_RS
-    lds_sync();  // the front and the counters; the bucket stores are ordered by the next refill's full barrier
-#else
     __syncthreads();
-#endif
 #ifdef TDA_PROFILE
     C.q2[5] += clock64() - t3;
 #endif
@@ -1339,24 +1315,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #endif
         for (; !done; ++step) {
             P2_T(ps0);
-#if TDA_PAR_SB
-            // the barrier, then the room check's reads issued with the front scan (one LDS round trip)
-            lds_sync();  // the previous step's toggles and appends are done
-            const uint32_t fc0 = PS.fcnt;
-            const int32_t er0 = PS.err;
-            uint64_t lmin = front_scan();
-            if (er0) break;
-            if (fc0 + need > kFrontRoom) {
-                front_room_slow(C, P, need);
-                if (PS.err) break;
-                lmin = front_scan();
-            }
-            P2_ACC(0, ps0);
-#else
             front_room(C, P, need);  // barrier: the previous step's toggles and appends are done
             P2_ACC(0, ps0);
             if (PS.err) break;
-#endif
             if (step > P.step_limit) {
                 if (tid == 0) PS.err = 61;
                 break;
@@ -1366,11 +1327,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             uint64_t t0 = clock64();
 #endif
             P2_T(ps1);
-#if TDA_PAR_SB
-            uint64_t pk = C.rd.min(lmin);
-#else
             uint64_t pk = front_min(C.rd);
-#endif
             P2_ACC(1, ps1);
 #ifdef TDA_PROFILE
             pf[1] += clock64() - t0;
