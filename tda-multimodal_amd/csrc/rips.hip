@@ -1407,7 +1407,14 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             // L a multiple of 8: a 1-D grid whose blocks take their layers XCD by XCD (app_block)
             const int xl = (L % 8 == 0 && !test_env_is("TDA_APP_XCD", "0")) ? L : 0;
             const dim3 ag = xl ? dim3(gx * (unsigned)L) : dim3(gx, L);
-            if (d == 1 && dl)
+            // H1 above the LDS-matrix range: 16 x 16 edge tiles over LDS-staged v-tiles (TDA_APP_TILE=0: one edge per thread)
+            const bool tiled = d == 1 && !dl && !test_env_is("TDA_APP_TILE", "0");
+            if (tiled) {
+                const uint64_t nt = ((uint64_t)n + kAppTS - 1) / kAppTS, tiles = nt * (nt + 1) / 2;
+                const unsigned tx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(tiles, std::max<uint64_t>(1, app_total / L)));
+                const dim3 tg = xl ? dim3(tx * (unsigned)L) : dim3(tx, L);
+                hipLaunchKernelGGL(k_apparent_tile, tg, dim3(256), 0, st, dist, n, stats, db[d], rowmax, a.thresh, xl);
+            } else if (d == 1 && dl)
                 hipLaunchKernelGGL((k_apparent<1, true>), ag, dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh, xl);
             else if (d == 1)
                 hipLaunchKernelGGL((k_apparent<1, false>), ag, dim3(256), alds, st, dist, n, stats, db[d], rowmax, a.thresh, xl);

@@ -1379,6 +1379,82 @@ __device__ __forceinline__ AppBlock app_block(int xcd_layers) {
     return {(int)((b & 7u) + 8u * (r / G)), r % G, G};
 }
 
+// Classify simplex s (vertices vs descending, diameter sd <= r) from its oldest cofacet (vertex
+// bv, diameter bcd; bv < 0: empty coboundary): 1 = apparent (pivot bit set, pair counted), 2 =
+// residual (an empty coboundary too: essential unless cleared, decided by the reduction).
+template <int DIM, typename Dat>
+__device__ __forceinline__ int apparent_kind(uint64_t s, const int (&vs)[DIM + 1], float sd, int bv, float bcd, Dat dat, int n,
+                                             uint32_t* piv, uint64_t& tixv, uint64_t& acc_cs, uint64_t& acc_app) {
+    if (bv < 0 || bcd != sd) return 2;
+    bool app = true;
+#pragma unroll
+    for (int u = 0; u <= DIM; ++u) {
+        if (vs[u] < bv) continue;
+        // diam of (s u {bv}) \ {vs[u]}
+        float fd = 0.0f;
+#pragma unroll
+        for (int i = 0; i <= DIM; ++i) {
+            if (i == u) continue;
+            fd = fmaxf(fd, dat((size_t)bv * n + vs[i]));
+#pragma unroll
+            for (int j = i + 1; j <= DIM; ++j)
+                if (j != u) fd = fmaxf(fd, dat((size_t)vs[i] * n + vs[j]));
+        }
+        app &= fd < sd;
+    }
+    if (!app) return 2;
+    const uint64_t tix = cofacet_index<DIM>(vs, bv);
+    matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
+    tixv = tix;
+    acc_cs += pair_hash(s, tix);
+    acc_app += 1;
+    return 1;
+}
+
+// One simplex per lane (kind 0: none): the words of set H2 pivot bits (sparse-cleared bitmap) and
+// the residual columns, each wave aggregated.
+template <int DIM>
+__device__ __forceinline__ void apparent_append(int kind, uint64_t s, float sd, uint64_t tixv, const DimBufs& b, LayerStats* st, int l,
+                                                uint64_t* resid) {
+    if (DIM == 2 && b.clr) {  // sparse-cleared bitmap: list the words set (wave aggregated)
+        const uint64_t mc = __ballot(kind == 1);
+        if (mc) {
+            uint64_t cb = 0;
+            if (lane_id() == __builtin_ctzll(mc)) cb = atomicAdd((unsigned long long*)&st->n_clr2, (unsigned long long)__popcll(mc));
+            cb = shfl_u64(cb, __builtin_ctzll(mc)) + lanes_below(mc);
+            if (kind == 1 && cb < b.clr_cap) st_glb(b.clr + (size_t)l * b.clr_cap, cb, tixv >> 5);
+        }
+    }
+    // residual append (wave aggregated)
+    const uint64_t m = __ballot(kind == 2);
+    if (m) {
+        uint64_t basepos = 0;
+        if (lane_id() == __builtin_ctzll(m))
+            basepos = atomicAdd((unsigned long long*)&st->n_residual[DIM], (unsigned long long)__popcll(m));
+        basepos = shfl_u64(basepos, __builtin_ctzll(m));
+        if (kind == 2) {
+            uint64_t pos = basepos + lanes_below(m);
+            if (pos < b.rcap)
+                st_glb(resid, pos, col_key(sd, s));
+            else
+                atomicOr(&st->err, ERR_RESID_CAP);
+        }
+    }
+}
+
+__device__ __forceinline__ void apparent_stats(LayerStats* st, int dim, uint64_t acc_cs, uint64_t acc_app, uint64_t acc_cols) {
+    acc_cs = wave_sum_u64(acc_cs);
+    acc_app = wave_sum_u64(acc_app);
+    acc_cols = wave_sum_u64(acc_cols);
+    if (lane_id() == 0) {
+        if (acc_app) {
+            atomicAdd((unsigned long long*)&st->checksum[dim], (unsigned long long)acc_cs);
+            atomicAdd((unsigned long long*)&st->all_pairs[dim], (unsigned long long)acc_app);
+        }
+        if (acc_cols) atomicAdd((unsigned long long*)&st->n_columns[dim], (unsigned long long)acc_cols);
+    }
+}
+
 template <int DIM, bool DLDS>
 __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
                                                   DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh,
@@ -1431,75 +1507,126 @@ __global__ __launch_bounds__(256) void k_apparent(const float* __restrict__ dist
                         if (cd == sd) break;
                     }
                 }
-                if (bv < 0) {
-                    kind = 2;  // empty coboundary: essential unless cleared -> decided by k_reduce_all
-                } else {
-                    kind = 2;
-                    if (bcd == sd) {
-                        bool app = true;
+                kind = apparent_kind<DIM>(s, vs, sd, bv, bcd, dat, n, piv, tixv, acc_cs, acc_app);
+            }
+        }
+        acc_cols += (kind != 0);
+        apparent_append<DIM>(kind, s, sd, tixv, b, st, l, resid);
+    }
+    apparent_stats(st, DIM, acc_cs, acc_app, acc_cols);
+}
+
+// H1 apparent pass at large N (r06): the edge columns in 16 x 16 tiles (a in one block of 16
+// vertices, b in another, a > b), the oldest-cofacet scan over v-tiles of kAppTV rows whose
+// columns a and b are staged in LDS -- 2 x 64 B of every row per tile of 256 edges, where the
+// one-edge-per-thread pass read a 1-KB row segment per 256 edges of one a and every tile's rows
+// from L2 again (torus1024x32: 3.2 GB of fabric reads per 32-layer launch for 128 MB of
+// matrices).  The next v-tile's loads are in flight while the current one is scanned.  Each edge's
+// scan, early exit, apparent test and outputs are k_apparent<1, false>'s.
+constexpr int kAppTS = 16;   // tile side (vertices)
+constexpr int kAppTV = 64;   // rows per v-tile
+__global__ __launch_bounds__(256) void k_apparent_tile(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
+                                                       DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh,
+                                                       int xcd_layers) {
+    __shared__ float Ta[2][kAppTV][kAppTS + 1], Tb[2][kAppTV][kAppTS + 1];
+    __shared__ uint32_t s_min;
+    __shared__ int s_any[3];  // "a lane is still scanning", one cell per v-tile mod 3 (a slow reader of cell j
+                              // is past barrier j + 1 before anyone clears it again)
+    const AppBlock ab = app_block(xcd_layers);
+    const int l = ab.l;
+    const float* Dg = dist + (size_t)l * n * n;
+    const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, &s_min);
+    auto dat = [&](size_t i) -> float { return ld_glb(Dg, i); };
+    LayerStats* st = stats + l;
+    const uint32_t* cleared = b.cleared ? b.cleared + (size_t)l * b.cleared_words : nullptr;
+    uint32_t* piv = b.pivbits + (size_t)l * b.piv_words;
+    uint64_t* resid = b.resid + (size_t)l * b.rcap;
+    const int nt = (n + kAppTS - 1) / kAppTS;
+    uint64_t acc_cs = 0, acc_app = 0, acc_cols = 0;
+    const int t = threadIdx.x, ti = t / kAppTS, tj = t % kAppTS;
+    // staging: thread t loads rows (t / 16) + 16 q, q < 4, column t % 16, of both column blocks
+    const int sr = t / kAppTS, sc = t % kAppTS;
+    for (uint32_t tile = ab.bx; tile < (uint32_t)(nt * (nt + 1) / 2); tile += ab.nbx) {
+        // tile -> (ta >= tb): row ta holds tiles ta (ta + 1) / 2 .. + ta
+        int ta = (int)((sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);
+        while ((ta + 1) * (ta + 2) / 2 <= (int)tile) ++ta;
+        while (ta * (ta + 1) / 2 > (int)tile) --ta;
+        const int tb = (int)tile - ta * (ta + 1) / 2;
+        const int a = ta * kAppTS + ti, bb = tb * kAppTS + tj;
+        const int A0 = ta * kAppTS, B0 = tb * kAppTS;
+        int kind = 0;
+        uint64_t tixv = 0;
+        int vs[2] = {a, bb};
+        float sd = 0.0f;
+        uint64_t s = 0;
+        bool live = false;  // still scanning
+        if (a < n && bb < a) {
+            s = (uint64_t)a * (a - 1) / 2 + (uint64_t)bb;
+            if (!(cleared && ((ld_glb(cleared, s >> 5) >> (s & 31)) & 1u))) {
+                sd = dat((size_t)a * n + bb);
+                live = sd <= r;
+                kind = live ? 2 : 0;  // decided below
+            }
+        }
+        float bcd = INFINITY;
+        int bv = -1;
+        // v-tiles from the top (vertices descending)
+        const int nv = (n + kAppTV - 1) / kAppTV;
+        float ra[kAppTV / 16], rb[kAppTV / 16];
+        auto load = [&](int vt) {
 #pragma unroll
-                        for (int u = 0; u <= DIM; ++u) {
-                            if (vs[u] < bv) continue;
-                            // diam of (s u {bv}) \ {vs[u]}
-                            float fd = 0.0f;
+            for (int q = 0; q < kAppTV / 16; ++q) {
+                const int v = vt * kAppTV + sr + 16 * q;
+                const bool ok = v < n;
+                ra[q] = ok && A0 + sc < n ? ld_glb(Dg, (size_t)v * n + A0 + sc) : 0.0f;
+                rb[q] = ok && B0 + sc < n ? ld_glb(Dg, (size_t)v * n + B0 + sc) : 0.0f;
+            }
+        };
+        auto store = [&](int buf) {
 #pragma unroll
-                            for (int i = 0; i <= DIM; ++i) {
-                                if (i == u) continue;
-                                fd = fmaxf(fd, dat((size_t)bv * n + vs[i]));
-#pragma unroll
-                                for (int j = i + 1; j <= DIM; ++j)
-                                    if (j != u) fd = fmaxf(fd, dat((size_t)vs[i] * n + vs[j]));
-                            }
-                            app &= fd < sd;
-                        }
-                        if (app) {
-                            kind = 1;
-                            uint64_t tix = cofacet_index<DIM>(vs, bv);
-                            matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
-                            tixv = tix;
-                            acc_cs += pair_hash(s, tix);
-                            acc_app += 1;
+            for (int q = 0; q < kAppTV / 16; ++q) {
+                Ta[buf][sr + 16 * q][sc] = ra[q];
+                Tb[buf][sr + 16 * q][sc] = rb[q];
+            }
+        };
+        int buf = 0, cell = 0;
+        load(nv - 1);
+        store(0);
+        if (t == 0) s_any[0] = 0;
+        __syncthreads();
+        for (int vt = nv - 1; vt >= 0; --vt) {
+            if (vt > 0) load(vt - 1);  // in flight during the scan below
+            if (live) {
+                for (int k = kAppTV - 1; k >= 0; --k) {
+                    const int v = vt * kAppTV + k;
+                    if (v >= n || v == a || v == bb) continue;
+                    const float cd = fmaxf(sd, fmaxf(Ta[buf][k][ti], Tb[buf][k][tj]));
+                    if (cd <= r && cd < bcd) {
+                        bcd = cd;
+                        bv = v;
+                        if (cd == sd) {
+                            live = false;
+                            break;
                         }
                     }
                 }
             }
+            const int next = cell == 2 ? 0 : cell + 1;
+            if (live) s_any[cell] = 1;  // every writer writes 1
+            if (vt > 0) store(buf ^ 1);
+            if (t == 0) s_any[next] = 0;
+            __syncthreads();
+            const bool more = s_any[cell] != 0;
+            buf ^= 1;
+            cell = next;
+            if (!more) break;
         }
+        if (kind == 2) kind = apparent_kind<1>(s, vs, sd, bv, bcd, dat, n, piv, tixv, acc_cs, acc_app);
         acc_cols += (kind != 0);
-        if (DIM == 2 && b.clr) {  // sparse-cleared bitmap: list the words set (wave aggregated)
-            const uint64_t mc = __ballot(kind == 1);
-            if (mc) {
-                uint64_t cb = 0;
-                if (lane_id() == __builtin_ctzll(mc)) cb = atomicAdd((unsigned long long*)&st->n_clr2, (unsigned long long)__popcll(mc));
-                cb = shfl_u64(cb, __builtin_ctzll(mc)) + lanes_below(mc);
-                if (kind == 1 && cb < b.clr_cap) st_glb(b.clr + (size_t)l * b.clr_cap, cb, tixv >> 5);
-            }
-        }
-        // residual append (wave aggregated)
-        const uint64_t m = __ballot(kind == 2);
-        if (m) {
-            uint64_t basepos = 0;
-            if (lane_id() == __builtin_ctzll(m))
-                basepos = atomicAdd((unsigned long long*)&st->n_residual[DIM], (unsigned long long)__popcll(m));
-            basepos = shfl_u64(basepos, __builtin_ctzll(m));
-            if (kind == 2) {
-                uint64_t pos = basepos + lanes_below(m);
-                if (pos < b.rcap)
-                    st_glb(resid, pos, col_key(sd, s));
-                else
-                    atomicOr(&st->err, ERR_RESID_CAP);
-            }
-        }
+        apparent_append<1>(kind, s, sd, tixv, b, st, l, resid);
+        __syncthreads();  // the staging buffers are rewritten by the next tile
     }
-    acc_cs = wave_sum_u64(acc_cs);
-    acc_app = wave_sum_u64(acc_app);
-    acc_cols = wave_sum_u64(acc_cols);
-    if (lane_id() == 0) {
-        if (acc_app) {
-            atomicAdd((unsigned long long*)&st->checksum[DIM], (unsigned long long)acc_cs);
-            atomicAdd((unsigned long long*)&st->all_pairs[DIM], (unsigned long long)acc_app);
-        }
-        if (acc_cols) atomicAdd((unsigned long long*)&st->n_columns[DIM], (unsigned long long)acc_cols);
-    }
+    apparent_stats(st, 1, acc_cs, acc_app, acc_cols);
 }
 
 // Small-N apparent pass (N <= 64, the reference's clouds): same columns,

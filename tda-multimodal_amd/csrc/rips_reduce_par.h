@@ -1338,16 +1338,14 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 ++nref;
 #endif
                 P2_T(ps6);
-                if (tid == 0) PS.lfail = layer_cap_missed(st);  // read behind col_refill's first barrier
+                // (a per-refill check of the layer's cap-miss flag, to stop the layer's columns in flight
+                // early, cost torus1024 ~1.5 ms: its global load sat in the refill's first barrier.
+                // Columns of a flagged layer stop at their next pickup instead.)
                 const bool more = col_refill(C, P);
                 P2_ACC(6, ps6);
 #ifdef TDA_PROFILE
                 pf[4] += clock64() - t0;
 #endif
-                if (PS.lfail) {  // another column of this layer missed its cap: the layer re-runs
-                    done = true;
-                    continue;
-                }
                 if (!more) {
                     if (PS.err) break;
                     if (capped) {  // empty below the cap: the pivot lies above it -> this layer re-runs uncapped

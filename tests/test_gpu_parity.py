@@ -928,3 +928,22 @@ def test_cap_miss_h2_sphere_and_circle(gpu, oracle, monkeypatch):
     assert info["cap_reruns"] == 2, info["cap_reruns"]
     for l in range(4):
         assert_same(res[l], oracle.rips(X[l], maxdim=2), 2, l)
+
+
+@pytest.mark.parametrize("n,L", [(129, 8), (300, 3), (777, 8)])
+@pytest.mark.parametrize("tile", ["1", "0"])
+def test_h1_apparent_tiles_vs_oracle(gpu, oracle, monkeypatch, n, L, tile):
+    """The tiled H1 apparent pass (r06, k_apparent_tile: 16 x 16 edge tiles over
+    LDS-staged v-tiles, N > 128) and the one-edge-per-thread pass
+    (TDA_APP_TILE=0) both equal the oracle: N not a multiple of the tile side,
+    the XCD-ordered 1-D grid (L = 8) and the 2-D grid (L = 3)."""
+    monkeypatch.setenv("TDA_APP_TILE", tile)
+    syn = gpu.synthetic
+    X = np.stack([syn.torus(n, seed=40 + l) for l in range(L)])
+    res = gpu.ripser_batch(X, maxdim=1)
+    exp = _TILE_ORACLE.setdefault((n, L), [oracle.rips(X[l], maxdim=1) for l in range(L)])
+    for l in range(L):
+        assert_same(res[l], exp[l], 1, (n, l, tile))
+
+
+_TILE_ORACLE: dict = {}
