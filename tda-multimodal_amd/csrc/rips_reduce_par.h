@@ -87,9 +87,7 @@ constexpr uint32_t kParSpin = 1u << 22;       // polls before a wait on another 
 // capped column ran empty below its cap; the layer's remaining columns are
 // dropped and the host re-runs that layer alone without caps.
 enum : int32_t { ERR_PAR = 128, ERR_PAR2 = 256, ERR_CAP_MISS = 512 };
-__device__ __forceinline__ uint32_t layer_cap_missed(const LayerStats* st) {
-    return (uint32_t)__hip_atomic_load(&st->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (uint32_t)ERR_CAP_MISS;
-}
+
 
 struct ParCtl {  // zeroed by k_par_init
     unsigned long long next;     // next fresh item
@@ -207,7 +205,6 @@ struct ParLds {
     uint32_t kf;    // front holds levels 0..kf
     int32_t err;
     uint32_t wide;  // wide H2 keys: the low 32 bits (index fingerprint) are not unique -> verify hits
-    uint32_t lfail; // the column's layer missed a column cap (ERR_CAP_MISS): drop its work
 };
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
@@ -601,8 +598,85 @@ __device__ __forceinline__ void front_room_slow(ParCol& C, const ParBufs& P, uin
 // Insert keys (bit r of vmask; all >= the current pivot) into the working
 // column: front levels toggle in LDS, the rest append to HBM buckets.  No
 // barrier: the caller made room (front_room) for every key of the pass.
+#ifndef TDA_PAR_ILV  // r06 A/B: a coboundary round's slot atomics, stage writes, chunk lookups and toggles interleaved
+#define TDA_PAR_ILV 0
+#endif
+// The same as col_add below for one coboundary round (R = kParRV), with the two LDS dependency chains
+// of the round -- back keys: slot atomic -> chunk pointer -> store; front keys: stage write -> stage
+// read -> CAS -- issued side by side instead of one after the other.
+template <int R>
+__device__ __forceinline__ void col_add_ilv(const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
+    static_assert(R * 64 <= (int)kStageW, "stage");
+    const uint64_t last = PS.last;
+    const uint32_t kf = PS.kf;
+    const int ln = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t fm = 0, bm = 0, bb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        bb[r] = par_bucket(k[r], last);
+        if ((vmask >> r) & 1u) {
+            if (bb[r] <= kf) fm |= 1u << r;
+            else bm |= 1u << r;
+        }
+    }
+    // back keys: slot atomics issued first
+    uint32_t slot[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) slot[r] = ((bm >> r) & 1u) ? atomicAdd(&PS.bcnt[bb[r]], 1u) : 0u;
+    // front keys: packed into the wave's stage while the atomics are in flight
+    uint64_t m[R];
+    uint32_t wtot = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        m[r] = __ballot((fm >> r) & 1u);
+        wtot += (uint32_t)__popcll(m[r]);
+    }
+    {
+        uint32_t off = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if ((fm >> r) & 1u) PS.stage[w][off + lanes_below(m[r])] = k[r];
+            off += (uint32_t)__popcll(m[r]);
+        }
+    }
+    // back keys: chunk pointers and stores (bucket_append's second half)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!((bm >> r) & 1u)) continue;
+        const uint32_t kc = chunk_of(slot[r]);
+        if (slot[r] == chunk_start(kc) && kc + 2 < (uint32_t)kParChunks && PS.cptr[bb[r]][kc + 2] == kNoChunk) {
+            const uint64_t sz = 256ull << (kc + 2);
+            const uint64_t o = aadd(&P.ctl->bpool_used, sz);
+            if (o + sz <= P.bpool_cap) PS.cptr[bb[r]][kc + 2] = (uint32_t)(o >> 8);
+            else PS.err = 22;
+        }
+        const uint32_t cp = kc < (uint32_t)kParChunks ? PS.cptr[bb[r]][kc] : kNoChunk;
+        if (cp == kNoChunk) {
+            PS.err = 21;
+            continue;
+        }
+        st_glb(P.bpool, (uint64_t)cp * 256 + (slot[r] - chunk_start(kc)), k[r]);
+    }
+    // front keys: toggles (front_toggle's second half)
+    if (!wtot) return;
+    uint32_t ins = 0;
+    for (uint32_t pos = (uint32_t)ln; pos < wtot; pos += 64) ins += tab_toggle(PS.stage[w][pos]);
+    const uint64_t mi = __ballot(ins != 0);
+    if (__popcll(mi) > 0) {
+        const uint32_t n = (uint32_t)wave_sum_u64(ins);
+        if (ln == 0) atomicAdd(&PS.fcnt, n);
+    }
+}
+
 template <int R>
 __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
+#if TDA_PAR_ILV && !defined(TDA_PROFILE) && !defined(TDA_PROF2)
+    if constexpr (R == kParRV) {
+        (void)C;
+        col_add_ilv<R>(P, k, vmask);
+        return;
+    }
+#endif
     const uint64_t last = PS.last;
     const uint32_t kf = PS.kf;
     uint32_t fm = 0, bm = 0, bb[R];
@@ -1211,13 +1285,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         uint64_t nres_l = ld_glb(P.item_base, l + 1) - ld_glb(P.item_base, l);
         const uint64_t omask = par_omask(nres_l, P.ostride);
         uint64_t* colpiv = P.colpiv + (size_t)l * b1.rcap;
-        // a layer that missed a column cap is re-run without caps by the host: its columns are dropped
-        if (tid == 0) PS.lfail = layer_cap_missed(st);
-        __syncthreads();
-        if (PS.lfail) {
-            if (tid == 0) ast(colpiv + j, kParSkip);
-            continue;
-        }
         const uint64_t ckey = ld_glb(resid, j);
         const uint64_t sidx = key_idx(ckey);
         const float sdm = key_diam(ckey);
@@ -1228,10 +1295,10 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         // because pivots only grow along a column's reduction.  The records j adds come from
         // EARLIER columns (larger births, so larger caps: they hold every key j keeps), and an
         // evicted column re-adds the record of an earlier one (the same order).  A column that
-        // runs empty below its cap has its pivot above it: its layer is flagged (ERR_CAP_MISS), the
-        // layer's other columns are dropped, and the host re-runs that layer alone without caps --
-        // the other layers of the launch are unaffected (a missed column never claims a pivot, and
-        // a column of another layer never reads this layer's records).  90 % of the keys the longest
+        // runs empty below its cap has its pivot above it: its layer is flagged (ERR_CAP_MISS) and the
+        // host re-runs that layer alone without caps -- the other layers of the launch are unaffected
+        // (a missed column never claims a pivot, and a column of another layer never reads this
+        // layer's records); the flagged layer's other H1 columns still run, its H2 columns do not.  90 % of the keys the longest
         // torus1024 column generates lie above its final pivot (tools/front_sim.py).
         float rc = r;
         bool capped = false;
@@ -1338,9 +1405,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 ++nref;
 #endif
                 P2_T(ps6);
-                // (a per-refill check of the layer's cap-miss flag, to stop the layer's columns in flight
-                // early, cost torus1024 ~1.5 ms: its global load sat in the refill's first barrier.
-                // Columns of a flagged layer stop at their next pickup instead.)
                 const bool more = col_refill(C, P);
                 P2_ACC(6, ps6);
 #ifdef TDA_PROFILE
@@ -1349,12 +1413,8 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 if (!more) {
                     if (PS.err) break;
                     if (capped) {  // empty below the cap: the pivot lies above it -> this layer re-runs uncapped
-                        if (tid == 0) {
-                            atomicOr(&st->err, ERR_CAP_MISS);
-                            ast(colpiv + j, kParSkip);
-                        }
-                        done = true;
-                        continue;
+                        if (tid == 0) PS.err = 81;
+                        break;
                     }
                     if (tid == 0) ast(colpiv + j, kParEss);  // zero column: essential
                     done = true;
@@ -1548,6 +1608,19 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             __syncthreads();
         }
         if (PS.err) {
+            if (PS.err == 81) {
+                // a capped column ran empty below its cap: its layer is flagged (ERR_CAP_MISS) and re-run
+                // alone, uncapped, by the host; this worker goes on with the next column.  (Handled here,
+                // off the step loop: a flag check in the pickup or in the step loop raised k_reduce_par's
+                // SGPR spills 164 -> 180 and cost torus1024 ~2 ms, r06.)
+                __syncthreads();  // every thread has read PS.err
+                if (tid == 0) {
+                    atomicOr(&st->err, ERR_CAP_MISS);
+                    ast(colpiv + j, kParSkip);
+                    PS.err = 0;
+                }
+                continue;  // the pickup's barrier publishes PS.err = 0
+            }
             if (tid == 0) {
                 acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)item << 16) | (uint64_t)PS.err);  // first error: item, code
                 aadd(&P.ctl->abort, 1);
@@ -1578,6 +1651,9 @@ __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats
         for (int q = 0; q < L; ++q) {
             P.item_base[q] = s;
             uint64_t c = (uint64_t)stats[q].n_residual[dim];
+            // H2 of a layer whose H1 missed a column cap: nothing (the host re-runs the layer; its H1
+            // pivots, H2's clearing test, are incomplete)
+            if (dim > 1 && (stats[q].err & ERR_CAP_MISS)) c = 0;
             s += c > rcap ? rcap : c;
         }
         P.item_base[L] = s;
