@@ -205,6 +205,7 @@ struct ParLds {
     uint32_t kf;    // front holds levels 0..kf
     int32_t err;
     uint32_t wide;  // wide H2 keys: the low 32 bits (index fingerprint) are not unique -> verify hits
+    uint64_t ccol[3];  // TDA_PAR_LSC: the current column's layer, index in the layer, item
 };
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
@@ -598,6 +599,9 @@ __device__ __forceinline__ void front_room_slow(ParCol& C, const ParBufs& P, uin
 // Insert keys (bit r of vmask; all >= the current pivot) into the working
 // column: front levels toggle in LDS, the rest append to HBM buckets.  No
 // barrier: the caller made room (front_room) for every key of the pass.
+#ifndef TDA_PAR_LSC  // r06 A/B: the column's layer / index / item read back from LDS where the owner path and the
+#define TDA_PAR_LSC 0   // column's end need them, instead of live (scalar) registers through the step loop
+#endif
 #ifndef TDA_PAR_ILV  // r06 A/B: a coboundary round's slot atomics, stage writes, chunk lookups and toggles interleaved
 #define TDA_PAR_ILV 0
 #endif
@@ -1280,11 +1284,20 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         const uint64_t* resid = b1.resid + (size_t)l * b1.rcap;
         const uint32_t* pivg = b1.pivbits + (size_t)l * b1.piv_words;
         const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
-        uint64_t* okey = P.okey + (size_t)l * P.ostride;
-        uint64_t* oval = P.oval + (size_t)l * P.ostride;
-        uint64_t nres_l = ld_glb(P.item_base, l + 1) - ld_glb(P.item_base, l);
-        const uint64_t omask = par_omask(nres_l, P.ostride);
-        uint64_t* colpiv = P.colpiv + (size_t)l * b1.rcap;
+#if TDA_PAR_LSC
+        if (tid == 0) {  // published by the working column's reset barrier below
+            PS.ccol[0] = (uint64_t)l;
+            PS.ccol[1] = j;
+            PS.ccol[2] = item;
+        }
+#define PAR_CL ((int)PS.ccol[0])
+#define PAR_CJ (PS.ccol[1])
+#define PAR_CITEM (PS.ccol[2])
+#else
+#define PAR_CL l
+#define PAR_CJ j
+#define PAR_CITEM item
+#endif
         const uint64_t ckey = ld_glb(resid, j);
         const uint64_t sidx = key_idx(ckey);
         const float sdm = key_diam(ckey);
@@ -1314,7 +1327,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         decode<DIM>(sidx, n, sv);
         const uint32_t* cbits = DIM == 1 ? mst : clr + (size_t)l * clr_words;
         if (!rec0 && ((ld_glb(cbits, sidx >> 5) >> (sidx & 31)) & 1u)) {  // cleared: an H_{DIM-1} death
-            if (tid == 0) ast(colpiv + j, kParSkip);
+            if (tid == 0) ast(P.colpiv + (size_t)l * b1.rcap + j, kParSkip);
             continue;
         }
         // ---------------- working column: reset (chunks stay), then the coboundary or the record
@@ -1416,7 +1429,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                         if (tid == 0) PS.err = 81;
                         break;
                     }
-                    if (tid == 0) ast(colpiv + j, kParEss);  // zero column: essential
+                    if (tid == 0) ast(P.colpiv + (size_t)PAR_CL * b1.rcap + PAR_CJ, kParEss);  // zero column: essential
                     done = true;
                 }
                 continue;
@@ -1495,6 +1508,11 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             // ---------------- residual pivot: owner map
             P2_T(ps7);
             const uint64_t fkey = WIDE ? pk : filt_key(pd, pidx);  // colpiv: k_par_emit decodes it
+            const int lc = PAR_CL;
+            const uint64_t jc = PAR_CJ;
+            uint64_t* okey = P.okey + (size_t)lc * P.ostride;
+            uint64_t* oval = P.oval + (size_t)lc * P.ostride;
+            const uint64_t omask = par_omask(ld_glb(P.item_base, lc + 1) - ld_glb(P.item_base, lc), P.ostride);
             for (uint32_t round = 0;; ++round) {
                 if (tid == 0) {
                     uint64_t slot = 0;
@@ -1512,21 +1530,21 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                     break;
                 }
                 const uint64_t oi = v >> 32;
-                if (v != 0 && oi < j) {  // earlier owner: add its record
+                if (v != 0 && oi < jc) {  // earlier owner: add its record
                     col_add_record(C, P, (v & 0xFFFFFFFFull) - 1);
                     ++adds;
                     break;
                 }
-                if (v != 0 && oi == j) {
+                if (v != 0 && oi == jc) {
                     if (tid == 0) PS.err = 72;
                     break;
                 }
                 // free, or owned by a later column: publish R_j, then claim
                 if (my_rec < 0) {
-                    my_rec = col_save(C, P, pk, item, &my_seg);
+                    my_rec = col_save(C, P, pk, PAR_CITEM, &my_seg);
                     if (my_rec < 0) break;
                 }
-                const uint64_t mine = (j << 32) | (uint64_t)(my_rec + 1);
+                const uint64_t mine = (jc << 32) | (uint64_t)(my_rec + 1);
                 if (tid == 0) {
                     bool ok;
                     if (v == 0) {
@@ -1542,13 +1560,13 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                                 aadd(&P.ctl->abort, 1);
                                 acas((uint64_t*)&P.ctl->err, 0, 53);
                             } else {
-                                const uint64_t oitem = ld_glb(P.item_base, l) + oi;
+                                const uint64_t oitem = ld_glb(P.item_base, lc) + oi;
                                 ast(P.rq + qt, (oitem << 32) | (v & 0xFFFFFFFFull));
                             }
                             aadd(&P.ctl->evictions, 1);
                         }
                     }
-                    if (ok) ast(colpiv + j, fkey);
+                    if (ok) ast(P.colpiv + (size_t)lc * b1.rcap + jc, fkey);
                     PS.bc[6] = ok;
                 }
                 __syncthreads();
@@ -1601,7 +1619,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             }
         }
 #endif
-        if (tid == 0 && adds) atomicAdd((unsigned long long*)&st->n_adds[DIM], (unsigned long long)adds);
+        if (tid == 0 && adds) atomicAdd((unsigned long long*)&stats[PAR_CL].n_adds[DIM], (unsigned long long)adds);
         if (done && my_rec >= 0 && my_seg) {  // the claimed record references this workgroup's chunks: fresh ones next
             for (uint32_t e = tid; e < (uint32_t)kParLv * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
                     prealloc = false;
@@ -1615,20 +1633,24 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 // SGPR spills 164 -> 180 and cost torus1024 ~2 ms, r06.)
                 __syncthreads();  // every thread has read PS.err
                 if (tid == 0) {
-                    atomicOr(&st->err, ERR_CAP_MISS);
-                    ast(colpiv + j, kParSkip);
+                    atomicOr(&stats[PAR_CL].err, ERR_CAP_MISS);
+                    ast(P.colpiv + (size_t)PAR_CL * b1.rcap + PAR_CJ, kParSkip);
                     PS.err = 0;
                 }
                 continue;  // the pickup's barrier publishes PS.err = 0
             }
             if (tid == 0) {
-                acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)item << 16) | (uint64_t)PS.err);  // first error: item, code
+                acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)PAR_CITEM << 16) | (uint64_t)PS.err);  // first error: item, code
                 aadd(&P.ctl->abort, 1);
             }
             break;
         }
     }
 }
+
+#undef PAR_CL
+#undef PAR_CJ
+#undef PAR_CITEM
 
 // per-layer residual counts -> item prefix, control block, owner maps cleared
 __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats, int L, uint64_t rcap, ParBufs P, int dim) {
