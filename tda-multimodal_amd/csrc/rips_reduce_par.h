@@ -205,7 +205,7 @@ struct ParLds {
     uint32_t kf;    // front holds levels 0..kf
     int32_t err;
     uint32_t wide;  // wide H2 keys: the low 32 bits (index fingerprint) are not unique -> verify hits
-    uint64_t ccol[3];  // TDA_PAR_LSC: the current column's layer, index in the layer, item
+    uint64_t ccol[3];  // the current column's layer, index in the layer, item
 };
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
@@ -599,88 +599,11 @@ __device__ __forceinline__ void front_room_slow(ParCol& C, const ParBufs& P, uin
 // Insert keys (bit r of vmask; all >= the current pivot) into the working
 // column: front levels toggle in LDS, the rest append to HBM buckets.  No
 // barrier: the caller made room (front_room) for every key of the pass.
-#ifndef TDA_PAR_LSC  // r06 A/B: the column's layer / index / item read back from LDS where the owner path and the
-#define TDA_PAR_LSC 0   // column's end need them, instead of live (scalar) registers through the step loop
-#endif
-#ifndef TDA_PAR_ILV  // r06 A/B: a coboundary round's slot atomics, stage writes, chunk lookups and toggles interleaved
-#define TDA_PAR_ILV 0
-#endif
-// The same as col_add below for one coboundary round (R = kParRV), with the two LDS dependency chains
-// of the round -- back keys: slot atomic -> chunk pointer -> store; front keys: stage write -> stage
-// read -> CAS -- issued side by side instead of one after the other.
-template <int R>
-__device__ __forceinline__ void col_add_ilv(const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
-    static_assert(R * 64 <= (int)kStageW, "stage");
-    const uint64_t last = PS.last;
-    const uint32_t kf = PS.kf;
-    const int ln = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t fm = 0, bm = 0, bb[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        bb[r] = par_bucket(k[r], last);
-        if ((vmask >> r) & 1u) {
-            if (bb[r] <= kf) fm |= 1u << r;
-            else bm |= 1u << r;
-        }
-    }
-    // back keys: slot atomics issued first
-    uint32_t slot[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) slot[r] = ((bm >> r) & 1u) ? atomicAdd(&PS.bcnt[bb[r]], 1u) : 0u;
-    // front keys: packed into the wave's stage while the atomics are in flight
-    uint64_t m[R];
-    uint32_t wtot = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        m[r] = __ballot((fm >> r) & 1u);
-        wtot += (uint32_t)__popcll(m[r]);
-    }
-    {
-        uint32_t off = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if ((fm >> r) & 1u) PS.stage[w][off + lanes_below(m[r])] = k[r];
-            off += (uint32_t)__popcll(m[r]);
-        }
-    }
-    // back keys: chunk pointers and stores (bucket_append's second half)
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (!((bm >> r) & 1u)) continue;
-        const uint32_t kc = chunk_of(slot[r]);
-        if (slot[r] == chunk_start(kc) && kc + 2 < (uint32_t)kParChunks && PS.cptr[bb[r]][kc + 2] == kNoChunk) {
-            const uint64_t sz = 256ull << (kc + 2);
-            const uint64_t o = aadd(&P.ctl->bpool_used, sz);
-            if (o + sz <= P.bpool_cap) PS.cptr[bb[r]][kc + 2] = (uint32_t)(o >> 8);
-            else PS.err = 22;
-        }
-        const uint32_t cp = kc < (uint32_t)kParChunks ? PS.cptr[bb[r]][kc] : kNoChunk;
-        if (cp == kNoChunk) {
-            PS.err = 21;
-            continue;
-        }
-        st_glb(P.bpool, (uint64_t)cp * 256 + (slot[r] - chunk_start(kc)), k[r]);
-    }
-    // front keys: toggles (front_toggle's second half)
-    if (!wtot) return;
-    uint32_t ins = 0;
-    for (uint32_t pos = (uint32_t)ln; pos < wtot; pos += 64) ins += tab_toggle(PS.stage[w][pos]);
-    const uint64_t mi = __ballot(ins != 0);
-    if (__popcll(mi) > 0) {
-        const uint32_t n = (uint32_t)wave_sum_u64(ins);
-        if (ln == 0) atomicAdd(&PS.fcnt, n);
-    }
-}
-
+// (r06: a coboundary round's two LDS dependency chains -- back keys: slot atomic -> chunk pointer ->
+// store; front keys: stage write -> stage read -> CAS -- issued side by side instead of one after the
+// other, measured no faster: torus1024 33.8 vs 33.7 ms)
 template <int R>
 __device__ __forceinline__ void col_add(ParCol& C, const ParBufs& P, const uint64_t (&k)[R], uint32_t vmask) {
-#if TDA_PAR_ILV && !defined(TDA_PROFILE) && !defined(TDA_PROF2)
-    if constexpr (R == kParRV) {
-        (void)C;
-        col_add_ilv<R>(P, k, vmask);
-        return;
-    }
-#endif
     const uint64_t last = PS.last;
     const uint32_t kf = PS.kf;
     uint32_t fm = 0, bm = 0, bb[R];
@@ -1284,7 +1207,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         const uint64_t* resid = b1.resid + (size_t)l * b1.rcap;
         const uint32_t* pivg = b1.pivbits + (size_t)l * b1.piv_words;
         const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
-#if TDA_PAR_LSC
+        // the column's layer / index / item, read back from LDS where the owner path and the column's
+        // end need them, so they are not live in scalar registers through the step loop (r06: SGPR
+        // spills 167 -> 159, torus1024 32.3 -> 32.0 ms, torus2048 657 -> 655 ms)
         if (tid == 0) {  // published by the working column's reset barrier below
             PS.ccol[0] = (uint64_t)l;
             PS.ccol[1] = j;
@@ -1293,11 +1218,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #define PAR_CL ((int)PS.ccol[0])
 #define PAR_CJ (PS.ccol[1])
 #define PAR_CITEM (PS.ccol[2])
-#else
-#define PAR_CL l
-#define PAR_CJ j
-#define PAR_CITEM item
-#endif
         const uint64_t ckey = ld_glb(resid, j);
         const uint64_t sidx = key_idx(ckey);
         const float sdm = key_diam(ckey);
