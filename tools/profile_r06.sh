@@ -17,7 +17,7 @@ ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT" || exit 1
 export TDA_BENCH_STAGE_ONLY=1
 mkdir -p gpurun_out/$TAG
-for WL in ${WLS:-sweep48_host sweep48 grid144 torus1024 torus1024x32 raw4096 ripser324}; do
+for WL in ${WLS:-sweep48_host sweep48 grid144 torus1024 torus1024x32 raw4096}; do
     rm -rf gpurun_out/prof_$WL
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$WL -o run -- \
         python3 bench.py --workload $WL --extra "" --steps 20 --warmup 3 --no-cpu > gpurun_out/$TAG/stage_$WL.json 2> gpurun_out/prof_$WL.err
