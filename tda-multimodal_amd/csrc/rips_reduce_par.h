@@ -189,27 +189,6 @@ constexpr uint32_t kTabMax = kFrontLog * 3 / 4;  // filled slots allowed before 
 constexpr uint32_t kTabPer = kFrontLog / kParT;  // slots per thread in scans
 constexpr uint32_t kStageW = 64 * (kParRegs > 4 ? kParRegs : 4);           // per-wave staging of the keys one toggle pass hands to the table
 
-#ifndef TDA_PAR_KA  // r06 A/B: the kernel's arguments copied to LDS and read from there outside the step loop
-#define TDA_PAR_KA 0
-#endif
-// k_reduce_par's arguments as the pickup, the column set-up, the owner path and the column's end
-// read them (TDA_PAR_KA): an LDS copy whose loads are not hoisted across the step loop's barriers,
-// so those values are not live in scalar registers while a column is reduced
-struct ParKArgs {
-    ParBufs P;
-    const float* dist;
-    const uint32_t* dcode;
-    LayerStats* stats;
-    const uint64_t* resid;
-    uint64_t rcap;
-    const uint32_t* pivbits;
-    uint64_t piv_words;
-    const uint32_t* mst;
-    uint64_t mst_words;
-    const uint32_t* clr;
-    uint64_t clr_words;
-};
-
 struct ParLds {
     uint64_t log[kFrontLog];
     uint64_t stage[kParW][kStageW];
@@ -227,9 +206,6 @@ struct ParLds {
     int32_t err;
     uint32_t wide;  // wide H2 keys: the low 32 bits (index fingerprint) are not unique -> verify hits
     uint64_t ccol[3];  // the current column's layer, index in the layer, item
-#if TDA_PAR_KA
-    ParKArgs ka;
-#endif
 };
 extern __shared__ ParLds par_smem[];
 #define PS (par_smem[0])
@@ -623,6 +599,8 @@ __device__ __forceinline__ void front_room_slow(ParCol& C, const ParBufs& P, uin
 // Insert keys (bit r of vmask; all >= the current pivot) into the working
 // column: front levels toggle in LDS, the rest append to HBM buckets.  No
 // barrier: the caller made room (front_room) for every key of the pass.
+// (r06: the kernel's arguments copied to LDS and read from there outside the step loop -- SGPR
+// spills 159 -> 119 but 13 VGPRs spilled to scratch: torus1024 31.9 -> 34.3 ms, measured and dropped.)
 // (r06: a coboundary round's two LDS dependency chains -- back keys: slot atomic -> chunk pointer ->
 // store; front keys: stage write -> stage read -> CAS -- issued side by side instead of one after the
 // other, measured no faster: torus1024 33.8 vs 33.7 ms)
@@ -1175,42 +1153,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         PS.err = 0;
         PS.wide = WIDE ? 1u : 0u;
         PS.redm[0] = PS.redm[1] = PS.redm[2] = kEmpty64;
-#if TDA_PAR_KA
-        PS.ka = ParKArgs{P, dist, dcode, stats, b1.resid, b1.rcap, b1.pivbits, b1.piv_words, rb.mst, rb.mst_words, clr, clr_words};
-#endif
     }
     __syncthreads();
-#if TDA_PAR_KA
-    const ParKArgs& K = PS.ka;
-#define KP (K.P)
-#define K_DIST (K.dist)
-#define K_DCODE (K.dcode)
-#define K_STATS (K.stats)
-#define K_RESID (K.resid)
-#define K_RCAP (K.rcap)
-#define K_PIVBITS (K.pivbits)
-#define K_PIVW (K.piv_words)
-#define K_MST (K.mst)
-#define K_MSTW (K.mst_words)
-#define K_CLR (K.clr)
-#define K_CLRW (K.clr_words)
-#define K_TOTAL (ald(&K.P.ctl->total))
-#else
-#define KP P
-#define K_DIST dist
-#define K_DCODE dcode
-#define K_STATS stats
-#define K_RESID (b1.resid)
-#define K_RCAP (b1.rcap)
-#define K_PIVBITS (b1.pivbits)
-#define K_PIVW (b1.piv_words)
-#define K_MST (rb.mst)
-#define K_MSTW (rb.mst_words)
-#define K_CLR clr
-#define K_CLRW clr_words
     const uint64_t total = ald(&P.ctl->total);
-#define K_TOTAL total
-#endif
 #ifdef TDA_PROFILE
     if (tid == 0) atomicMin((unsigned long long*)&P.ctl->pad[0], (unsigned long long)wall_clock64());
 #endif
@@ -1223,24 +1168,24 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         if (tid == 0) {
             uint64_t got = kEmpty64;  // item << 32 | (record + 1)
             for (uint32_t spin = 0; spin < kParSpin; ++spin) {
-                if (ald(&KP.ctl->abort)) break;
-                const uint64_t h = ald(&KP.ctl->rq_head), t = ald(&KP.ctl->rq_tail);
-                if (h < t && h < KP.rq_cap) {
-                    if (acas((uint64_t*)&KP.ctl->rq_head, h, h + 1) != h) continue;
+                if (ald(&P.ctl->abort)) break;
+                const uint64_t h = ald(&P.ctl->rq_head), t = ald(&P.ctl->rq_tail);
+                if (h < t && h < P.rq_cap) {
+                    if (acas((uint64_t*)&P.ctl->rq_head, h, h + 1) != h) continue;
                     uint64_t v = 0;
-                    for (uint32_t q = 0; q < kParSpin && !(v = ald(KP.rq + h)); ++q) __builtin_amdgcn_s_sleep(1);
+                    for (uint32_t q = 0; q < kParSpin && !(v = ald(P.rq + h)); ++q) __builtin_amdgcn_s_sleep(1);
                     if (!v) {  // the pusher never wrote its slot
-                        aadd(&KP.ctl->abort, 1);
-                        acas((uint64_t*)&KP.ctl->err, 0, 51);
+                        aadd(&P.ctl->abort, 1);
+                        acas((uint64_t*)&P.ctl->err, 0, 51);
                         break;
                     }
-                    ast(KP.rq + h, 0);  // slots are used once per launch; leave the ring zeroed
+                    ast(P.rq + h, 0);  // slots are used once per launch; leave the ring zeroed
                     got = v;
                     break;
                 }
-                if (ald(&KP.ctl->next) < K_TOTAL) {
-                    const uint64_t c = aadd(&KP.ctl->next, 1);
-                    if (c < K_TOTAL) got = c << 32;
+                if (ald(&P.ctl->next) < total) {
+                    const uint64_t c = aadd(&P.ctl->next, 1);
+                    if (c < total) got = c << 32;
                 }
                 break;
             }
@@ -1254,16 +1199,16 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         const uint64_t rec0 = got & 0xFFFFFFFFull;  // 0: fresh column, else resume from record rec0 - 1
         // ---------------- layer / column
         int l = 0;
-        while (l + 1 < L && ld_glb(KP.item_base, l + 1) <= item) ++l;
-        const uint64_t j = item - ld_glb(KP.item_base, l);
-        LayerStats* st = K_STATS + l;
+        while (l + 1 < L && ld_glb(P.item_base, l + 1) <= item) ++l;
+        const uint64_t j = item - ld_glb(P.item_base, l);
+        LayerStats* st = stats + l;
         const float r = st->thresh;
-        const float* D = K_DIST + (size_t)l * n * n;
+        const float* D = dist + (size_t)l * n * n;
         // rows the coboundaries read: distances, or (WIDE) edge codes in float slots
-        const float* Dr = WIDE ? (const float*)(K_DCODE + (size_t)l * n * n) : D;
-        const uint64_t* resid = K_RESID + (size_t)l * K_RCAP;
-        const uint32_t* pivg = K_PIVBITS + (size_t)l * K_PIVW;
-        const uint32_t* mst = K_MST + (size_t)l * K_MSTW;
+        const float* Dr = WIDE ? (const float*)(dcode + (size_t)l * n * n) : D;
+        const uint64_t* resid = b1.resid + (size_t)l * b1.rcap;
+        const uint32_t* pivg = b1.pivbits + (size_t)l * b1.piv_words;
+        const uint32_t* mst = rb.mst + (size_t)l * rb.mst_words;
         // the column's layer / index / item, read back from LDS where the owner path and the column's
         // end need them, so they are not live in scalar registers through the step loop (r06: SGPR
         // spills 167 -> 159, torus1024 32.3 -> 32.0 ms, torus2048 657 -> 655 ms)
@@ -1292,8 +1237,8 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         // torus1024 column generates lie above its final pivot (tools/front_sim.py).
         float rc = r;
         bool capped = false;
-        if (!WIDE && KP.capf > 0.0f) {
-            const float capd = sdm + KP.capf * r;
+        if (!WIDE && P.capf > 0.0f) {
+            const float capd = sdm + P.capf * r;
             if (capd < r) {
                 rc = capd;
                 capped = true;
@@ -1302,24 +1247,24 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
         C.capbits = capped ? __float_as_uint(rc) : 0xFFFFFFFFu;
         int sv[DIM + 1];
         decode<DIM>(sidx, n, sv);
-        const uint32_t* cbits = DIM == 1 ? mst : K_CLR + (size_t)l * K_CLRW;
+        const uint32_t* cbits = DIM == 1 ? mst : clr + (size_t)l * clr_words;
         if (!rec0 && ((ld_glb(cbits, sidx >> 5) >> (sidx & 31)) & 1u)) {  // cleared: an H_{DIM-1} death
-            if (tid == 0) ast(KP.colpiv + (size_t)l * K_RCAP + j, kParSkip);
+            if (tid == 0) ast(P.colpiv + (size_t)l * b1.rcap + j, kParSkip);
             continue;
         }
         // ---------------- working column: reset (chunks stay), then the coboundary or the record
         if (!prealloc) {  // chunks 0..3 of every bucket (bucket_append opens chunk c + 2 from chunk c)
             if (tid == 0) {
                 constexpr uint64_t per = (uint64_t)kParLv * chunk_start(4);
-                const uint64_t o = aadd(&KP.ctl->bpool_used, per);
-                PS.bc[5] = o + per <= KP.bpool_cap ? o : kEmpty64;
+                const uint64_t o = aadd(&P.ctl->bpool_used, per);
+                PS.bc[5] = o + per <= P.bpool_cap ? o : kEmpty64;
             }
             __syncthreads();
             const uint64_t o = PS.bc[5];
             if (o == kEmpty64) {
                 if (tid == 0) {
-                    acas((uint64_t*)&KP.ctl->err, 0, ((uint64_t)item << 16) | 22u);
-                    aadd(&KP.ctl->abort, 1);
+                    acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)item << 16) | 22u);
+                    aadd(&P.ctl->abort, 1);
                 }
                 break;
             }
@@ -1351,9 +1296,9 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             else
                 col_cob2<PACKED, WIDE>(C, P, Dr, n, rc, sv[0], sv[1], sv[2], WIDE ? __uint_as_float(sc) : sdm, z);
         } else {
-            if (tid == 0) PS.last = ald(KP.rec + (rec0 - 1) * 4 + 2);  // the record's pivot: its smallest key
+            if (tid == 0) PS.last = ald(P.rec + (rec0 - 1) * 4 + 2);  // the record's pivot: its smallest key
             __syncthreads();
-            col_add_record(C, KP, rec0 - 1);
+            col_add_record(C, P, rec0 - 1);
         }
         int64_t my_rec = -1;
         bool my_seg = false;  // my_rec is zero-copy: it owns this workgroup's bucket chunks
@@ -1406,7 +1351,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                         if (tid == 0) PS.err = 81;
                         break;
                     }
-                    if (tid == 0) ast(KP.colpiv + (size_t)PAR_CL * K_RCAP + PAR_CJ, kParEss);  // zero column: essential
+                    if (tid == 0) ast(P.colpiv + (size_t)PAR_CL * b1.rcap + PAR_CJ, kParEss);  // zero column: essential
                     done = true;
                 }
                 continue;
@@ -1487,14 +1432,14 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             const uint64_t fkey = WIDE ? pk : filt_key(pd, pidx);  // colpiv: k_par_emit decodes it
             const int lc = PAR_CL;
             const uint64_t jc = PAR_CJ;
-            uint64_t* okey = KP.okey + (size_t)lc * KP.ostride;
-            uint64_t* oval = KP.oval + (size_t)lc * KP.ostride;
-            const uint64_t omask = par_omask(ld_glb(KP.item_base, lc + 1) - ld_glb(KP.item_base, lc), KP.ostride);
+            uint64_t* okey = P.okey + (size_t)lc * P.ostride;
+            uint64_t* oval = P.oval + (size_t)lc * P.ostride;
+            const uint64_t omask = par_omask(ld_glb(P.item_base, lc + 1) - ld_glb(P.item_base, lc), P.ostride);
             for (uint32_t round = 0;; ++round) {
                 if (tid == 0) {
                     uint64_t slot = 0;
                     bool found = false;
-                    const uint64_t v = round > 64 ? kEmpty64 : omap_find(KP, okey, oval, omask, pidx, &slot, &found);
+                    const uint64_t v = round > 64 ? kEmpty64 : omap_find(P, okey, oval, omask, pidx, &slot, &found);
                     PS.bc[6] = v;
                     PS.bc[7] = slot | (found ? 1ull << 63 : 0);
                 }
@@ -1508,7 +1453,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 }
                 const uint64_t oi = v >> 32;
                 if (v != 0 && oi < jc) {  // earlier owner: add its record
-                    col_add_record(C, KP, (v & 0xFFFFFFFFull) - 1);
+                    col_add_record(C, P, (v & 0xFFFFFFFFull) - 1);
                     ++adds;
                     break;
                 }
@@ -1518,7 +1463,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 }
                 // free, or owned by a later column: publish R_j, then claim
                 if (my_rec < 0) {
-                    my_rec = col_save(C, KP, pk, PAR_CITEM, &my_seg);
+                    my_rec = col_save(C, P, pk, PAR_CITEM, &my_seg);
                     if (my_rec < 0) break;
                 }
                 const uint64_t mine = (jc << 32) | (uint64_t)(my_rec + 1);
@@ -1532,18 +1477,18 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                     } else {
                         ok = acas(oval + slot, v, mine) == v;
                         if (ok) {  // evict the later owner: it resumes from its record
-                            const uint64_t qt = aadd(&KP.ctl->rq_tail, 1);
-                            if (qt >= KP.rq_cap) {
-                                aadd(&KP.ctl->abort, 1);
-                                acas((uint64_t*)&KP.ctl->err, 0, 53);
+                            const uint64_t qt = aadd(&P.ctl->rq_tail, 1);
+                            if (qt >= P.rq_cap) {
+                                aadd(&P.ctl->abort, 1);
+                                acas((uint64_t*)&P.ctl->err, 0, 53);
                             } else {
-                                const uint64_t oitem = ld_glb(KP.item_base, lc) + oi;
-                                ast(KP.rq + qt, (oitem << 32) | (v & 0xFFFFFFFFull));
+                                const uint64_t oitem = ld_glb(P.item_base, lc) + oi;
+                                ast(P.rq + qt, (oitem << 32) | (v & 0xFFFFFFFFull));
                             }
-                            aadd(&KP.ctl->evictions, 1);
+                            aadd(&P.ctl->evictions, 1);
                         }
                     }
-                    if (ok) ast(KP.colpiv + (size_t)lc * K_RCAP + jc, fkey);
+                    if (ok) ast(P.colpiv + (size_t)lc * b1.rcap + jc, fkey);
                     PS.bc[6] = ok;
                 }
                 __syncthreads();
@@ -1596,7 +1541,7 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
             }
         }
 #endif
-        if (tid == 0 && adds) atomicAdd((unsigned long long*)&K_STATS[PAR_CL].n_adds[DIM], (unsigned long long)adds);
+        if (tid == 0 && adds) atomicAdd((unsigned long long*)&stats[PAR_CL].n_adds[DIM], (unsigned long long)adds);
         if (done && my_rec >= 0 && my_seg) {  // the claimed record references this workgroup's chunks: fresh ones next
             for (uint32_t e = tid; e < (uint32_t)kParLv * kParChunks; e += kParT) (&PS.cptr[0][0])[e] = kNoChunk;
                     prealloc = false;
@@ -1610,15 +1555,15 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
                 // SGPR spills 164 -> 180 and cost torus1024 ~2 ms, r06.)
                 __syncthreads();  // every thread has read PS.err
                 if (tid == 0) {
-                    atomicOr(&K_STATS[PAR_CL].err, ERR_CAP_MISS);
-                    ast(KP.colpiv + (size_t)PAR_CL * K_RCAP + PAR_CJ, kParSkip);
+                    atomicOr(&stats[PAR_CL].err, ERR_CAP_MISS);
+                    ast(P.colpiv + (size_t)PAR_CL * b1.rcap + PAR_CJ, kParSkip);
                     PS.err = 0;
                 }
                 continue;  // the pickup's barrier publishes PS.err = 0
             }
             if (tid == 0) {
-                acas((uint64_t*)&KP.ctl->err, 0, ((uint64_t)PAR_CITEM << 16) | (uint64_t)PS.err);  // first error: item, code
-                aadd(&KP.ctl->abort, 1);
+                acas((uint64_t*)&P.ctl->err, 0, ((uint64_t)PAR_CITEM << 16) | (uint64_t)PS.err);  // first error: item, code
+                aadd(&P.ctl->abort, 1);
             }
             break;
         }
@@ -1628,19 +1573,6 @@ __global__ __launch_bounds__(kParT) void k_reduce_par(const float* __restrict__ 
 #undef PAR_CL
 #undef PAR_CJ
 #undef PAR_CITEM
-#undef KP
-#undef K_DIST
-#undef K_DCODE
-#undef K_STATS
-#undef K_RESID
-#undef K_RCAP
-#undef K_PIVBITS
-#undef K_PIVW
-#undef K_MST
-#undef K_MSTW
-#undef K_CLR
-#undef K_CLRW
-#undef K_TOTAL
 
 // per-layer residual counts -> item prefix, control block, owner maps cleared
 __global__ __launch_bounds__(256) void k_par_init(LayerStats* __restrict__ stats, int L, uint64_t rcap, ParBufs P, int dim) {
