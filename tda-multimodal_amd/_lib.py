@@ -3,6 +3,8 @@
 The product path has exactly one implementation: the HIP library.  If it is
 missing or no gfx950 device is visible, calls raise -- there is no CPU
 fallback (the CPU restatement under oracle/ is test infrastructure only).
+The host side of a call's inputs and results (the NaN check, the per-layer
+result objects) is the small CPython extension _hostviews.so, required too.
 """
 from __future__ import annotations
 
@@ -208,7 +210,48 @@ def build(verbose: bool = False, out: str | None = None, extra_flags: tuple = ()
     if verbose and r.stderr:
         print(r.stderr, file=sys.stderr)
     os.replace(out + ".tmp", out)
+    if out == LIB_PATH:
+        build_hostviews()
     return out
+
+
+HOSTVIEWS_PATH = os.path.join(BUILD_DIR, "_hostviews.so")
+_hostviews = None
+
+
+def build_hostviews(out: str | None = None) -> str:
+    """Compile csrc/hostviews.c (CPython + numpy C API, host code: a batch's
+    per-layer result objects in one call) into _build/_hostviews.so."""
+    import sysconfig
+
+    import numpy as np
+
+    out = out or HOSTVIEWS_PATH
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [os.environ.get("CC", "gcc"), "-O3", "-shared", "-fPIC", "-Wall", "-Werror", "-I" + sysconfig.get_paths()["include"],
+           "-I" + np.get_include(), "-o", out + ".tmp", os.path.join(CSRC, "hostviews.c")]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hostviews build failed:\n" + r.stderr[-4000:])
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def hostviews():
+    """The _hostviews extension (segments / layer_tuples); raise loudly if it is absent."""
+    global _hostviews
+    if _hostviews is None:
+        import importlib.machinery
+        import importlib.util
+
+        if not os.path.exists(HOSTVIEWS_PATH):
+            raise RuntimeError(f"host extension not built: {HOSTVIEWS_PATH} is missing (run __graft_entry__.build())")
+        loader = importlib.machinery.ExtensionFileLoader("_hostviews", HOSTVIEWS_PATH)
+        spec = importlib.util.spec_from_file_location("_hostviews", HOSTVIEWS_PATH, loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _hostviews = mod
+    return _hostviews
 
 
 def lib():

@@ -1,0 +1,179 @@
+// hostviews.c -- the host side of a batched call's result, in C.
+//
+// A batch of L layers comes back as one (T, 2) float64 pairs array; every
+// layer's dgms is a list of maxdim + 1 views into it (ripser.py's result
+// dict, debug_tda_pipeline.py:110 reads result['dgms'] per layer).  In
+// Python that is L x (maxdim + 1) slices plus L LayerResult tuples, ~0.5 us
+// a layer on the bench host -- a quarter of the host-input headline's time
+// per layer, and all of it under the GIL that the pipeline's worker threads
+// share.  These two functions make the same objects in one call each.
+//
+//   segments(pairs, off, cnt, nd) -> [[pairs[o:o+c] for the nd dims] per layer]
+//   layer_tuples(cls, batch, L)   -> [cls((batch, l)) for l in range(L)]
+//   finite_ptrs(arrays)           -> the input parts' data pointers, after the
+//                                    NaN / infinity check
+//
+// Host code only (CPython + numpy C API); no device calls.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
+#include <numpy/arrayobject.h>
+
+static PyObject* segments(PyObject* self, PyObject* args) {
+    (void)self;
+    PyArrayObject *pairs, *off, *cnt;
+    Py_ssize_t nd;
+    if (!PyArg_ParseTuple(args, "O!O!O!n", &PyArray_Type, &pairs, &PyArray_Type, &off, &PyArray_Type, &cnt, &nd))
+        return NULL;
+    if (PyArray_NDIM(pairs) != 2 || PyArray_DIM(pairs, 1) != 2 || PyArray_TYPE(pairs) != NPY_FLOAT64) {
+        PyErr_SetString(PyExc_ValueError, "pairs must be a (T, 2) float64 array");
+        return NULL;
+    }
+    if (PyArray_NDIM(off) != 1 || PyArray_NDIM(cnt) != 1 || PyArray_TYPE(off) != NPY_INT64 || PyArray_TYPE(cnt) != NPY_INT64 ||
+        PyArray_DIM(off, 0) != PyArray_DIM(cnt, 0) || !PyArray_IS_C_CONTIGUOUS(off) || !PyArray_IS_C_CONTIGUOUS(cnt)) {
+        PyErr_SetString(PyExc_ValueError, "off / cnt must be contiguous int64 arrays of one length");
+        return NULL;
+    }
+    const Py_ssize_t S = PyArray_DIM(off, 0);
+    if (nd <= 0 || S % nd != 0) {
+        PyErr_SetString(PyExc_ValueError, "the segment count must be a multiple of nd");
+        return NULL;
+    }
+    const npy_int64* o = (const npy_int64*)PyArray_DATA(off);
+    const npy_int64* c = (const npy_int64*)PyArray_DATA(cnt);
+    const npy_intp T = PyArray_DIM(pairs, 0);
+    for (Py_ssize_t s = 0; s < S; ++s)
+        if (o[s] < 0 || c[s] < 0 || o[s] > T || c[s] > T - o[s]) {
+            PyErr_SetString(PyExc_ValueError, "segment out of the pairs array");
+            return NULL;
+        }
+    char* base = PyArray_BYTES(pairs);
+    npy_intp strides[2] = {PyArray_STRIDE(pairs, 0), PyArray_STRIDE(pairs, 1)};
+    const int flags = PyArray_FLAGS(pairs) & (NPY_ARRAY_WRITEABLE | NPY_ARRAY_ALIGNED);
+    PyArray_Descr* descr = PyArray_DESCR(pairs);
+    const Py_ssize_t L = S / nd;
+    PyObject* out = PyList_New(L);
+    if (!out) return NULL;
+    for (Py_ssize_t l = 0; l < L; ++l) {
+        PyObject* lst = PyList_New(nd);
+        if (!lst) goto fail;
+        PyList_SET_ITEM(out, l, lst);
+        for (Py_ssize_t k = 0; k < nd; ++k) {
+            const Py_ssize_t s = l * nd + k;
+            npy_intp dims[2] = {(npy_intp)c[s], 2};
+            Py_INCREF(descr);  // stolen by NewFromDescr
+            PyObject* v = PyArray_NewFromDescr(&PyArray_Type, descr, 2, dims, strides, base + (npy_intp)o[s] * strides[0], flags, NULL);
+            if (!v) goto fail;
+            Py_INCREF(pairs);  // stolen by SetBaseObject (which walks to the owner of the data, as slicing does)
+            if (PyArray_SetBaseObject((PyArrayObject*)v, (PyObject*)pairs) < 0) {
+                Py_DECREF(v);
+                goto fail;
+            }
+            PyList_SET_ITEM(lst, k, v);
+        }
+    }
+    return out;
+fail:
+    Py_DECREF(out);
+    return NULL;
+}
+
+static PyObject* layer_tuples(PyObject* self, PyObject* args) {
+    (void)self;
+    PyTypeObject* cls;
+    PyObject* batch;
+    Py_ssize_t L;
+    if (!PyArg_ParseTuple(args, "O!On", &PyType_Type, &cls, &batch, &L)) return NULL;
+    if (!PyType_IsSubtype(cls, &PyTuple_Type) || L < 0) {
+        PyErr_SetString(PyExc_TypeError, "cls must be a tuple subclass and L >= 0");
+        return NULL;
+    }
+    PyObject* out = PyList_New(L);
+    if (!out) return NULL;
+    for (Py_ssize_t l = 0; l < L; ++l) {
+        // what tuple.__new__ does for a subclass: tp_alloc(cls, n), then the items
+        PyObject* t = cls->tp_alloc(cls, 2);
+        if (!t) goto fail;
+        PyObject* li = PyLong_FromSsize_t(l);
+        if (!li) {
+            Py_DECREF(t);
+            goto fail;
+        }
+        Py_INCREF(batch);
+        PyTuple_SET_ITEM(t, 0, batch);
+        PyTuple_SET_ITEM(t, 1, li);
+        PyList_SET_ITEM(out, l, t);
+    }
+    return out;
+fail:
+    Py_DECREF(out);
+    return NULL;
+}
+
+// every element finite: no exponent field of all ones (NaN and +-inf)
+static int all_finite(const char* p, npy_intp n, int f64) {
+    unsigned bad = 0;
+    if (f64) {
+        const npy_uint64* q = (const npy_uint64*)p;
+        for (npy_intp i = 0; i < n; ++i) bad |= (unsigned)((q[i] & 0x7FF0000000000000ull) == 0x7FF0000000000000ull);
+    } else {
+        const npy_uint32* q = (const npy_uint32*)p;
+        for (npy_intp i = 0; i < n; ++i) bad |= (unsigned)((q[i] & 0x7F800000u) == 0x7F800000u);
+    }
+    return !bad;
+}
+
+// finite_ptrs(arrays) -> [data pointer of each]: the host input parts of one
+// call (contiguous float32 / float64 numpy arrays), after ripser.py's
+// "Input contains NaN or infinity." check over all of them
+static PyObject* finite_ptrs(PyObject* self, PyObject* arg) {
+    (void)self;
+    PyObject* seq = PySequence_Fast(arg, "finite_ptrs needs a sequence of arrays");
+    if (!seq) return NULL;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    PyObject** items = PySequence_Fast_ITEMS(seq);
+    PyObject* out = PyList_New(n);
+    if (!out) {
+        Py_DECREF(seq);
+        return NULL;
+    }
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (!PyArray_Check(items[i])) {
+            PyErr_SetString(PyExc_TypeError, "finite_ptrs: not a numpy array");
+            goto fail;
+        }
+        PyArrayObject* a = (PyArrayObject*)items[i];
+        const int t = PyArray_TYPE(a);
+        if ((t != NPY_FLOAT32 && t != NPY_FLOAT64) || !PyArray_IS_C_CONTIGUOUS(a)) {
+            PyErr_SetString(PyExc_TypeError, "finite_ptrs: arrays must be contiguous float32 / float64");
+            goto fail;
+        }
+        if (!all_finite(PyArray_BYTES(a), PyArray_SIZE(a), t == NPY_FLOAT64)) {
+            PyErr_SetString(PyExc_ValueError, "Input contains NaN or infinity.");
+            goto fail;
+        }
+        PyObject* p = PyLong_FromVoidPtr(PyArray_DATA(a));
+        if (!p) goto fail;
+        PyList_SET_ITEM(out, i, p);
+    }
+    Py_DECREF(seq);
+    return out;
+fail:
+    Py_DECREF(seq);
+    Py_DECREF(out);
+    return NULL;
+}
+
+static PyMethodDef kMethods[] = {
+    {"finite_ptrs", finite_ptrs, METH_O, "finite_ptrs(arrays): data pointers of contiguous float arrays, all elements finite"},
+    {"segments", segments, METH_VARARGS, "segments(pairs, off, cnt, nd): per-layer lists of nd views pairs[o:o+c]"},
+    {"layer_tuples", layer_tuples, METH_VARARGS, "layer_tuples(cls, batch, L): [cls((batch, l)) for l in range(L)]"},
+    {NULL, NULL, 0, NULL},
+};
+
+static struct PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_hostviews", NULL, -1, kMethods};
+
+PyMODINIT_FUNC PyInit__hostviews(void) {
+    import_array();
+    return PyModule_Create(&kModule);
+}

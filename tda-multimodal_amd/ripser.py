@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import ctypes
 import warnings
-from itertools import repeat
 
 import numpy as np
 
@@ -56,11 +55,8 @@ class LayerResult(tuple):
     @property
     def dgms(self) -> list:
         b, l = self
-        if b.dg is None:  # first access: every layer's views in one pass (L x (maxdim+1) slices)
-            P, nd = b.pairs, b.nd
-            o = b.off.ravel()
-            v = [P[x:y] for x, y in zip(o.tolist(), (o + b.cnt.ravel()).tolist())]
-            b.dg = [v[q:q + nd] for q in range(0, len(v), nd)]
+        if b.dg is None:  # first access: every layer's views in one C call (L x (maxdim+1) slices)
+            b.dg = _lib.hostviews().segments(b.pairs, b.off.ravel(), b.cnt.ravel(), b.nd)
         return b.dg[l]
 
     @property
@@ -164,7 +160,7 @@ def _unpack(res_p, want_dist: bool, n_sets: int = 0) -> tuple[list, dict]:
     b.dist64 = _arr(r.dist64, L * N * N, np.float64).reshape(L, N, N) if want_dist and bool(r.dist64) else None
     b.tn = _arr(r.twonn, L, np.float32) if bool(r.twonn) else None
     b.sil = _arr(r.silhouette, L * n_sets, np.float64).reshape(L, n_sets) if bool(r.silhouette) else None
-    out = list(map(LayerResult, zip(repeat(b, L), range(L))))
+    out = _lib.hostviews().layer_tuples(LayerResult, b, L)
     ns = r.n_stages
     stages = [(r.stage_name[i].decode(), float(r.stage_ms[i])) for i in range(ns)] if ns else []
     return out, {"device_ms": r.device_ms, "stages": stages, "cap_reruns": int(r.n_cap_reruns)}
@@ -245,14 +241,16 @@ def _prep_input(X, input_ready: bool):
         raise ValueError("X must be (L, N, D)")
     if X.dtype not in (np.float32, np.float64):
         X = X.astype(np.float64)
-    keep = np.ascontiguousarray(X)
-    if not np.all(np.isfinite(keep)):
-        raise ValueError("Input contains NaN or infinity.")
-    return keep, False, None, keep.dtype == np.float64, 0
+    # the NaN / infinity check runs in _data_ptrs, over every part in one C call
+    return np.ascontiguousarray(X), False, None, X.dtype == np.float64, 0
 
 
-def _data_ptr(keep):
-    return keep.data_ptr() if _is_torch(keep) else keep.ctypes.data
+def _data_ptrs(keeps: list, on_dev: bool) -> list:
+    """Data pointers of one call's prepared inputs; host inputs must be all
+    finite (ripser.py raises "Input contains NaN or infinity.")."""
+    if on_dev:
+        return [k.data_ptr() for k in keeps]
+    return _lib.hostviews().finite_ptrs(keeps)
 
 
 def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bool = False, device: int = 0,
@@ -303,7 +301,7 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
             if k[0].shape != k0[0].shape or k[1:4] != k0[1:4]:
                 raise ValueError("parts must share shape, dtype and device")
         keep_parts = [k[0] for k in kept]
-        ptrs = (ctypes.c_void_p * len(parts))(*[_data_ptr(k) for k in keep_parts])
+        ptrs = (ctypes.c_void_p * len(parts))(*_data_ptrs(keep_parts, k0[1]))
         a.x_parts = ctypes.cast(ptrs, ctypes.c_void_p)
         a.n_parts = len(parts)
         keep = k0[0]
@@ -316,7 +314,7 @@ def ripser_batch(X, maxdim: int = 1, thresh: float = np.inf, distance_matrix: bo
         shape = (Lp * len(parts),) + tuple(keep.shape[1:])
     else:
         keep, on_dev, device_p, dtype_is64, stream = _prep_input(X, input_ready)
-        a.x = _data_ptr(keep)
+        a.x = _data_ptrs([keep], on_dev)[0]
         a.x_on_device = 1 if on_dev else 0
         if on_dev:
             device = device_p
@@ -496,7 +494,9 @@ class SweepPipeline:
         self._n = 0
         self._lock = threading.Lock()
         self._pending = []  # (X, args, future, producer event or None) not yet dispatched
+        self._plen = 0  # layers in _pending
         self._pkey = None
+        self._kw_key = self._args_key(self.kw)
         self._run = run  # the batch call (default ripser_batch; CPU tests pass a stand-in)
 
     @staticmethod
@@ -506,22 +506,28 @@ class SweepPipeline:
                 raise TypeError(f"SweepPipeline picks the {k} itself; do not pass {k}=")
 
     @staticmethod
-    def _key(X, args):
+    def _in_key(X):
         """Sweeps coalesce only with the same FULL shape (the C ABI's parts are
-        equal: L % n_parts == 0), dtype, device and arguments.  Scalar
-        arguments compare by value; anything else (label arrays, lists) by
-        identity -- a repr() of a large numpy array is summarised and two
-        different arrays could compare equal."""
-        dev = (X.device.type, X.device.index) if _is_torch(X) else None
+        equal: L % n_parts == 0), dtype, device and arguments (_args_key)."""
+        return type(X).__module__, (X.device.type, X.device.index) if _is_torch(X) else None, tuple(X.shape), X.dtype
+
+    @staticmethod
+    def _args_key(args):
+        """Scalar arguments compare by value; anything else (label arrays,
+        lists) by identity -- a repr() of a large numpy array is summarised and
+        two different arrays could compare equal."""
 
         def val(v):
             return ("v", v) if v is None or isinstance(v, (bool, int, float, str)) else ("id", id(v))
 
-        return (type(X).__module__, dev, tuple(X.shape), str(X.dtype), tuple(sorted((k, val(v)) for k, v in args.items())))
+        return tuple(sorted((k, val(v)) for k, v in args.items()))
 
     def submit(self, X, **kw):
-        self._check_kw(kw)
-        args = dict(self.kw, **kw)
+        if kw:
+            self._check_kw(kw)
+            args = dict(self.kw, **kw)
+        else:  # the pipeline's own arguments (never mutated: a dispatch copies them)
+            args = self.kw
         if not (_is_torch(X) and X.is_cuda):
             X = np.asarray(X)
         if X.ndim != 3:
@@ -536,11 +542,13 @@ class SweepPipeline:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(X.device))
         with self._lock:
-            key = self._key(X, args)
+            # without call arguments the argument half of the key is the pipeline's own, computed once
+            key = (self._in_key(X), self._args_key(args) if kw else self._kw_key)
             if self._pending and (key != self._pkey or self.coalesce == 1):
                 self._dispatch_locked()
-            lo = sum(int(p[0].shape[0]) for p in self._pending)
-            f = _SweepFuture(self, lo, lo + int(X.shape[0]))
+            lo = self._plen
+            self._plen += int(X.shape[0])
+            f = _SweepFuture(self, lo, self._plen)
             self._pending.append((X, args, f, ev))
             self._pkey = key
             if len(self._pending) >= self.coalesce:
@@ -559,7 +567,7 @@ class SweepPipeline:
                 self._dispatch_locked()
 
     def _dispatch_locked(self):
-        batch, self._pending = self._pending, []
+        batch, self._pending, self._plen = self._pending, [], 0
         run = self._run or ripser_batch
         e = self._n % self.depth  # executor (host thread) of this call
         s = self.slots[e]
