@@ -112,7 +112,10 @@ CALL_KW = {"raw4096": {"twonn": True}, "torus2048_h2": {"thresh": 1.2}}
 # (pipeline.sequential).  sweep48_L4 stays one call at a time: it is the per-call latency record.
 # grid144 (parallel reducer) and raw4096 (distance + H0 + TwoNN) gain from calls in flight but not from wider
 # calls (r04: grid144 5.60 K -> 7.54 K layers/s with 3 in flight, 7.87 K with 4; raw4096 120 K -> 148 K with 4).
-PIPE = {"sweep48": (4, 8), "sweep48_host": (4, 8), "sweep48_L4": (1, 1), "sweep48_L1": (1, 1), "grid144": (4, 1),
+# r06, after the host side moved to C (_hostviews): sweep48_host at 400 steps, 15 interleaved repeats
+# (tools/short_run.py, profiles/r06_steady_shapes_b.txt): 4 x 8 581 K, 5 x 8 579 K, 6 x 6 617 K, 8 x 8 655 K,
+# 6 x 8 667 K; at the driver's 20 steps 6 x 4 and 4 x 5 tie (414 / 409 K, profiles/r06_short_run_20steps.txt).
+PIPE = {"sweep48": (6, 8), "sweep48_host": (6, 8), "sweep48_L4": (1, 1), "sweep48_L1": (1, 1), "grid144": (4, 1),
         "raw4096": (4, 1), "torus1024x32": (1, 1)}  # workload -> (depth, coalesce); (1, 1): one call at a time (env A/B only)
 def pipe_shape(name: str, steps: int) -> tuple:
     """(depth, coalesce) of a workload's timed loop: its PIPE row, with fewer

@@ -1842,7 +1842,9 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         if (int rc = enqueue()) return rc;
     }
     const auto h1 = hclk::now();
-    HIPC(hipStreamSynchronize(s));  // (an event sync or a busy-polled end event measured the same, r02)
+    // (an event sync or a busy-polled end event measured the same for one call at a time, r02; and
+    // for six pipelined slots, hipStreamQuery polled in a loop: 697-701 vs 540-727 K layers/s, r06)
+    HIPC(hipStreamSynchronize(s));
     const auto h2 = hclk::now();
 
     int errs = 0;

@@ -5,7 +5,7 @@ one wave of calls, so the rate is one call's latency, not the pipeline's
 steady state.  This times bench._timed_steps (the bench's own timed loop) at
 K steps for several (depth, coalesce) shapes, interleaved, R repeats each.
 
-    python tools/short_run.py [steps] [repeats]
+    python tools/short_run.py [steps] [repeats] [shapes, e.g. 4x5,2x10]
 """
 import importlib
 import json
@@ -26,6 +26,8 @@ def main():
     bench = importlib.import_module("bench")
     Xs = bench.workload_sweeps("sweep48_host")
     shapes = [(4, 5), (2, 10), (1, 10), (5, 4), (3, 7), (7, 3), (8, 3), (6, 4), (1, 16)]
+    if len(sys.argv) > 3:
+        shapes = [tuple(int(v) for v in s.split("x")) for s in sys.argv[3].split(",")]
     rates = {s: [] for s in shapes}
     for r in range(reps):
         for depth, co in shapes:
