@@ -321,7 +321,9 @@ int make_plan(Plan& p, bool force_global, int scale, bool force_big, int no_par)
     p.memset_lo = o;
     p.o_stats = take(L * sizeof(LayerStats));
     p.o_mst = take(L * p.mst_words * 4);
-    p.piv2_sparse = p.maxdim >= 2 && L * p.piv_words[2] * 4 >= (2ull << 30) && !test_env_is("TDA_PIV2_SPARSE", "0");
+    // (TDA_PIV2_SPARSE=1 forces the sparse-clear bitmap at any size: the stale-bit tests at N = 300)
+    p.piv2_sparse = p.maxdim >= 2 && ((L * p.piv_words[2] * 4 >= (2ull << 30) && !test_env_is("TDA_PIV2_SPARSE", "0")) ||
+                                      test_env_is("TDA_PIV2_SPARSE", "1"));
     for (int d = 1; d <= p.maxdim; ++d)
         if (!(d == 2 && p.piv2_sparse)) p.o_piv[d] = take(L * p.piv_words[d] * 4);
     p.o_rowmax = take(L * N * 4);
@@ -1147,7 +1149,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     const float capf = (no_cap || h2_serial || !(std::isinf(a.thresh) || a.thresh == 3.402823466e+38f)) ? 0.0f : par_capf();
     gk.capf = capf;
     gk.variant = (p.dense ? 1 : 0) | (p.big ? 2 : 0) | (p.fast ? 4 : 0) | (p.lds_mode ? 8 : 0) | (p.cmode << 4) | (p.par ? 1 << 8 : 0) | (dist_mfma ? 1 << 9 : 0) |
-                 (p.wide ? 1 << 10 : 0) | (p.want64 ? 1 << 11 : 0);
+                 (p.wide ? 1 << 10 : 0) | (p.want64 ? 1 << 11 : 0) | (p.par2 ? 1 << 12 : 0) | (p.piv2_sparse ? 1 << 13 : 0);
     gk.thresh = a.thresh;
     gk.n_label_sets = nls;
     gk.sil_K = sil_K;  // baked into the k_silhouette launch (argument K and its LDS size)
@@ -1398,11 +1400,22 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         const size_t alds = 16 + (dl ? (size_t)n * n * 4 : 0);
         // N <= 64: the small-N pass (32-bit decode, 4 vertices per LDS read); TDA_APP_SMALL=0 -> k_apparent
         if (n <= 64 && dl && !test_env_is("TDA_APP_SMALL", "0")) {
-            const size_t slds = 16 + (size_t)n * ((n + 3) & ~3) * 4;
+            // the pivot bitmap copied in LDS when it fits and a block's simplices outnumber a quarter
+            // of its words (every block flushes the whole copy): r06, 160 layers per call,
+            // apparent<1> 24.7 -> 19.3 us, apparent<2> 73.7 -> 57.0 us; at 32 layers per call (540
+            // triangles per block) the flushes cost more than the atomics saved: call 0.171 -> 0.177 ms.
+            // TDA_APP_PIV_LDS=0 / 1: never / always.
+            const uint64_t per_block = (p.ncand[d] + gx - 1) / gx;
+            const bool pl_fit = db[d].piv_words * 4 <= kSmallPivLdsMax;
+            const bool pl_on = test_env_is("TDA_APP_PIV_LDS", "1") ? pl_fit
+                               : test_env_is("TDA_APP_PIV_LDS", "0") ? false
+                                                                    : pl_fit && per_block * 4 >= db[d].piv_words;
+            const uint32_t pl_words = pl_on ? (uint32_t)db[d].piv_words : 0u;
+            const size_t slds = 16 + small_piv_offset(n) + 4ull * pl_words;
             if (d == 1)
-                hipLaunchKernelGGL((k_apparent_small<1>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh);
+                hipLaunchKernelGGL((k_apparent_small<1>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh, pl_words);
             else
-                hipLaunchKernelGGL((k_apparent_small<2>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh);
+                hipLaunchKernelGGL((k_apparent_small<2>), dim3(gx, L), dim3(256), slds, st, dist, n, stats, db[d], rowmax, a.thresh, pl_words);
         } else {
             // L a multiple of 8: a 1-D grid whose blocks take their layers XCD by XCD (app_block)
             const int xl = (L % 8 == 0 && !test_env_is("TDA_APP_XCD", "0")) ? L : 0;

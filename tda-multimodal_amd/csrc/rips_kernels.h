@@ -1639,7 +1639,9 @@ __global__ __launch_bounds__(256) void k_apparent_tile(const float* __restrict__
 // order and tie rule are k_apparent's: vertices descending, a strictly smaller
 // diameter wins (so the largest vertex among equal minima), stop at
 // diam == diam(s) -- no later vertex can beat it, as every cofacet diameter is
-// >= diam(s).
+// >= diam(s).  With pl_words > 0 the apparent pivots collect in an LDS copy of
+// the layer's pivot bitmap, OR-ed into HBM once per non-zero word at the end
+// (r06: one scattered HBM atomic per pair was a quarter of the pass).
 template <int DIM>
 __device__ __forceinline__ void decode_small(uint32_t s, int n, int (&vs)[DIM + 1]) {
     uint32_t rem = s;
@@ -1665,9 +1667,14 @@ __device__ __forceinline__ void decode_small(uint32_t s, int n, int (&vs)[DIM + 
     }
 }
 
+// LDS of k_apparent_small: 16 | the matrix, rows padded to 4 | the pivot bitmap copy (pl_words)
+__host__ __device__ constexpr size_t small_piv_offset(int n) { return (size_t)n * ((n + 3) & ~3) * 4; }
+constexpr uint32_t kSmallPivLdsMax = 32 * 1024;  // largest LDS bitmap copy (bytes): C(48, 4) bits take 24 KB
+
 template <int DIM>
 __global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict__ dist, int n, LayerStats* __restrict__ stats,
-                                                        DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh) {
+                                                        DimBufs b, const uint32_t* __restrict__ rowmax, float user_thresh,
+                                                        uint32_t pl_words) {
     typedef float v4f __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int l = blockIdx.y;
@@ -1687,6 +1694,12 @@ __global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict_
             if (j >= ns) j -= ns, ++i;
         }
     }
+    // the block's apparent pivots collect in an LDS copy of the pivot bitmap when it fits
+    // (pl_words > 0: the launch sized the LDS for it) and reach HBM as one OR per non-zero word
+    // at the end, instead of one scattered HBM atomic per pair
+    TDA_LDS uint32_t* pl = (TDA_LDS uint32_t*)(smem + 16 + small_piv_offset(n));
+    if (pl_words)
+        for (uint32_t w = threadIdx.x; w < pl_words; w += blockDim.x) pl[w] = 0u;
     __syncthreads();
     LayerStats* st = stats + l;
     const uint32_t* cleared = b.cleared ? b.cleared + (size_t)l * b.cleared_words : nullptr;
@@ -1764,7 +1777,10 @@ __global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict_
                     if (app) {
                         kind = 1;
                         const uint64_t tix = cofacet_index<DIM>(vs, bv);
-                        matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
+                        if (pl_words)
+                            __hip_atomic_fetch_or(pl + (tix >> 5), 1u << (tix & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else
+                            matomic_or<false>(&piv[tix >> 5], 1u << (tix & 31));  // no return: fire and forget
                         acc_cs += pair_hash(s, tix);
                         acc_app += 1;
                     }
@@ -1786,6 +1802,13 @@ __global__ __launch_bounds__(256) void k_apparent_small(const float* __restrict_
                 else
                     atomicOr(&st->err, ERR_RESID_CAP);
             }
+        }
+    }
+    if (pl_words) {
+        __syncthreads();
+        for (uint32_t w = threadIdx.x; w < pl_words; w += blockDim.x) {
+            const uint32_t v = pl[w];
+            if (v) matomic_or<false>(&piv[w], v);
         }
     }
     acc_cs = wave_sum_u64(acc_cs);

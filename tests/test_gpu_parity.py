@@ -99,6 +99,20 @@ def test_sweep48_maxdim2_vs_oracle(gpu, oracle, monkeypatch, chain):
         assert_same(res[l], orc[l], 2, f"layer{l}")
 
 
+@pytest.mark.parametrize("piv_lds", ["0", "1"])
+def test_small_apparent_pivot_bitmap_lds_vs_oracle(gpu, oracle, monkeypatch, piv_lds):
+    """k_apparent_small's pivot bits through the LDS copy of the bitmap (flushed
+    once per non-zero word) and through one HBM atomic per pair, forced both
+    ways (TDA_APP_PIV_LDS), H0-H2 on 32 layers of the sweep and on 4 layers of
+    N = 64 (whose H2 bitmap does not fit the copy: the atomics either way)."""
+    monkeypatch.setenv("TDA_APP_PIV_LDS", piv_lds)
+    for X in (gpu.synthetic.sweep48(32, 3), np.stack([gpu.synthetic.torus(64, seed=s) for s in range(4)])):
+        res = gpu.ripser_batch(X, maxdim=2)
+        orc = oracle.rips_batch_f32(X, 2)
+        for l in range(X.shape[0]):
+            assert_same(res[l], orc[l], 2, f"N={X.shape[1]} layer{l} piv_lds={piv_lds}")
+
+
 @pytest.mark.parametrize("reduce_kernel", ["auto", "wave", "big"])
 def test_grid144_maxdim2_vs_oracle(gpu, oracle, monkeypatch, reduce_kernel):
     """C5 layers; both serial-reduction kernels (one wave per layer with
@@ -457,6 +471,23 @@ def test_h2_sparse_pivot_bitmap_reused_across_calls(gpu, monkeypatch):
     for name in ("torus2048_t12", "torus2048_t16", "torus2048_t12"):
         res = gpu.ripser_batch(z[f"{name}__X"], maxdim=2, thresh=float(z[f"{name}__user_thresh"]))
         assert_same_golden(res[0], z, name, 0, 2)
+
+
+@pytest.mark.parametrize("par2", ["1", "0"])
+def test_h2_sparse_pivot_bitmap_serial_h2_reused(gpu, oracle, monkeypatch, par2):
+    """The sparse-clear H2 pivot bitmap forced at N = 300 (TDA_PIV2_SPARSE=1),
+    three calls on one workspace (torus A, torus B, torus A), each against the
+    oracle -- with H2 on the parallel reducer and (TDA_PAR2=0) on the serial
+    radix heap, whose residual-pivot bits k_clear_words does not know: the
+    call after it must start from a full memset."""
+    monkeypatch.setenv("TDA_PIV2_SPARSE", "1")
+    monkeypatch.setenv("TDA_PAR2", par2)
+    monkeypatch.setenv("TDA_PAR_STRICT", "1")
+    clouds = [gpu.synthetic.torus(300, seed=s) for s in (0, 1)]
+    refs = [oracle.rips(X, maxdim=2) for X in clouds]
+    for k in (0, 1, 0):
+        res = gpu.ripser_batch(clouds[k][None], maxdim=2)[0]
+        assert_same(res, refs[k], 2, f"torus300 seed {k} par2={par2}")
 
 
 @pytest.mark.parametrize("wide,par2", [("0", "1"), ("1", "1"), ("0", "0"), ("1", "0")])
