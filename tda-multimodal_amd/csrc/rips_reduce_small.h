@@ -87,9 +87,8 @@ struct EdgeRecV {
     bool tie;
     float len;
 };
-__device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 q = ((const TDA_LDS u32x4*)R)[e];
+typedef unsigned int rec_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ EdgeRecV rec_fields(rec_u32x4 q) {
     EdgeRecV v;
     v.M = (uint64_t)q.x | ((uint64_t)q.y << 32);
     v.off = q.z & 0xFFFFu;
@@ -99,6 +98,8 @@ __device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) {
     v.len = __uint_as_float(q.w);
     return v;
 }
+__device__ __forceinline__ EdgeRecV load_rec(const EdgeRec* R, uint32_t e) { return rec_fields(((const TDA_LDS rec_u32x4*)R)[e]); }
+__device__ __forceinline__ EdgeRecV load_rec_glb(const EdgeRec* R, uint32_t e) { return rec_fields(((const TDA_GLB rec_u32x4*)R)[e]); }
 
 struct DenseBufs {
     EdgeRec* recs;      // [L][E]
@@ -126,8 +127,8 @@ struct DenseBufs {
 //                  counting smaller 64-bit keys; its block mask M_e; by rank:
 //                  the block size and the length bits
 //   k_prep_tables  recs / cls / cls2 and the rank tables: inv16[rank] = edge
-//                  | first | tie; FAST and TABLE: inv32[rank] = a | b << 6 |
-//                  w << 12 | first << 18 | tie << 19; FAST: rank_of[triangle]
+//                  | first | tie; FAST: inv32[rank] = a | b << 6 |
+//                  w << 12 | first << 18 | tie << 19 and rank_of[triangle]
 //                  (0xFFFF above thresh); TABLE: cobt[e][v] = rank of
 //                  {a, b, v} from its youngest facet's block
 constexpr int kPrepEdges = 256;  // edges per k_prep_edges mask block (16 per wave)
@@ -374,10 +375,10 @@ __global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restri
         }
         if ((uint32_t)ln < (uint32_t)__popcll(M))
             st_glb(inv, off + ln, (uint16_t)(e | (ln == 0 ? kInvFirst : 0u) | (tie ? kInvTie : 0u)));
-        if (cmode != kChainGeneral && ln < n && ((M >> ln) & 1ull)) {
+        if (cmode == kChainFast && ln < n && ((M >> ln) & 1ull)) {  // (TABLE decodes its rare steps from recs: r06)
             const uint32_t r2 = off + bits_above(M, ln);
             st_glb(inv32, r2, (uint32_t)a | ((uint32_t)b << 6) | ((uint32_t)ln << 12) | ((uint32_t)(r2 == off) << 18) | ((uint32_t)tie << 19));
-            if (cmode == kChainFast) st_glb(ro, tri_id(a, b, ln), (uint16_t)r2);
+            st_glb(ro, tri_id(a, b, ln), (uint16_t)r2);
         }
         if (cmode == kChainTable && ln < n) {
             // lane v: youngest facet e' of {a, b, v} (longest edge, ties ->
@@ -418,7 +419,8 @@ __global__ __launch_bounds__(kPrepTabT) void k_prep_tables(const float* __restri
 //   kChainTable (N <= 48): cobt[e][v] is the coboundary of edge e by rank and
 //     inv16[rank] carries edge | first | tie | residual, so an apparent step is
 //     three dependent LDS reads (bitmap, inv16, cobt) and a ds_xor; the
-//     rare new-pair / tie steps decode through inv32 in global memory.
+//     rare new-pair / tie steps decode the triangle from its youngest facet's
+//     HBM record (r06: no inv32 table -- 69 KB of writes per 48-point layer).
 //   kChainFast (N <= ~51): rank_of[triangle] + inv32 in LDS.
 //   kChainGeneral: edge records (youngest facet, block mask) + inv16.
 // LDS: [16][D][recs E | rank_of | cobt][inv16 | inv32][W 64K][res 64K][piv][cols][own].
@@ -440,6 +442,7 @@ struct ChainCtx {
     uint16_t* own;
     const float* Dg;
     const uint32_t* inv32g;
+    const EdgeRec* Rg;  // the layer's edge records in HBM (TABLE: the rare steps' triangle decode)
     uint32_t* res1;
     uint32_t* pool;
     uint64_t pool_words;
@@ -469,6 +472,7 @@ __device__ __forceinline__ void h1_chain_wave(const ChainCtx& c) {
     uint16_t* own = c.own;
     const float* Dg = c.Dg;
     const uint32_t* inv32g = c.inv32g;
+    const EdgeRec* Rg = c.Rg;
     uint32_t* res1 = c.res1;
     LayerStats* st = c.st;
     const int n = c.n, l = c.l, ln = lane_id();
@@ -477,7 +481,7 @@ __device__ __forceinline__ void h1_chain_wave(const ChainCtx& c) {
 #ifdef TDA_PROFILE
     const uint64_t t_entry = c.t_entry;
 #endif
-    (void)Dl, (void)R, (void)rof, (void)cobt, (void)inv32, (void)res, (void)Dg, (void)inv32g, (void)l;
+    (void)Dl, (void)R, (void)rof, (void)cobt, (void)inv32, (void)res, (void)Dg, (void)inv32g, (void)Rg, (void)l;
     const float r = st->thresh;
     Pair* P = c.P;
     uint32_t* pool = c.pool;
@@ -597,11 +601,16 @@ __device__ __forceinline__ void h1_chain_wave(const ChainCtx& c) {
             a = q.a;
             b2 = q.b;
             w = kth_highest(q.M, rk - q.off);
-        } else {
-            const uint32_t q = FAST ? ld_lds(inv32, rk) : ld_glb(inv32g, rk);
+        } else if constexpr (FAST) {
+            const uint32_t q = ld_lds(inv32, rk);
             a = (int)(q & 63u);
             b2 = (int)((q >> 6) & 63u);
             w = (int)((q >> 12) & 63u);
+        } else {  // TABLE: the youngest facet from inv16, its block from the HBM record (no inv32 table)
+            const EdgeRecV q = load_rec_glb(Rg, ld_lds(inv, rk) & kInvEdge);
+            a = q.a;
+            b2 = q.b;
+            w = kth_highest(q.M, rk - q.off);
         }
     };
 
@@ -934,6 +943,7 @@ __global__ __launch_bounds__(kChainT) void k_h1_chain(const float* __restrict__ 
     c.own = own;
     c.Dg = Dg;
     c.inv32g = inv32g;
+    c.Rg = db.recs + (size_t)l * db.E;
     c.res1 = res1;
     c.pool = (uint32_t*)(rb.rpool + (size_t)l * rb.rpool_cap);
     c.pool_words = 2ull * rb.rpool_cap;
