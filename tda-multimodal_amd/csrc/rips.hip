@@ -472,6 +472,8 @@ struct Workspace {
     hipEvent_t evin = nullptr;         // caller's stream -> library stream
     char* hin = nullptr;               // pinned staging of host inputs (stable graph source)
     size_t hin_cap = 0;
+    char* hdist = nullptr;             // pinned landing of the distance matrices (want_dist: f32, then f64)
+    size_t hdist_cap = 0;
     void* xin = nullptr;  // gathered device input parts (ABI 6 x_parts)
     size_t xin_cap = 0;
     uint64_t gen = 0;                  // bumped whenever a buffer baked into graphs moves
@@ -1013,6 +1015,16 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     const bool dev_parts = !host_in && nparts > 0;
     const size_t xbytes = input_kind == 2 ? binom((uint64_t)n, 2) * 4
                                           : (size_t)L * n * (input_kind == 1 ? (size_t)n : (size_t)p.D) * esz;
+    // want_dist: the matrices come back by an async copy queued behind the call's work (one
+    // stream sync for both; r06: a blocking hipMemcpy after the sync cost ~20 us per small call)
+    const size_t dbytes = a.want_dist ? (size_t)L * n * n * (4 + (p.want64 ? 8 : 0)) : 0;
+    if (dbytes > w.hdist_cap) {
+        if (w.hdist) HIPC(hipHostFree(w.hdist));
+        w.hdist = nullptr;
+        w.hdist_cap = 0;
+        HIPC(hipHostMalloc((void**)&w.hdist, std::max<size_t>(dbytes, 1 << 16), hipHostMallocDefault));
+        w.hdist_cap = std::max<size_t>(dbytes, 1 << 16);
+    }
     if (host_in) {
         if (w.hin_cap < xbytes) {
             drop_graphs(w);
@@ -1854,6 +1866,10 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
     } else {
         if (int rc = enqueue()) return rc;
     }
+    if (a.want_dist) {
+        HIPC(hipMemcpyAsync(w.hdist, dist, sizeof(float) * L * n * n, hipMemcpyDeviceToHost, s));
+        if (p.want64) HIPC(hipMemcpyAsync(w.hdist + sizeof(float) * L * n * n, B + p.o_d64, sizeof(double) * L * n * n, hipMemcpyDeviceToHost, s));
+    }
     const auto h1 = hclk::now();
     // (an event sync or a busy-polled end event measured the same for one call at a time, r02; and
     // for six pipelined slots, hipStreamQuery polled in a loop: 697-701 vs 540-727 K layers/s, r06)
@@ -2130,13 +2146,13 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 }
             }
     }
-    if (a.want_dist) {
+    if (a.want_dist) {  // landed by the async copies behind the call (synchronised above)
         R->dist.resize((size_t)L * n * n);
-        HIPC(hipMemcpy(R->dist.data(), dist, sizeof(float) * L * n * n, hipMemcpyDeviceToHost));
+        std::memcpy(R->dist.data(), w.hdist, sizeof(float) * L * n * n);
     }
     if (p.want64) {
         R->dist64.resize((size_t)L * n * n);
-        HIPC(hipMemcpy(R->dist64.data(), B + p.o_d64, sizeof(double) * L * n * n, hipMemcpyDeviceToHost));
+        std::memcpy(R->dist64.data(), w.hdist + sizeof(float) * L * n * n, sizeof(double) * L * n * n);
     }
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, w.ev0, w.ev1);
