@@ -164,7 +164,76 @@ fail:
     return NULL;
 }
 
+// a C-contiguous view of `base`'s data at byte offset `off` (read-only unless `writeable`)
+static PyObject* view_of(PyArrayObject* base, int type, Py_ssize_t off, int nd, npy_intp* dims, int writeable) {
+    PyArray_Descr* d = PyArray_DescrFromType(type);  // new reference, stolen below
+    PyObject* v = PyArray_NewFromDescr(&PyArray_Type, d, nd, dims, NULL, PyArray_BYTES(base) + off,
+                                       NPY_ARRAY_ALIGNED | (writeable ? NPY_ARRAY_WRITEABLE : 0), NULL);
+    if (!v) return NULL;
+    Py_INCREF(base);
+    if (PyArray_SetBaseObject((PyArrayObject*)v, (PyObject*)base) < 0) {
+        Py_DECREF(v);
+        return NULL;
+    }
+    return v;
+}
+
+// blob_arrays(address, nbytes, L, nd, total) -> (cnt, off, cs, na, nc, nr, nadd, ne, bidx, didx,
+// thr, pairs): one copy of a result blob (include/tda_rips.h: meta[7][L][nd] | num_edges[L] |
+// birth_idx[T], death_idx[T] | thresh[L] f32 (padded to 8 B) | birth[T], death[T] f32) and the
+// read-only views ripser.py's _unpack made of it with a dozen numpy calls, plus the (T, 2) float64
+// pairs every dgms view points into
+static PyObject* blob_arrays(PyObject* self, PyObject* args) {
+    (void)self;
+    unsigned long long addr;
+    Py_ssize_t nbytes, L, nd, T;
+    if (!PyArg_ParseTuple(args, "Knnnn", &addr, &nbytes, &L, &nd, &T)) return NULL;
+    const Py_ssize_t S = L * nd, o_ne = 7 * S, o_idx = o_ne + L, o_thr = o_idx + 2 * T, o_bd = o_thr + (L + 1) / 2;
+    if (L < 0 || nd <= 0 || T < 0 || nbytes != 8 * (o_bd + T) || (!addr && nbytes)) {
+        PyErr_SetString(PyExc_ValueError, "blob_arrays: size does not match the blob layout");
+        return NULL;
+    }
+    npy_intp wd[1] = {(npy_intp)(o_bd + T)};
+    PyArrayObject* w = (PyArrayObject*)PyArray_SimpleNew(1, wd, NPY_INT64);
+    if (!w) return NULL;
+    if (nbytes) memcpy(PyArray_DATA(w), (const void*)(uintptr_t)addr, (size_t)nbytes);
+    npy_intp pdim[2] = {(npy_intp)T, 2};
+    PyArrayObject* pairs = (PyArrayObject*)PyArray_SimpleNew(2, pdim, NPY_FLOAT64);
+    if (!pairs) {
+        Py_DECREF(w);
+        return NULL;
+    }
+    {
+        const float* bd = (const float*)(PyArray_BYTES(w) + 8 * o_bd);
+        double* P = (double*)PyArray_DATA(pairs);
+        for (Py_ssize_t i = 0; i < T; ++i) {
+            P[2 * i] = (double)bd[i];
+            P[2 * i + 1] = (double)bd[T + i];
+        }
+    }
+    npy_intp md[2] = {(npy_intp)L, (npy_intp)nd}, ld[1] = {(npy_intp)L}, td[1] = {(npy_intp)T};
+    PyObject* out[12] = {NULL};
+    for (int k = 0; k < 7; ++k) out[k] = view_of(w, k == 2 ? NPY_UINT64 : NPY_INT64, 8 * k * S, 2, md, 0);
+    out[7] = view_of(w, NPY_INT64, 8 * o_ne, 1, ld, 0);
+    out[8] = view_of(w, NPY_INT64, 8 * o_idx, 1, td, 0);
+    out[9] = view_of(w, NPY_INT64, 8 * (o_idx + T), 1, td, 0);
+    out[10] = view_of(w, NPY_FLOAT32, 8 * o_thr, 1, ld, 0);
+    out[11] = (PyObject*)pairs;
+    Py_DECREF(w);  // the views hold it
+    PyObject* t = PyTuple_New(12);
+    for (int k = 0; k < 12; ++k) {
+        if (!out[k] || !t) {
+            for (int q = 0; q < 12; ++q) Py_XDECREF(out[q]);
+            Py_XDECREF(t);
+            return NULL;
+        }
+    }
+    for (int k = 0; k < 12; ++k) PyTuple_SET_ITEM(t, k, out[k]);
+    return t;
+}
+
 static PyMethodDef kMethods[] = {
+    {"blob_arrays", blob_arrays, METH_VARARGS, "blob_arrays(address, nbytes, L, nd, total): a result blob's arrays, one copy"},
     {"finite_ptrs", finite_ptrs, METH_O, "finite_ptrs(arrays): data pointers of contiguous float arrays, all elements finite"},
     {"segments", segments, METH_VARARGS, "segments(pairs, off, cnt, nd): per-layer lists of nd views pairs[o:o+c]"},
     {"layer_tuples", layer_tuples, METH_VARARGS, "layer_tuples(cls, batch, L): [cls((batch, l)) for l in range(L)]"},

@@ -132,29 +132,13 @@ def _unpack(res_p, want_dist: bool, n_sets: int = 0) -> tuple[list, dict]:
     r = res_p.contents
     L, md, N = r.L, r.maxdim, r.N
     nd = md + 1
-    S = L * nd
     total = r.n_pairs
     b = _Batch()
     b.L, b.nd, b.N = L, nd, N
-    # one copy of the result blob (tda_rips.h): meta | num_edges | idx | thresh | birth, death
-    raw = ctypes.string_at(r.blob, r.blob_bytes)
-    w = np.frombuffer(raw, dtype=np.int64)
-    meta = w[:7 * S].reshape(7, L, nd)
-    b.cnt, b.off = meta[0], meta[1]
-    b.cs = meta[2].view(np.uint64)
-    b.na, b.nc, b.nr, b.nadd = meta[3], meta[4], meta[5], meta[6]
-    o = 7 * S
-    b.ne = w[o:o + L]
-    o += L
-    b.bidx, b.didx = w[o:o + total], w[o + total:o + 2 * total]
-    o += 2 * total
-    b.thr = np.frombuffer(raw, dtype=np.float32, count=L, offset=8 * o)
-    o += (L + 1) // 2
-    bd = np.frombuffer(raw, dtype=np.float32, count=2 * total, offset=8 * o) if total else np.zeros(0, np.float32)
-    pairs = np.empty((total, 2), dtype=np.float64)  # every diagram is a view into it
-    pairs[:, 0] = bd[:total]
-    pairs[:, 1] = bd[total:]
-    b.pairs = pairs
+    # one copy of the result blob (tda_rips.h: meta | num_edges | idx | thresh | birth, death) and
+    # its views, made in one C call; pairs (total, 2) float64: every diagram is a view into it
+    (b.cnt, b.off, b.cs, b.na, b.nc, b.nr, b.nadd, b.ne, b.bidx, b.didx, b.thr,
+     b.pairs) = _lib.hostviews().blob_arrays(r.blob or 0, r.blob_bytes, L, nd, total)
     b.dg = None
     b.dist = _arr(r.dist, L * N * N, np.float32).reshape(L, N, N) if want_dist and bool(r.dist) else None
     b.dist64 = _arr(r.dist64, L * N * N, np.float64).reshape(L, N, N) if want_dist and bool(r.dist64) else None

@@ -93,3 +93,48 @@ def test_sweep_pipeline_keys():
     x32, x64 = np.zeros((2, 4, 3), np.float32), np.zeros((2, 4, 3), np.float64)
     assert SP._in_key(x32) == SP._in_key(np.ones((2, 4, 3), np.float32))
     assert SP._in_key(x32) != SP._in_key(x64) and SP._in_key(x32) != SP._in_key(np.zeros((3, 4, 3), np.float32))
+
+
+def _unpack_reference(raw: bytes, L: int, nd: int, total: int):
+    """The numpy form of the result blob's views (what ripser.py did before blob_arrays)."""
+    S = L * nd
+    w = np.frombuffer(raw, dtype=np.int64)
+    meta = w[:7 * S].reshape(7, L, nd)
+    o = 7 * S
+    ne = w[o:o + L]
+    o += L
+    bidx, didx = w[o:o + total], w[o + total:o + 2 * total]
+    o += 2 * total
+    thr = np.frombuffer(raw, dtype=np.float32, count=L, offset=8 * o)
+    o += (L + 1) // 2
+    bd = np.frombuffer(raw, dtype=np.float32, count=2 * total, offset=8 * o) if total else np.zeros(0, np.float32)
+    pairs = np.empty((total, 2))
+    pairs[:, 0] = bd[:total]
+    pairs[:, 1] = bd[total:]
+    return (meta[0], meta[1], meta[2].view(np.uint64), meta[3], meta[4], meta[5], meta[6], ne, bidx, didx, thr, pairs)
+
+
+@pytest.mark.parametrize("L,nd,total", [(1, 2, 0), (1, 3, 7), (5, 2, 33), (32, 3, 2000), (3, 1, 5)])
+def test_blob_arrays_match_numpy_unpack(hv, L, nd, total):
+    rng = np.random.default_rng(L * 100 + total)
+    words = 7 * L * nd + L + 2 * total + (L + 1) // 2 + total
+    w = rng.integers(-2 ** 62, 2 ** 62, size=words, dtype=np.int64)
+    # float words: finite values, inf deaths and a NaN-free pattern as the library writes them
+    fl = rng.standard_normal(2 * total).astype(np.float32)
+    fl[total:][::5] = np.inf
+    o = 7 * L * nd + L + 2 * total
+    th = np.zeros(2 * ((L + 1) // 2), np.float32)
+    th[:L] = rng.random(L)
+    w[o:o + (L + 1) // 2] = th.view(np.int64)
+    w[o + (L + 1) // 2:] = fl.view(np.int64) if total else w[o + (L + 1) // 2:]
+    raw = w.tobytes()
+    got = hv.blob_arrays(w.ctypes.data, w.nbytes, L, nd, total)
+    ref = _unpack_reference(raw, L, nd, total)
+    assert len(got) == 12
+    for g, r in zip(got, ref):
+        assert g.dtype == r.dtype and g.shape == r.shape and np.array_equal(g, r), (g, r)
+    assert all(not g.flags.writeable for g in got[:11]) and got[11].flags.writeable
+    del w  # the arrays own their copy
+    assert np.array_equal(got[11], ref[11])
+    with pytest.raises(ValueError):
+        hv.blob_arrays(0, 8, L, nd, total)

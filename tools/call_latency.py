@@ -45,5 +45,23 @@ def main():
     pstats.Stats(pr).sort_stats("tottime").print_stats(14)
 
 
+def stages():
+    """Serial stage times of one 36-point layer at maxdim 1 (median of 200 calls)."""
+    import statistics
+    pkg = importlib.import_module("tda-multimodal_amd")
+    X = pkg.synthetic.reference_clouds()
+    acc = {}
+    for i in range(240):
+        _, info = pkg.ripser_batch(X[i % 32][None], maxdim=1, return_time=True, stage_times=True, stage_serial=True)
+        if i >= 40:
+            for k, v in info["stages"]:
+                acc.setdefault(k, []).append(v)
+    print("stages (serial, one 36-point layer, maxdim 1, median ms): " +
+          ", ".join(f"{k} {statistics.median(v):.4f}" for k, v in acc.items()))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[2] == "stages":
+        stages()
+    else:
+        main()
