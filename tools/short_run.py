@@ -28,10 +28,13 @@ def main():
     shapes = [(4, 5), (2, 10), (1, 10), (5, 4), (3, 7), (7, 3), (8, 3), (6, 4), (1, 16)]
     if len(sys.argv) > 3:
         shapes = [tuple(int(v) for v in s.split("x")) for s in sys.argv[3].split(",")]
+    # SHORT_ONE_STREAM=0: every call on its slot's four streams (SweepPipeline's default is one stream
+    # per slot when depth > 1)
+    kw = {"one_stream": False} if os.environ.get("SHORT_ONE_STREAM") == "0" else {}
     rates = {s: [] for s in shapes}
     for r in range(reps):
         for depth, co in shapes:
-            el, _ = bench._timed_steps(pkg, torch, Xs, 2, {}, steps, 5, depth, True, 0, co)
+            el, _ = bench._timed_steps(pkg, torch, Xs, 2, kw, steps, 5, depth, True, 0, co)
             rates[(depth, co)].append(steps * 32 / el)
         print(f"rep {r}: " + " ".join(f"{d}x{c} {rates[(d, c)][-1] / 1e3:.0f}K" for d, c in shapes), flush=True)
     out = {f"{d}x{c}": {"median": statistics.median(v), "mean": statistics.mean(v), "min": min(v), "max": max(v)}
