@@ -6,7 +6,8 @@
 // Python that is L x (maxdim + 1) slices plus L LayerResult tuples, ~0.5 us
 // a layer on the bench host -- a quarter of the host-input headline's time
 // per layer, and all of it under the GIL that the pipeline's worker threads
-// share.  These two functions make the same objects in one call each.
+// share.  The functions below make the same objects in one call each (and
+// the result blob's arrays, and the input check).
 //
 //   segments(pairs, off, cnt, nd) -> [[pairs[o:o+c] for the nd dims] per layer]
 //   layer_tuples(cls, batch, L)   -> [cls((batch, l)) for l in range(L)]
@@ -212,23 +213,28 @@ static PyObject* blob_arrays(PyObject* self, PyObject* args) {
         }
     }
     npy_intp md[2] = {(npy_intp)L, (npy_intp)nd}, ld[1] = {(npy_intp)L}, td[1] = {(npy_intp)T};
-    PyObject* out[12] = {NULL};
-    for (int k = 0; k < 7; ++k) out[k] = view_of(w, k == 2 ? NPY_UINT64 : NPY_INT64, 8 * k * S, 2, md, 0);
-    out[7] = view_of(w, NPY_INT64, 8 * o_ne, 1, ld, 0);
-    out[8] = view_of(w, NPY_INT64, 8 * o_idx, 1, td, 0);
-    out[9] = view_of(w, NPY_INT64, 8 * (o_idx + T), 1, td, 0);
-    out[10] = view_of(w, NPY_FLOAT32, 8 * o_thr, 1, ld, 0);
-    out[11] = (PyObject*)pairs;
-    Py_DECREF(w);  // the views hold it
     PyObject* t = PyTuple_New(12);
-    for (int k = 0; k < 12; ++k) {
-        if (!out[k] || !t) {
-            for (int q = 0; q < 12; ++q) Py_XDECREF(out[q]);
-            Py_XDECREF(t);
+    if (!t) {
+        Py_DECREF(pairs);
+        Py_DECREF(w);
+        return NULL;
+    }
+    PyTuple_SET_ITEM(t, 11, (PyObject*)pairs);
+    // (type, byte offset, rank, dims) of the eleven views: meta[7] (checksums unsigned), num_edges,
+    // birth_idx, death_idx, thresh
+    const int types[11] = {NPY_INT64, NPY_INT64, NPY_UINT64, NPY_INT64, NPY_INT64, NPY_INT64, NPY_INT64,
+                           NPY_INT64, NPY_INT64, NPY_INT64, NPY_FLOAT32};
+    const Py_ssize_t offs[11] = {0, 8 * S, 16 * S, 24 * S, 32 * S, 40 * S, 48 * S, 8 * o_ne, 8 * o_idx, 8 * (o_idx + T), 8 * o_thr};
+    for (int k = 0; k < 11; ++k) {
+        PyObject* v = view_of(w, types[k], offs[k], k < 7 ? 2 : 1, k < 7 ? md : (k == 8 || k == 9) ? td : ld, 0);
+        if (!v) {
+            Py_DECREF(t);  // releases pairs and the views made so far
+            Py_DECREF(w);
             return NULL;
         }
+        PyTuple_SET_ITEM(t, k, v);
     }
-    for (int k = 0; k < 12; ++k) PyTuple_SET_ITEM(t, k, out[k]);
+    Py_DECREF(w);  // the views hold it
     return t;
 }
 
