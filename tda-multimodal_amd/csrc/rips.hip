@@ -1366,7 +1366,7 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
             dnb.eM = (uint64_t*)(B + p.o_eM);
             dnb.necnt = (uint32_t*)(B + p.o_necnt);
             const dim3 pg((unsigned)L, (unsigned)((dnb.E + kPrepEdges - 1) / kPrepEdges + 1));  // + the rank-sort block
-            hipLaunchKernelGGL(k_prep_edges, pg, dim3(kPrepT), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode);
+            hipLaunchKernelGGL(k_prep_edges, pg, dim3(kPrepT), p.prep_lds, s2, dist, n, rowmax, a.thresh, dnb, p.cmode, stats);
             HIPC(hipGetLastError());
             if (int rc = tm2.mark("k_prep_edges")) return rc;
             // blocks per layer: 8 up to 64 layers (sweep48, 32 layers: 27 -> 18 us), 4 above (256 layers:
@@ -1994,6 +1994,11 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
                 mx = w.hstats[l].prof[1][2];
                 mxa = w.hstats[l].prof[1][3] & 0xFFFF;
             }
+        }
+        {
+            const uint64_t* e = w.hstats[0].prof[4];
+            fprintf(stderr, "[tda-prof] k_prep_edges layer 0 (us from block entry): sort block thresh %.2f staged %.2f sorted %.2f end %.2f; mask blocks (max) thresh %.2f staged %.2f end %.2f\n",
+                    e[0] * 0.01, e[1] * 0.01, e[2] * 0.01, e[3] * 0.01, e[4] * 0.01, e[5] * 0.01, e[6] * 0.01);
         }
         {
             const uint64_t* h = w.hstats[0].prof[3];

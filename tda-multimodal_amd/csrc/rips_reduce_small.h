@@ -145,20 +145,30 @@ constexpr int kChainGeneral = 0, kChainFast = 1, kChainTable = 2;
 // edges <= thresh (they sort first; keys are unique, so this equals the count
 // of smaller keys that r03 computed with E x E comparisons in every block).
 // Sort stages with j <= 64 stay inside one wave's 128 keys: register
-// shuffles, no LDS and no block barrier.  k_prep_tables derives the per-rank block sizes and lengths
-// from M_e and the ranks.
+// shuffles, no LDS and no block barrier (TDA_PROFILE, a 36-point layer: the
+// network takes 14 of the kernel's 17 us; r06: counting smaller keys instead,
+// in this block or in every block, was slower or no shorter).  k_prep_tables
+// derives the per-rank block sizes and lengths from M_e and the ranks.
 constexpr int kPrepT = 1024;
 __global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__ dist, int n, const uint32_t* __restrict__ rowmax,
-                                                       float user_thresh, DenseBufs db, int cmode) {
+                                                       float user_thresh, DenseBufs db, int cmode, LayerStats* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NW = kPrepT / 64, EPW = kPrepEdges / NW;  // waves, edges per wave
     const int l = blockIdx.x, t = threadIdx.x, ln = t & 63, wv = t >> 6;
+#ifdef TDA_PROFILE  // wall-clock ticks (100 MHz) from the block's entry: the sort block [0..3], the mask blocks' max [4..6]
+    const uint64_t pe0 = wall_clock64();
+#define PE_STAMP(i) do { if (t == 0) atomicMax((unsigned long long*)&stats[l].prof[4][i], (unsigned long long)(wall_clock64() - pe0)); } while (0)
+#else
+#define PE_STAMP(i) (void)stats
+#endif
     const int E = n * (n - 1) / 2;
     const int nb = (E + kPrepEdges - 1) / kPrepEdges;
     const float r = block_thresh(rowmax + (size_t)l * n, n, user_thresh, (uint32_t*)smem);
+    PE_STAMP(blockIdx.y == 0 ? 0 : 4);
     float* D = (float*)(smem + 16);
     stage_to_lds(D, dist + (size_t)l * n * n, 4ull * n * n, t, kPrepT);
     __syncthreads();
+    PE_STAMP(blockIdx.y == 0 ? 1 : 5);
     if (blockIdx.y == 0) {  // ranks (y = 0: dispatched first, the long pole overlaps the mask blocks)
         TDA_LDS uint64_t* keys = (TDA_LDS uint64_t*)(D + ((n * n + 3) & ~3));  // [P]
         int P = 2;
@@ -204,6 +214,7 @@ __global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__
             keys[i0 + 1] = x1;
         }
         __syncthreads();
+        PE_STAMP(2);
         uint32_t* ep = db.epos + (size_t)l * db.E;
         for (int q = t; q < E; q += kPrepT) {
             const uint64_t k = keys[q];
@@ -212,6 +223,7 @@ __global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__
             // edges <= thresh sort first: the last of them writes their count
             if (in && (q + 1 == E || !(__uint_as_float((uint32_t)(keys[q + 1] >> 32)) <= r))) st_glb(db.necnt, (size_t)l, (uint32_t)(q + 1));
         }
+        PE_STAMP(3);
         return;
     }
     const int mb = blockIdx.y - 1;  // mask block 0 .. nb-1
@@ -249,6 +261,8 @@ __global__ __launch_bounds__(kPrepT) void k_prep_edges(const float* __restrict__
             if (ln == 0 && e < E) st_glb(db.eM + (size_t)l * db.E, (size_t)e, m);
         }
     }
+    PE_STAMP(6);
+#undef PE_STAMP
 }
 
 // tables: kPrepTabBlocks blocks of 1024 threads per layer.  Every block
