@@ -11,7 +11,7 @@ or a random finite one, as batches of 1 to 8 layers through ripser_batch
 indices, pair counts and checksums against the CPU oracle (oracle/).  Prints one line per batch and a summary; exits 1 on the first
 mismatch.
 
-    python tools/parity_sweep.py [batches] [seed] [nmax]
+    python tools/parity_sweep.py [batches] [seed] [nmax] [md2max]
 """
 import importlib
 import json
@@ -33,10 +33,10 @@ def _oracle_layer(args):
     return oracle.rips(X, maxdim=md, thresh=thresh)
 
 
-def draw(rng, nmax=260):
+def draw(rng, nmax=260, md2max=140):
     kind = rng.choice(["gauss", "lattice", "dups", "clusters", "circle"])
     n = int(rng.integers(2, nmax + 1))
-    md = 2 if n <= 140 and rng.random() < 0.6 else 1
+    md = 2 if n <= md2max and rng.random() < 0.6 else 1
     D = int(rng.choice([1, 2, 3, 8])) if kind in ("gauss", "dups") else (2 if kind == "circle" else 3)
     L = int(rng.integers(1, 9))
     X = np.empty((L, n, D), np.float32)
@@ -62,6 +62,7 @@ def main():
     batches = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 2026
     nmax = int(sys.argv[3]) if len(sys.argv) > 3 else 260
+    md2max = int(sys.argv[4]) if len(sys.argv) > 4 else 140
     import torch
 
     pkg = importlib.import_module("tda-multimodal_amd")
@@ -69,7 +70,7 @@ def main():
     stats = {"batches": 0, "layers": 0, "pairs": 0, "by_kind": {}}
     t0 = time.time()
     for b in range(batches):
-        kind, X, md, thresh = draw(rng, nmax)
+        kind, X, md, thresh = draw(rng, nmax, md2max)
         Xin = torch.from_numpy(X).to("cuda:0") if b % 2 else X
         res = pkg.ripser_batch(Xin, maxdim=md, thresh=thresh)
         refs = [_oracle_layer((X[l], md, thresh)) for l in range(X.shape[0])]
