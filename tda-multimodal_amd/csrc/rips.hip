@@ -6,7 +6,11 @@
 // debug_tda_pipeline.py:92-150) with ~8 + 3*maxdim kernel launches on one
 // stream and a single host synchronisation at the end.
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
 #include <link.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -17,6 +21,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -31,6 +36,29 @@ using namespace tda;
 namespace {
 
 thread_local std::string g_err;
+
+// TDA_SEGV_TRACE=1 (diagnostics): a host segfault prints the faulting thread's native frames
+// (backtrace_symbols_fd: module + offset) before the default action
+void segv_trace(int sig, siginfo_t* si, void*) {
+    void* fr[64];
+    const int nf = backtrace(fr, 64);
+    char msg[128];
+    const int m = snprintf(msg, sizeof msg, "[tda-segv] signal %d, address %p, thread %ld\n", sig, si ? si->si_addr : nullptr,
+                           (long)syscall(SYS_gettid));
+    if (m > 0) (void)!write(2, msg, (size_t)m);
+    backtrace_symbols_fd(fr, nf, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+__attribute__((constructor)) void install_segv_trace() {
+    const char* e = getenv("TDA_SEGV_TRACE");
+    if (!e || e[0] != '1') return;
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
+}
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -506,6 +534,7 @@ struct GraphKey {
 struct GraphEntry {
     GraphKey key;
     hipGraphExec_t exec;
+    hipGraph_t graph;  // kept as long as its exec (r06: see the capture below)
 };
 
 // records an event after each stage when stage timing is on
@@ -620,6 +649,11 @@ std::mutex g_ws_mu;
 // while any slot captures: they take this lock too (first call / growth only;
 // replays never take it).
 std::mutex g_capture_mu;
+// Graph launches: replays (and direct launches) share it; a capture with its instantiation and
+// first launch holds it alone.  r06 (tools/concurrency_stress.py: 8 slots, calls of mixed shapes
+// at once): a freshly instantiated graph's first hipGraphLaunch faulted inside the HIP runtime
+// (a null dereference) while other slots replayed theirs; one slot at a time never did.
+std::shared_mutex g_launch_mu;
 std::vector<Workspace*> g_ws;
 
 Workspace* get_ws(int dev, int slot) {
@@ -634,7 +668,10 @@ Workspace* get_ws(int dev, int slot) {
 }
 
 void drop_graphs(Workspace& w) {
-    for (auto& g : w.graphs) (void)hipGraphExecDestroy(g.exec);
+    for (auto& g : w.graphs) {
+        (void)hipGraphExecDestroy(g.exec);
+        (void)hipGraphDestroy(g.graph);
+    }
     w.graphs.clear();
     ++w.gen;
 }
@@ -1836,14 +1873,17 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         w.piv2_dirty = true;  // until this call has cleared the words it set
     }
     if (ge) {
+        std::shared_lock<std::shared_mutex> launch_lock(g_launch_mu);
         HIPC(hipEventRecord(w.ev0, s));
         HIPC(hipGraphLaunch(ge->exec, s));
         HIPC(hipEventRecord(w.ev1, s));
     } else if (capture) {
         // capture + instantiate one graph at a time across the process: concurrent
         // captures from several slot threads crashed the HIP runtime once (r03, host
-        // segfault inside a first call of two slots); replays run concurrently
+        // segfault inside a first call of two slots); replays run concurrently with each
+        // other, but not with a capture and its first launch (g_launch_mu)
         std::lock_guard<std::mutex> cap_lock(g_capture_mu);
+        std::unique_lock<std::shared_mutex> launch_lock(g_launch_mu);
         HIPC(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         const int rc = enqueue();
         hipGraph_t graph = nullptr;
@@ -1855,15 +1895,22 @@ int run_pipeline(const tda_rips_args& a, int input_kind, const void* host_or_dev
         if (ce != hipSuccess) return fail(TDA_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
         GraphEntry e;
         e.key = gk;
+        e.graph = graph;
+        // the captured graph lives as long as its executable instance: destroying it right after
+        // hipGraphInstantiate (legal by the API) faulted in the instance's first hipGraphLaunch
+        // when other slots' threads were calling at the same time (r06, tools/concurrency_stress.py)
         const hipError_t ie = hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (ie != hipSuccess) return fail(TDA_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+        if (ie != hipSuccess) {
+            (void)hipGraphDestroy(graph);
+            return fail(TDA_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+        }
         if (w.graphs.size() >= 16) drop_graphs(w), e.key.gen = w.gen;
         w.graphs.push_back(e);
         HIPC(hipEventRecord(w.ev0, s));
         HIPC(hipGraphLaunch(w.graphs.back().exec, s));
         HIPC(hipEventRecord(w.ev1, s));
     } else {
+        std::shared_lock<std::shared_mutex> launch_lock(g_launch_mu);
         if (int rc = enqueue()) return rc;
     }
     if (a.want_dist) {

@@ -7,7 +7,10 @@ at once, thread k on workspace slot k, host and device input mixed, several
 rounds, so plans of different shapes are captured, grown and replayed side by
 side; every layer's pairs, indices and checksums must equal the oracle's.
 
-    python tools/concurrency_stress.py [batches] [threads] [rounds] [seed]
+    python tools/concurrency_stress.py [batches] [threads] [rounds] [seed] [warm]
+
+warm=1: one call per slot from the main thread before the threads start (a
+cold-start race and a steady-state fault then tell apart).
 """
 import importlib
 import os
@@ -27,6 +30,8 @@ def main():
     threads = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     seed = int(sys.argv[4]) if len(sys.argv) > 4 else 99
+    warm = len(sys.argv) > 5 and sys.argv[5] == "1"
+    verbose = os.environ.get("STRESS_VERBOSE") == "1"
     import parity_sweep
     from oracle import oracle
 
@@ -40,6 +45,10 @@ def main():
     import torch
 
     pkg = importlib.import_module("tda-multimodal_amd")
+    # device inputs are made here, before the threads start (STRESS_TORCH_IN_THREADS=1: in the threads)
+    in_threads = os.environ.get("STRESS_TORCH_IN_THREADS") == "1"
+    dev = [None if in_threads else torch.from_numpy(w[1]).to("cuda:0") for w in work]
+    torch.cuda.synchronize()
     errors = []
     counts = [0] * threads
 
@@ -47,8 +56,12 @@ def main():
         try:
             for r in range(rounds):
                 for b in range(k, batches, threads):
-                    kind, X, md, thresh, refs = work[(b + r * 7) % batches]
-                    Xin = torch.from_numpy(X).to("cuda:0") if (b + r) % 2 else X
+                    q = (b + r * 7) % batches
+                    kind, X, md, thresh, refs = work[q]
+                    Xin = (torch.from_numpy(X).to("cuda:0") if in_threads else dev[q]) if (b + r) % 2 else X
+                    if verbose:
+                        print(f"slot {k} round {r} batch {b}: {kind} N={X.shape[1]} D={X.shape[2]} L={X.shape[0]} maxdim {md} "
+                              f"thresh {thresh} {'device' if (b + r) % 2 else 'host'}", flush=True)
                     res = pkg.ripser_batch(Xin, maxdim=md, thresh=thresh, slot=k)
                     for l, (g, o) in enumerate(zip(res, refs)):
                         for d in range(md + 1):
@@ -62,6 +75,10 @@ def main():
         except Exception as e:  # reported below
             errors.append(f"slot {k}: {type(e).__name__}: {e}")
 
+    if warm:
+        for k in range(threads):
+            pkg.ripser_batch(work[k][1], maxdim=work[k][2], thresh=work[k][3], slot=k)
+        print("warm: one call per slot done", flush=True)
     torch.cuda.synchronize()
     t0 = time.time()
     ts = [threading.Thread(target=run, args=(k,)) for k in range(threads)]
